@@ -1,0 +1,39 @@
+# Top-level build: the HIP E-step library (gfx950), the oracle (C restatement,
+# test infrastructure), and the test-only MATLAB API double + MEX gateway.
+PKG      := clustering-hidden-markov-models-with-variational-bayesian-hierarchical-em_amd
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
+LIBDIR   := $(PKG)/lib
+SRCS     := $(PKG)/csrc/vbhem_kernels.hip $(PKG)/csrc/vbhem_capi.hip
+HDRS     := include/vbhem_estep.h $(PKG)/csrc/vbhem_internal.h
+OBJS     := $(patsubst $(PKG)/csrc/%.hip,$(LIBDIR)/%.o,$(SRCS))
+
+all: lib oracle
+
+lib: $(LIBDIR)/libvbhem_estep.so
+
+$(LIBDIR)/%.o: $(PKG)/csrc/%.hip $(HDRS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -Iinclude -I$(PKG)/csrc -c -o $@ $<
+
+$(LIBDIR)/libvbhem_estep.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle liboracle.so
+
+# test-only: a MATLAB mx/mex API double and the MEX gateway built against it
+mex: tests/mxshim/libmxshim.so $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so
+
+tests/mxshim/libmxshim.so: tests/mxshim/mxshim.c tests/mxshim/mex.h
+	gcc -O2 -fPIC -shared -Itests/mxshim -o $@ $<
+
+$(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so: integration/vbhem_hmm_bwd_fwd_mex.c include/vbhem_estep.h $(LIBDIR)/libvbhem_estep.so tests/mxshim/mex.h
+	gcc -O2 -fPIC -shared -Iinclude -Itests/mxshim -o $@ $< -L$(LIBDIR) -lvbhem_estep -Wl,-rpath,'$$ORIGIN'
+
+clean:
+	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so tests/mxshim/libmxshim.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle mex clean

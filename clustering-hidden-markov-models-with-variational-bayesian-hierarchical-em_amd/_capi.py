@@ -1,0 +1,81 @@
+"""ctypes binding of libvbhem_estep.so (include/vbhem_estep.h).
+
+The library is built in-tree (``make lib`` / ``__graft_entry__.build()``) into
+``<package>/lib/``.  torch is imported first so that the library binds to the
+HIP runtime torch already loaded (both carry SONAME libamdhip64.so.7); device
+buffers are torch tensors and the stream is torch's current stream.
+
+There is no CPU fallback: if the library is missing, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libvbhem_estep.so")
+
+VBHEM_COV_DIAG, VBHEM_COV_FULL = 0, 1
+_c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+
+
+class BaseT(ctypes.Structure):
+    _fields_ = [("N", _c_int), ("SB", _c_int), ("d", _c_int), ("covmode", _c_int),
+                ("nstates", _vp), ("prior", _vp), ("A", _vp), ("centres", _vp), ("covars", _vp)]
+
+
+class ClusterT(ctypes.Structure):
+    _fields_ = [("K", _c_int), ("S", _c_int), ("logA", _vp), ("logPi", _vp), ("m", _vp),
+                ("P", _vp), ("c", _vp)]
+
+
+EXPORTS = {
+    "vbhem_pairs_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int]),
+    "vbhem_estep_pairs": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "vbhem_estep_pairs_host": (_c_int, [_c_int, ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
+                                        _vp, _vp, _vp, _vp, _vp, _vp]),
+    "vbhem_stats_nu": (_c_size, [_c_int, _c_int]),
+    "vbhem_stats_len": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "vbhem_fused_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int]),
+    "vbhem_estep_fused": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "vbhem_last_fallback_count": (_c_int, [_vp, _vp]),
+    "vbhem_last_error": (ctypes.c_char_p, []),
+    "vbhem_version": (ctypes.c_char_p, []),
+}
+
+_LIB = None
+
+
+class VbhemError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the CDLL; raises if the HIP library is absent."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libvbhem_estep.so not found at {LIB_PATH}; build it with `make lib` "
+                "(or __graft_entry__.build()).  There is no CPU fallback.")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = h
+    return _LIB
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().vbhem_last_error().decode(errors="replace")
+        raise VbhemError(f"{what} failed (status {rc}): {msg}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())

@@ -1,0 +1,399 @@
+// vbhem_capi.hip -- C ABI of libvbhem_estep.so (declared in include/vbhem_estep.h).
+//
+// Validates arguments, plans the launch geometry (pairs per block, LDS
+// carve-up), carves the caller's workspace and enqueues the kernels of
+// vbhem_kernels.hip on the caller's stream.  No allocation, no host
+// synchronisation on the device-pointer entry points (graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "vbhem_estep.h"
+#include "vbhem_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char *where) {
+  return fail(VBHEM_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
+constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
+constexpr int kExactThreads = 256;                // fallback kernel threads
+constexpr size_t kGroupBudget = (size_t)2 << 30;  // per-pair buffers per group (fused)
+constexpr int kMaxSlabs = 1024;
+
+inline int odd_up(int x) { return (x % 2 == 0) ? x + 1 : x; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct FbPlan {
+  vbhem::FbArgs a;
+  dim3 block;
+  size_t lds;
+  int PPB;
+};
+
+bool plan_fb(int SB, int d, int covmode, int K, int S, int T, FbPlan &out) {
+  const int NE = S * SB;
+  if (NE > kFbMaxThreads) return false;
+  const int RS = odd_up(SB), AS = odd_up(S), ABS = odd_up(SB);
+  const int np = covmode == VBHEM_COV_FULL ? d * (d + 1) / 2 : d;
+  const int MS = odd_up(d), PS = odd_up(np);
+  double best = -1.0;
+  bool found = false;
+  for (int ppb = 1; ppb <= 32; ++ppb) {
+    const int BJ = std::min(ppb, K);
+    const int BI = ppb / BJ;
+    const int P = BI * BJ;
+    if (P != ppb) continue;
+    const int threads = (P * NE + 63) / 64 * 64;
+    if (threads > kFbMaxThreads) break;
+    size_t off = 0;
+    vbhem::FbArgs a{};
+    a.off_At = (int)off; off += (size_t)BJ * S * AS;
+    a.off_amax = (int)off; off += (size_t)BJ * S;
+    a.off_lpi = (int)off; off += (size_t)BJ * S;
+    a.off_Ab = (int)off; off += (size_t)BI * SB * ABS;
+    a.off_pib = (int)off; off += (size_t)BI * SB;
+    a.off_flag = (int)off; off += (size_t)(P + 1) / 2;
+    a.off_reg = (int)off;
+    size_t k1 = 0;
+    a.off_k1m = (int)k1; k1 += (size_t)BJ * S * MS;
+    a.off_k1P = (int)k1; k1 += (size_t)BJ * S * PS;
+    a.off_k1c = (int)k1; k1 += (size_t)BJ * S;
+    a.off_k1mu = (int)k1; k1 += (size_t)BI * SB * MS;
+    a.off_k1C = (int)k1; k1 += (size_t)BI * SB * PS;
+    const size_t pstride = (size_t)(T - 1) * S * RS + (size_t)(T - 1) * NE + 3 * (size_t)S * RS +
+                           (size_t)S * S + SB;
+    const size_t reg = std::max(k1, (size_t)P * pstride);
+    const size_t lds = (off + reg) * sizeof(double);
+    if (lds > kLdsLimit) continue;
+    const double util = double(P * NE) / threads;
+    const int blocks_per_cu = std::max<int>(1, (int)(kLdsLimit / lds));
+    const int waves = std::min(32, blocks_per_cu * threads / 64);
+    const double score = util * std::min(waves, 16) + 1e-3 * std::min(threads, 256);
+    if (score > best) {
+      best = score;
+      found = true;
+      a.SB = SB; a.d = d; a.covmode = covmode; a.K = K; a.S = S; a.T = T;
+      a.BI = BI; a.BJ = BJ; a.NE = NE; a.RS = RS; a.AS = AS; a.ABS = ABS;
+      a.njb = (K + BJ - 1) / BJ;
+      a.np = np; a.MS = MS; a.PS = PS;
+      a.pair_stride = (int)pstride;
+      out.a = a;
+      out.block = dim3(threads);
+      out.lds = lds;
+      out.PPB = P;
+    }
+  }
+  return found;
+}
+
+size_t exact_stride(int S, int SB, int T) {
+  return (size_t)6 * S * SB + SB + (size_t)S * S * SB * T;
+}
+
+int check_inputs(const vbhem_base_t *b, const vbhem_cluster_t *c, int T, bool need_ptrs = true) {
+  if (!b || !c) return fail(VBHEM_ERR_ARG, "null base or cluster descriptor");
+  if (b->N < 0 || b->SB < 1 || b->d < 1 || c->K < 1 || c->S < 1 || T < 1)
+    return fail(VBHEM_ERR_ARG, "invalid sizes (need N>=0, SB>=1, d>=1, K>=1, S>=1, T>=1)");
+  if (b->covmode != VBHEM_COV_DIAG && b->covmode != VBHEM_COV_FULL)
+    return fail(VBHEM_ERR_ARG, "covmode must be VBHEM_COV_DIAG or VBHEM_COV_FULL");
+  if (need_ptrs && b->N > 0 &&
+      (!b->prior || !b->A || !b->centres || !b->covars || !c->logA || !c->logPi || !c->m ||
+       !c->P || !c->c))
+    return fail(VBHEM_ERR_ARG, "null input array");
+  if ((long long)b->N * c->K > 0x7fffffffLL)
+    return fail(VBHEM_ERR_UNSUPPORTED, "N*K exceeds 2^31-1 pairs per call; shard the bases");
+  return VBHEM_OK;
+}
+
+void fill_inputs(vbhem::FbArgs &a, const vbhem_base_t *b, const vbhem_cluster_t *c) {
+  a.prior = b->prior; a.A = b->A; a.centres = b->centres; a.covars = b->covars;
+  a.logA = c->logA; a.logPi = c->logPi; a.m = c->m; a.P = c->P; a.c = c->c;
+}
+
+// ---- workspace carving -------------------------------------------------------
+struct Carver {
+  char *base;
+  size_t off = 0;
+  explicit Carver(void *p) : base(static_cast<char *>(p)) {}
+  template <class T>
+  T *take(size_t n) {
+    off = align_up(off, 256);
+    T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+struct PairsWs {
+  int *flags;  // [0]=count [1]=total [2..] list
+  double *scratch;
+  double *tnu;
+};
+
+size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, bool need_tnu,
+                   PairsWs &w) {
+  Carver cv(ws);
+  const size_t np = (size_t)b->N * c->K;
+  w.flags = cv.take<int>(2 + np);
+  w.scratch = cv.take<double>(exact_stride(c->S, b->SB, T) * kExactThreads);
+  w.tnu = need_tnu ? cv.take<double>(np * c->S * b->SB) : nullptr;
+  return cv.off + 256;
+}
+
+struct FusedWs {
+  int group;  // bases per group
+  int nslab;
+  int slab_len;
+  int *flags;
+  double *scratch, *nu1, *xi, *tnu, *slabs;
+};
+
+size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, FusedWs &w) {
+  Carver cv(ws);
+  const int K = c->K, S = c->S, SB = b->SB;
+  const size_t per_base = (size_t)K * (S + (size_t)S * S + (size_t)S * SB) * sizeof(double);
+  size_t g = std::max<size_t>(1, kGroupBudget / std::max<size_t>(1, per_base));
+  g = std::min<size_t>(g, (size_t)std::max(1, b->N));
+  w.group = (int)g;
+  w.nslab = std::min<int>(w.group, kMaxSlabs);
+  w.slab_len = (int)vbhem_stats_len(K, S, b->d, b->covmode);
+  w.flags = cv.take<int>(2 + g * K);
+  w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
+  w.nu1 = cv.take<double>(g * K * S);
+  w.xi = cv.take<double>(g * K * S * S);
+  w.tnu = cv.take<double>(g * K * S * SB);
+  w.slabs = cv.take<double>((size_t)w.nslab * w.slab_len);
+  return cv.off + 256;
+}
+
+int run_fb(const vbhem::FbArgs &proto, const FbPlan &plan, int i_begin, int i_end, int i_buf0,
+           double *LL, double *nu1, double *xi, double *tnu, int *flags, double *scratch,
+           hipStream_t st) {
+  if (i_end <= i_begin) return VBHEM_OK;
+  vbhem::FbArgs a = proto;
+  a.i_begin = i_begin;
+  a.i_end = i_end;
+  a.i_buf0 = i_buf0;
+  a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
+  a.flag_count = flags;
+  a.flag_list = flags + 2;
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  const int nib = (i_end - i_begin + a.BI - 1) / a.BI;
+  const dim3 grid((unsigned)nib * (unsigned)a.njb);
+  e = vbhem::launch_fb(a, grid, plan.block, plan.lds, st);
+  if (e != hipSuccess) return hip_fail(e, "fb_pairs_kernel");
+  e = vbhem::launch_fb_exact(a, scratch, exact_stride(a.S, a.SB, a.T), kExactThreads, st);
+  if (e != hipSuccess) return hip_fail(e, "fb_exact_kernel");
+  return VBHEM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *vbhem_last_error(void) { return g_err.c_str(); }
+
+const char *vbhem_version(void) { return "vbhem-mi355x 0.1.0 (gfx950)"; }
+
+size_t vbhem_stats_nu(int d, int covmode) {
+  return covmode == VBHEM_COV_FULL ? (size_t)1 + d + (size_t)d * (d + 1) / 2 : (size_t)1 + 2 * d;
+}
+
+size_t vbhem_stats_len(int K, int S, int d, int covmode) {
+  return (size_t)K + (size_t)K * S + (size_t)K * S * S + 2 + (size_t)K * S * vbhem_stats_nu(d, covmode);
+}
+
+size_t vbhem_pairs_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T) {
+  if (check_inputs(base, clus, T, false) != VBHEM_OK) return 0;
+  PairsWs w;
+  return carve_pairs(nullptr, base, clus, T, true, w);
+}
+
+int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
+                      double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
+                      double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
+                      void *stream) {
+  int rc = check_inputs(base, clus, T);
+  if (rc != VBHEM_OK) return rc;
+  if (base->N == 0) return VBHEM_OK;
+  if (!LL_elbo_dev || !sum_nu_1_dev || !emit_pr_dev || !emit_mu_dev || !emit_Mu_dev || !sum_xi_dev)
+    return fail(VBHEM_ERR_ARG, "null output array");
+  FbPlan plan;
+  if (!plan_fb(base->SB, base->d, base->covmode, clus->K, clus->S, T, plan))
+    return fail(VBHEM_ERR_UNSUPPORTED,
+                "no launch geometry fits (S*SB must be <= 512 and the per-pair lattice "
+                "(2*(T-1)+3)*S*SB doubles must fit in 160 KiB of LDS)");
+  PairsWs w;
+  const size_t need = carve_pairs(nullptr, base, clus, T, sum_t_nu_dev == nullptr, w);
+  if (!workspace_dev || workspace_bytes < need)
+    return fail(VBHEM_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  carve_pairs(workspace_dev, base, clus, T, sum_t_nu_dev == nullptr, w);
+  double *tnu = sum_t_nu_dev ? sum_t_nu_dev : w.tnu;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  vbhem::FbArgs proto = plan.a;
+  fill_inputs(proto, base, clus);
+  rc = run_fb(proto, plan, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.flags,
+              w.scratch, st);
+  if (rc != VBHEM_OK) return rc;
+  vbhem::EmitArgs ea{};
+  ea.SB = base->SB; ea.d = base->d; ea.covmode = base->covmode; ea.K = clus->K; ea.S = clus->S;
+  ea.i_begin = 0; ea.i_end = base->N;
+  ea.centres = base->centres; ea.covars = base->covars; ea.tnu = tnu;
+  ea.emit_pr = emit_pr_dev; ea.emit_mu = emit_mu_dev; ea.emit_Mu = emit_Mu_dev;
+  hipError_t e = vbhem::launch_emit(ea, st);
+  if (e != hipSuccess) return hip_fail(e, "pair_emit_kernel");
+  return VBHEM_OK;
+}
+
+size_t vbhem_fused_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T) {
+  if (check_inputs(base, clus, T, false) != VBHEM_OK) return 0;
+  FusedWs w;
+  return carve_fused(nullptr, base, clus, T, w);
+}
+
+int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      const double *tildeN_dev, const double *logOmega_dev, double *stats_dev,
+                      double *hatZ_dev, double *LL_elbo_dev, void *workspace_dev,
+                      size_t workspace_bytes, void *stream) {
+  int rc = check_inputs(base, clus, T);
+  if (rc != VBHEM_OK) return rc;
+  if (!tildeN_dev || !logOmega_dev || !stats_dev || !hatZ_dev || !LL_elbo_dev)
+    return fail(VBHEM_ERR_ARG, "null fused argument");
+  FbPlan plan;
+  if (!plan_fb(base->SB, base->d, base->covmode, clus->K, clus->S, T, plan))
+    return fail(VBHEM_ERR_UNSUPPORTED,
+                "no launch geometry fits (S*SB must be <= 512 and the per-pair lattice "
+                "(2*(T-1)+3)*S*SB doubles must fit in 160 KiB of LDS)");
+  FusedWs w;
+  const size_t need = carve_fused(nullptr, base, clus, T, w);
+  if (!workspace_dev || workspace_bytes < need)
+    return fail(VBHEM_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  carve_fused(workspace_dev, base, clus, T, w);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+
+  // stats kernel geometry
+  const int K = clus->K, S = clus->S, SB = base->SB, d = base->d;
+  vbhem::StatsArgs sa{};
+  sa.K = K; sa.S = S; sa.SB = SB; sa.SBp = (SB + 3) / 4 * 4; sa.d = d; sa.covmode = base->covmode;
+  sa.NU = (int)vbhem_stats_nu(d, base->covmode);
+  sa.AST = odd_up(sa.SBp);
+  const int NT = (sa.NU + 15) / 16;
+  sa.UST = NT * 16;
+  const int R = K * S, MT = (R + 15) / 16;
+  sa.ntiles = MT * NT;
+  sa.slab_len = w.slab_len;
+  sa.centres = base->centres; sa.covars = base->covars; sa.LL = LL_elbo_dev;
+  sa.nu1 = w.nu1; sa.xi = w.xi; sa.tnu = w.tnu; sa.tildeN = tildeN_dev; sa.logOmega = logOmega_dev;
+  sa.hatZ = hatZ_dev; sa.slabs = w.slabs;
+  const size_t slds = ((size_t)R * sa.AST + (size_t)sa.SBp * sa.UST + 2 * (size_t)K + (size_t)K * S +
+                       (size_t)K * S * S + 2) * sizeof(double);
+  if (slds > kLdsLimit)
+    return fail(VBHEM_ERR_UNSUPPORTED, "statistics tile does not fit in LDS (K*S too large)");
+  const int ntg = (sa.ntiles + vbhem::stats_tiles_per_block() - 1) / vbhem::stats_tiles_per_block();
+
+  hipError_t e = hipMemsetAsync(w.slabs, 0, sizeof(double) * (size_t)w.nslab * w.slab_len, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(slabs)");
+  e = hipMemsetAsync(w.flags + 1, 0, sizeof(int), st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flag total)");
+
+  vbhem::FbArgs proto = plan.a;
+  fill_inputs(proto, base, clus);
+  for (int g0 = 0; g0 < base->N; g0 += w.group) {
+    const int g1 = std::min(base->N, g0 + w.group);
+    rc = run_fb(proto, plan, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.flags, w.scratch, st);
+    if (rc != VBHEM_OK) return rc;
+    sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
+    const int nchunk = std::min(w.nslab, g1 - g0);
+    e = vbhem::launch_stats(sa, nchunk, ntg, slds, st);
+    if (e != hipSuccess) return hip_fail(e, "stats_kernel");
+  }
+  e = vbhem::launch_stats_final(w.slabs, w.nslab, w.slab_len, stats_dev, st);
+  if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
+  return VBHEM_OK;
+}
+
+int vbhem_last_fallback_count(void *stream, const void *workspace_dev) {
+  // flags[1] accumulates over groups of the last fused call; flags[0] is the
+  // last group's (== whole call for the pairs path).
+  int v[2] = {0, 0};
+  if (!workspace_dev) return fail(VBHEM_ERR_ARG, "null workspace");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemcpyAsync(v, workspace_dev, sizeof(v), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "vbhem_last_fallback_count");
+  return std::max(v[0], v[1]);
+}
+
+int vbhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_cluster_t *ch, int T,
+                           double *LL_elbo, double *sum_nu_1, double *emit_pr, double *emit_mu,
+                           double *emit_Mu, double *sum_xi) {
+  int rc = check_inputs(bh, ch, T);
+  if (rc != VBHEM_OK) return rc;
+  if (bh->N == 0) return VBHEM_OK;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  const size_t N = bh->N, SB = bh->SB, d = bh->d, K = ch->K, S = ch->S;
+  const size_t dC = bh->covmode == VBHEM_COV_FULL ? d * d : d;
+  const size_t n_in[] = {N * SB, N * SB * SB, N * SB * d, N * SB * dC,
+                         K * S * S, K * S, K * S * d, K * S * dC, K * S};
+  const double *h_in[] = {bh->prior, bh->A, bh->centres, bh->covars,
+                          ch->logA, ch->logPi, ch->m, ch->P, ch->c};
+  const size_t n_out[] = {N * K, N * K * S, N * K * S, N * K * S * d, N * K * S * dC, N * K * S * S};
+  double *h_out[] = {LL_elbo, sum_nu_1, emit_pr, emit_mu, emit_Mu, sum_xi};
+  double *d_in[9] = {nullptr};
+  double *d_out[6] = {nullptr};
+  void *ws = nullptr;
+  rc = VBHEM_OK;
+  for (int k = 0; k < 9 && rc == VBHEM_OK; ++k) {
+    e = hipMalloc(&d_in[k], std::max<size_t>(1, n_in[k]) * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(d_in[k], h_in[k], n_in[k] * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) rc = hip_fail(e, "upload");
+  }
+  for (int k = 0; k < 6 && rc == VBHEM_OK; ++k) {
+    e = hipMalloc(&d_out[k], std::max<size_t>(1, n_out[k]) * sizeof(double));
+    if (e != hipSuccess) rc = hip_fail(e, "hipMalloc(out)");
+  }
+  vbhem_base_t bd = *bh;
+  vbhem_cluster_t cd = *ch;
+  bd.nstates = nullptr;
+  bd.prior = d_in[0]; bd.A = d_in[1]; bd.centres = d_in[2]; bd.covars = d_in[3];
+  cd.logA = d_in[4]; cd.logPi = d_in[5]; cd.m = d_in[6]; cd.P = d_in[7]; cd.c = d_in[8];
+  size_t wsb = 0;
+  if (rc == VBHEM_OK) {
+    wsb = vbhem_pairs_workspace_bytes(&bd, &cd, T);
+    e = hipMalloc(&ws, wsb);
+    if (e != hipSuccess) rc = hip_fail(e, "hipMalloc(workspace)");
+  }
+  if (rc == VBHEM_OK)
+    rc = vbhem_estep_pairs(&bd, &cd, T, d_out[0], d_out[1], d_out[2], d_out[3], d_out[4], d_out[5],
+                           nullptr, ws, wsb, nullptr);
+  if (rc == VBHEM_OK) {
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) rc = hip_fail(e, "kernel execution");
+  }
+  for (int k = 0; k < 6 && rc == VBHEM_OK; ++k) {
+    e = hipMemcpy(h_out[k], d_out[k], n_out[k] * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = hip_fail(e, "download");
+  }
+  for (int k = 0; k < 9; ++k) if (d_in[k]) (void)hipFree(d_in[k]);
+  for (int k = 0; k < 6; ++k) if (d_out[k]) (void)hipFree(d_out[k]);
+  if (ws) (void)hipFree(ws);
+  return rc;
+}
+
+}  // extern "C"

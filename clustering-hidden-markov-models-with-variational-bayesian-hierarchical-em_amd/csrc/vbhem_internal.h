@@ -1,0 +1,53 @@
+// vbhem_internal.h -- kernel argument blocks shared by the kernels and the
+// C-ABI layer (not part of the public interface; see include/vbhem_estep.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace vbhem {
+
+constexpr int kCovDiag = 0;
+constexpr int kCovFull = 1;
+
+// fb_pairs_kernel / fb_exact_kernel arguments.  All offsets are in doubles
+// from the start of dynamic LDS.
+struct FbArgs {
+  int SB, d, covmode, K, S, T;
+  int BI, BJ, NE, RS, AS, ABS, njb;
+  int i_begin, i_end, i_buf0;  // bases processed [i_begin, i_end); buffers row 0 = i_buf0
+  int np, MS, PS;              // packed-covariance count and LDS strides
+  const double *prior, *A, *centres, *covars;
+  const double *logA, *logPi, *m, *P, *c;
+  double *LL, *nu1, *xi, *tnu;
+  int *flag_count, *flag_list;
+  int off_At, off_amax, off_lpi, off_Ab, off_pib, off_flag, off_reg;
+  int off_k1m, off_k1P, off_k1c, off_k1mu, off_k1C;
+  int pair_stride;
+};
+
+struct EmitArgs {
+  int SB, d, covmode, K, S;
+  int i_begin, i_end;
+  const double *centres, *covars, *tnu;
+  double *emit_pr, *emit_mu, *emit_Mu;
+};
+
+struct StatsArgs {
+  int K, S, SB, SBp, d, covmode, NU, AST, UST, ntiles;
+  int i_begin, i_end, i_buf0, slab_len;
+  const double *centres, *covars, *LL, *nu1, *xi, *tnu, *tildeN, *logOmega;
+  double *hatZ, *slabs;
+};
+
+hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
+hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
+                           hipStream_t st);
+hipError_t launch_emit(const EmitArgs &a, hipStream_t st);
+hipError_t launch_stats(const StatsArgs &a, int nchunk, int ntg, size_t lds, hipStream_t st);
+hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
+                              hipStream_t st);
+int stats_tiles_per_block();
+int stats_threads();
+
+}  // namespace vbhem

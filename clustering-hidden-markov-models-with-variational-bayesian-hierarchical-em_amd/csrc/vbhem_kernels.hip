@@ -1,0 +1,759 @@
+// vbhem_kernels.hip -- MI355X (gfx950) kernels for the VBHEM-H3M E-step.
+//
+// Hot path = the per-(base HMM i, cluster HMM j) hierarchical backward/forward
+// recursion of src/vbhem/vbhem_hmm_bwd_fwd_mex.c (K1..K5, mex.c:715-1469),
+// followed by the responsibilities (vbhem_h3m_c_step_fc.m:271-283) and the
+// Z-weighted statistic reduction (vbhem_compute_Statistics.m:33-55).
+//
+// Kernels
+//   fb_pairs_kernel<D>  one chain per wavefront slice: lane = (cluster state a,
+//                       base state b) of one pair; several pairs per block share
+//                       staged base/cluster parameters in LDS.  K1 emission,
+//                       backward recursion with a factorised log-sum-exp, the
+//                       termination, the forward recursion.  fp64 throughout.
+//   fb_exact_kernel     reference-order fallback (stores Theta, S^2*Sb exps per
+//                       step) for pairs whose factorised normaliser left its
+//                       safe range (only with pathological hyperparameters).
+//   pair_emit_kernel    K5 per pair (MEX-equivalent emit_pr/mu/Mu outputs).
+//   stats_kernel        fused responsibilities + gated Z-weighted reduction;
+//                       the (K*S) x (Sb) x (1+d+d(d+1)/2) emission-moment
+//                       contraction runs on v_mfma_f64_16x16x4f64.
+//   stats_final_kernel  deterministic fixed-order sum of per-block slabs.
+//
+// Factorised backward step (exact algebra):
+//   l(rho,sig,b) = logA(rho,sig) + v(sig,b),  v = E + L
+//   exp(l) = A'(rho,sig) * G(sig,b) * exp(amax(rho) + M(b)),
+//     A' = exp(logA - amax(rho)),  G = exp(v - M(b)),  M(b) = max_sig v(sig,b)
+//   s(rho,b)   = M(b) + amax(rho) + log Z(rho,b),  Z = sum_sig A'(rho,sig) G(sig,b)
+//   Theta(rho,sig,b) = A'(rho,sig) G(sig,b) / Z(rho,b)
+// so a step costs S*Sb exps and S*Sb logs instead of the reference's S*S*Sb
+// exps; the forward step needs no transcendental at all.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+
+#include "vbhem_internal.h"
+
+namespace vbhem {
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+constexpr double kLog2Pi = 1.8378770664093454835606594728112353;  // log(2*pi)
+constexpr double kZMin = 1e-200;  // below: fall back to the exact reference order
+
+__device__ __forceinline__ int packed_index(int a, int b, int d) {
+  // upper-triangular (a <= b), row-major
+  return a * d - (a * (a - 1)) / 2 + (b - a);
+}
+
+// ---------------------------------------------------------------------------
+// K1: expected log-likelihood of base state b's Gaussian under cluster state a
+//   E = -1/2 ( d log 2pi + c + sum_{a,b} P_ab (Sigma_ab + x_a x_b) ),  x = mu - m
+// (mex.c:796-843 full, :744-759 diag).  P symmetric (P = v*W, W symmetrised at
+// vbhem_mstep_component.m:62,68); Cs holds Sigma_aa on the diagonal and
+// Sigma_ab + Sigma_ba off it, so an asymmetric Sigma is still exact.
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ double emission_full(int d, const double *__restrict__ mrow,
+                                                const double *__restrict__ Pp, double c,
+                                                const double *__restrict__ mu,
+                                                const double *__restrict__ Cs) {
+  double ell = 0.0;
+  if constexpr (D > 0) {
+    double x[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) x[q] = mu[q] - mrow[q];
+    int k = 0;
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      ell = fma(Pp[k], fma(x[q], x[q], Cs[k]), ell);
+      ++k;
+#pragma unroll
+      for (int r = q + 1; r < D; ++r) {
+        ell = fma(Pp[k], fma(2.0 * x[q], x[r], Cs[k]), ell);
+        ++k;
+      }
+    }
+  } else {
+    int k = 0;
+    for (int q = 0; q < d; ++q) {
+      const double xq = mu[q] - mrow[q];
+      ell = fma(Pp[k], fma(xq, xq, Cs[k]), ell);
+      ++k;
+      for (int r = q + 1; r < d; ++r) {
+        const double xr = mu[r] - mrow[r];
+        ell = fma(Pp[k], fma(2.0 * xq, xr, Cs[k]), ell);
+        ++k;
+      }
+    }
+  }
+  return -0.5 * (d * kLog2Pi + c + ell);
+}
+
+template <int D>
+__device__ __forceinline__ double emission_diag(int d, const double *__restrict__ mrow,
+                                                const double *__restrict__ P, double c,
+                                                const double *__restrict__ mu,
+                                                const double *__restrict__ C) {
+  double ell = 0.0;
+  const int dd = D > 0 ? D : d;
+#pragma unroll
+  for (int q = 0; q < (D > 0 ? D : 1); ++q) {
+    if constexpr (D > 0) {
+      const double x = mu[q] - mrow[q];
+      ell = fma(P[q], fma(x, x, C[q]), ell);
+    }
+  }
+  if constexpr (D == 0) {
+    for (int q = 0; q < dd; ++q) {
+      const double x = mu[q] - mrow[q];
+      ell = fma(P[q], fma(x, x, C[q]), ell);
+    }
+  }
+  return -0.5 * (d * kLog2Pi + c + ell);
+}
+
+// ---------------------------------------------------------------------------
+// fb_pairs_kernel: K1..K4 for BI bases x BJ clusters per block.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x;
+  const int nthr = blockDim.x;
+  const int S = p.S, SB = p.SB, NE = p.NE, RS = p.RS, AS = p.AS, ABS = p.ABS, T = p.T;
+  const int d = D > 0 ? D : p.d;
+  const int blk = blockIdx.x;
+  const int ib = blk / p.njb, jb = blk % p.njb;
+  const int i0 = p.i_begin + ib * p.BI, j0 = jb * p.BJ;
+  const int PPB = p.BI * p.BJ;
+
+  double *At = lds + p.off_At;      // [BJ][S][AS]   A' = exp(logA - rowmax)
+  double *amax = lds + p.off_amax;  // [BJ][S]
+  double *lpi = lds + p.off_lpi;    // [BJ][S]
+  double *Ab = lds + p.off_Ab;      // [BI][SB][ABS]
+  double *pib = lds + p.off_pib;    // [BI][SB]
+  int *pflag = reinterpret_cast<int *>(lds + p.off_flag);  // [PPB]
+  double *reg = lds + p.off_reg;    // union: K1 staging | per-pair scratch
+
+  // ---- stage cluster constants ------------------------------------------
+  for (int x = tid; x < p.BJ * S; x += nthr) {
+    const int bj = x / S, r = x - (x / S) * S, j = j0 + bj;
+    double mx = -INFINITY, lp = 0.0;
+    if (j < p.K) {
+      const double *la = p.logA + ((size_t)j * S + r) * S;
+      mx = la[0];
+      for (int s = 1; s < S; ++s) mx = fmax(mx, la[s]);
+      for (int s = 0; s < S; ++s) At[(bj * S + r) * AS + s] = exp(la[s] - mx);
+      lp = p.logPi[(size_t)j * S + r];
+    } else {
+      for (int s = 0; s < S; ++s) At[(bj * S + r) * AS + s] = 0.0;
+    }
+    amax[x] = mx;
+    lpi[x] = lp;
+  }
+  // ---- stage base transition / prior ------------------------------------
+  for (int x = tid; x < p.BI * SB * SB; x += nthr) {
+    const int bi = x / (SB * SB), rem = x - bi * SB * SB, g = rem / SB, be = rem - g * SB;
+    const int i = i0 + bi;
+    Ab[(bi * SB + g) * ABS + be] = (i < p.i_end) ? p.A[((size_t)i * SB + g) * SB + be] : 0.0;
+  }
+  for (int x = tid; x < p.BI * SB; x += nthr) {
+    const int bi = x / SB, be = x - bi * SB, i = i0 + bi;
+    pib[x] = (i < p.i_end) ? p.prior[(size_t)i * SB + be] : 0.0;
+  }
+  for (int x = tid; x < PPB; x += nthr) pflag[x] = 0;
+  // ---- stage K1 operands (packed) ----------------------------------------
+  double *k1m = reg + p.off_k1m;    // [BJ][S][MS]
+  double *k1P = reg + p.off_k1P;    // [BJ][S][PS]  packed P
+  double *k1c = reg + p.off_k1c;    // [BJ][S]
+  double *k1mu = reg + p.off_k1mu;  // [BI][SB][MS]
+  double *k1C = reg + p.off_k1C;    // [BI][SB][PS] packed Sigma (sym-folded)
+  const int np = p.np, MS = p.MS, PS = p.PS;
+  for (int x = tid; x < p.BJ * S; x += nthr) {
+    const int bj = x / S, s = x - bj * S, j = j0 + bj;
+    const bool ok = j < p.K;
+    for (int q = 0; q < d; ++q) k1m[x * MS + q] = ok ? p.m[((size_t)j * S + s) * d + q] : 0.0;
+    k1c[x] = ok ? p.c[(size_t)j * S + s] : 0.0;
+    if (p.covmode == kCovFull) {
+      const double *Pj = p.P + ((size_t)j * S + s) * d * d;
+      for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b)
+          k1P[x * PS + packed_index(a, b, d)] = ok ? Pj[a * d + b] : 0.0;
+    } else {
+      for (int q = 0; q < d; ++q) k1P[x * PS + q] = ok ? p.P[((size_t)j * S + s) * d + q] : 0.0;
+    }
+  }
+  for (int x = tid; x < p.BI * SB; x += nthr) {
+    const int bi = x / SB, be = x - bi * SB, i = i0 + bi;
+    const bool ok = i < p.i_end;
+    for (int q = 0; q < d; ++q) k1mu[x * MS + q] = ok ? p.centres[((size_t)i * SB + be) * d + q] : 0.0;
+    if (p.covmode == kCovFull) {
+      const double *Ci = p.covars + ((size_t)i * SB + be) * d * d;
+      for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b)
+          k1C[x * PS + packed_index(a, b, d)] =
+              ok ? (a == b ? Ci[a * d + a] : Ci[a * d + b] + Ci[b * d + a]) : 0.0;
+    } else {
+      for (int q = 0; q < d; ++q) k1C[x * PS + q] = ok ? p.covars[((size_t)i * SB + be) * d + q] : 0.0;
+    }
+  }
+  (void)np;
+  __syncthreads();
+
+  // ---- lane role -----------------------------------------------------------
+  const int q = tid / NE;
+  const int e = tid - q * NE;
+  const int a = e / SB;
+  const int b = e - a * SB;
+  const bool lane_ok = q < PPB;
+  const int bi = lane_ok ? q / p.BJ : 0, bj = lane_ok ? q - (q / p.BJ) * p.BJ : 0;
+  const int i = i0 + bi, j = j0 + bj;
+  const bool active = lane_ok && (i < p.i_end) && (j < p.K);
+  const size_t pair = (size_t)i * p.K + j;              // global (LL, flags)
+  const size_t lp = (size_t)(i - p.i_buf0) * p.K + j;   // local (nu1, xi, tnu)
+
+  double E = 0.0;
+  if (lane_ok) {
+    const int cs = bj * S + a, bs = bi * SB + b;
+    if (p.covmode == kCovFull)
+      E = emission_full<D>(d, k1m + cs * MS, k1P + cs * PS, k1c[cs], k1mu + bs * MS, k1C + bs * PS);
+    else
+      E = emission_diag<D>(d, k1m + cs * MS, k1P + cs * PS, k1c[cs], k1mu + bs * MS, k1C + bs * PS);
+  }
+  __syncthreads();  // K1 staging region is reused below
+
+  double *pr = reg + (size_t)(lane_ok ? q : 0) * p.pair_stride;
+  double *Gst = pr;                                   // [(T-1)][S][RS]
+  double *Zi = Gst + (size_t)(T - 1) * S * RS;        // [(T-1)][NE]
+  double *X1 = Zi + (size_t)(T - 1) * NE;             // [2][S][RS]  (ping-pong)
+  double *X2 = X1 + 2 * S * RS;                       // [S][RS]
+  double *H = X2 + S * RS;                            // [S*S]
+  double *Y = H + S * S;                              // [SB]
+  const double *Atj = At + bj * S * AS;
+  const double *amaxj = amax + bj * S;
+  const double *lpij = lpi + bj * S;
+  const double *Abi = Ab + bi * SB * ABS;
+  const double *pibi = pib + bi * SB;
+
+  // ---- K2: backward recursion (mex.c:915-1015) ------------------------------
+  double L = 0.0;
+  bool bad = false;
+  for (int t = T - 1; t >= 1; --t) {
+    double *Gt = Gst + (size_t)(t - 1) * S * RS;
+    const double v = E + L;
+    if (lane_ok) X1[a * RS + b] = v;
+    __syncthreads();
+    double Mb = 0.0;
+    if (lane_ok) {
+      Mb = X1[b];
+      for (int s = 1; s < S; ++s) Mb = fmax(Mb, X1[s * RS + b]);
+      Gt[a * RS + b] = exp(v - Mb);
+    }
+    __syncthreads();
+    if (lane_ok) {
+      const double *arow = Atj + a * AS;
+      double Z = 0.0;
+      for (int s = 0; s < S; ++s) Z = fma(arow[s], Gt[s * RS + b], Z);
+      bad |= !(Z >= kZMin);
+      Zi[(size_t)(t - 1) * NE + e] = 1.0 / Z;
+      X2[a * RS + b] = Mb + amaxj[a] + log(Z);
+    }
+    __syncthreads();
+    if (lane_ok) {
+      // L(rho=a, gamma=b) = sum_beta Ab(b, beta) * s(a, beta)
+      const double *arow = Abi + b * ABS;
+      const double *srow = X2 + a * RS;
+      double Ln = 0.0;
+      for (int be = 0; be < SB; ++be) Ln = fma(arow[be], srow[be], Ln);
+      L = Ln;
+    }
+  }
+
+  // ---- K3: termination (mex.c:1020-1080) ------------------------------------
+  const double v1 = lane_ok ? lpij[a] + E + L : 0.0;
+  if (lane_ok) X1[a * RS + b] = v1;
+  __syncthreads();
+  double M1 = 0.0;
+  if (lane_ok) {
+    M1 = X1[b];
+    for (int s = 1; s < S; ++s) M1 = fmax(M1, X1[s * RS + b]);
+    X2[a * RS + b] = exp(v1 - M1);
+  }
+  __syncthreads();
+  double nu = 0.0;
+  if (lane_ok) {
+    double Zs = 0.0;
+    for (int s = 0; s < S; ++s) Zs += X2[s * RS + b];
+    const double s1 = M1 + log(Zs);
+    nu = pibi[b] * exp(v1 - s1);                // nu_1 = prior .* Theta_1
+    if (a == 0) Y[b] = pibi[b] * s1;            // LL_elbo terms
+  }
+  __syncthreads();
+  double *Xc = X1, *Xn = X1 + S * RS;
+  if (lane_ok) {
+    Xc[a * RS + b] = nu;
+    for (int o = e; o < S * S; o += NE) H[o] = 0.0;
+  }
+  __syncthreads();
+  if (active) {
+    if (e == 0) {
+      double ll = 0.0;
+      for (int be = 0; be < SB; ++be) ll += Y[be];
+      p.LL[pair] = ll;
+    }
+    if (b == 0) {
+      double n1 = 0.0;
+      for (int be = 0; be < SB; ++be) n1 += Xc[a * RS + be];
+      p.nu1[lp * S + a] = n1;
+    }
+  }
+
+  // ---- K4: forward recursion (mex.c:1178-1298) ------------------------------
+  double tnu = nu;
+  for (int t = 1; t < T; ++t) {
+    const double *Gt = Gst + (size_t)(t - 1) * S * RS;
+    if (lane_ok) {
+      // f(rho=a, gamma=b) = sum_beta nu(a, beta) Ab(beta, b);  g = f / Z_t
+      const double *nrow = Xc + a * RS;
+      double f = 0.0;
+      for (int be = 0; be < SB; ++be) f = fma(nrow[be], Abi[be * ABS + b], f);
+      X2[a * RS + b] = f * Zi[(size_t)(t - 1) * NE + e];
+    }
+    __syncthreads();
+    if (lane_ok) {
+      // nu(sig=a, gamma=b) = G_t(a,b) * sum_rho A'(rho,a) g(rho,b)
+      double acc = 0.0;
+      for (int r = 0; r < S; ++r) acc = fma(Atj[r * AS + a], X2[r * RS + b], acc);
+      nu = Gt[a * RS + b] * acc;
+      tnu += nu;
+      // h(rho,sig) += sum_gamma g(rho,gamma) G_t(sig,gamma)
+      for (int o = e; o < S * S; o += NE) {
+        const int ro = o / S, so = o - ro * S;
+        const double *grow = X2 + ro * RS, *Grow = Gt + so * RS;
+        double h = 0.0;
+        for (int be = 0; be < SB; ++be) h = fma(grow[be], Grow[be], h);
+        H[o] += h;
+      }
+      Xn[a * RS + b] = nu;
+    }
+    __syncthreads();
+    double *tmp = Xc;
+    Xc = Xn;
+    Xn = tmp;
+  }
+
+  // ---- outputs ---------------------------------------------------------------
+  if (active) {
+    p.tnu[(lp * S + a) * SB + b] = tnu;
+    for (int o = e; o < S * S; o += NE) {
+      const int ro = o / S, so = o - ro * S;
+      p.xi[lp * S * S + o] = Atj[ro * AS + so] * H[o];
+    }
+    if (bad) pflag[q] = 1;
+  }
+  __syncthreads();
+  if (active && e == 0 && pflag[q]) {
+    const int slot = atomicAdd(p.flag_count, 1);
+    atomicAdd(p.flag_count + 1, 1);
+    p.flag_list[slot] = (int)pair;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fb_exact_kernel: reference-order recursion for flagged pairs (one thread per
+// pair, Theta in global scratch).  Mirrors mex.c:715-1298 step by step.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void fb_exact_kernel(const FbArgs p, double *scratch,
+                                                      size_t scratch_stride) {
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nt = gridDim.x * blockDim.x;
+  const int cnt = *p.flag_count;
+  const int S = p.S, SB = p.SB, d = p.d, T = p.T;
+  double *w = scratch + (size_t)gt * scratch_stride;
+  double *E = w, *L = E + S * SB, *Ln = L + S * SB, *lt = Ln + S * SB, *nu = lt + S * SB,
+         *tn = nu + S * SB, *ls = tn + S * SB, *Th = ls + SB;  // Th [T][S][S][SB]
+  for (int idx = gt; idx < cnt; idx += nt) {
+    const int pair = p.flag_list[idx];
+    const int i = pair / p.K, j = pair - (pair / p.K) * p.K;
+    const size_t lp = (size_t)(i - p.i_buf0) * p.K + j;
+    const double *Ab = p.A + (size_t)i * SB * SB;
+    const double *pb = p.prior + (size_t)i * SB;
+    const double *la = p.logA + (size_t)j * S * S;
+    const double *lpj = p.logPi + (size_t)j * S;
+    for (int s = 0; s < S; ++s)
+      for (int be = 0; be < SB; ++be) {
+        const double *mm = p.m + ((size_t)j * S + s) * d;
+        const double *mu = p.centres + ((size_t)i * SB + be) * d;
+        double ell = d * kLog2Pi + p.c[(size_t)j * S + s];
+        if (p.covmode == kCovFull) {
+          const double *P = p.P + ((size_t)j * S + s) * d * d;
+          const double *C = p.covars + ((size_t)i * SB + be) * d * d;
+          for (int k = 0; k < d * d; ++k) ell += P[k] * C[k];
+          for (int c2 = 0; c2 < d; ++c2) {
+            double col = 0.0;
+            for (int r = 0; r < d; ++r) col += (mu[r] - mm[r]) * P[r * d + c2];
+            ell += col * (mu[c2] - mm[c2]);
+          }
+        } else {
+          const double *P = p.P + ((size_t)j * S + s) * d;
+          const double *C = p.covars + ((size_t)i * SB + be) * d;
+          for (int r = 0; r < d; ++r) {
+            const double x = mu[r] - mm[r];
+            ell += P[r] * C[r];
+            ell += P[r] * (x * x);
+          }
+        }
+        E[s * SB + be] = -0.5 * ell;
+        L[s * SB + be] = 0.0;
+      }
+    for (int t = T - 1; t >= 1; --t) {
+      for (int rho = 0; rho < S; ++rho) {
+        for (int s = 0; s < S; ++s)
+          for (int be = 0; be < SB; ++be) lt[s * SB + be] = la[rho * S + s] + E[s * SB + be] + L[s * SB + be];
+        for (int be = 0; be < SB; ++be) {
+          double mv = lt[be];
+          for (int s = 1; s < S; ++s) mv = fmax(mv, lt[s * SB + be]);
+          double acc = 0.0;
+          for (int s = 0; s < S; ++s) acc += exp(lt[s * SB + be] - mv);
+          ls[be] = mv + log(acc);
+          for (int s = 0; s < S; ++s)
+            Th[(((size_t)t * S + rho) * S + s) * SB + be] = exp(lt[s * SB + be] - ls[be]);
+        }
+        for (int g = 0; g < SB; ++g) {
+          double acc = 0.0;
+          for (int be = 0; be < SB; ++be) acc += Ab[g * SB + be] * ls[be];
+          Ln[rho * SB + g] = acc;
+        }
+      }
+      for (int k = 0; k < S * SB; ++k) L[k] = Ln[k];
+    }
+    double LLv = 0.0;
+    for (int s = 0; s < S; ++s)
+      for (int be = 0; be < SB; ++be) lt[s * SB + be] = lpj[s] + E[s * SB + be] + L[s * SB + be];
+    for (int be = 0; be < SB; ++be) {
+      double mv = lt[be];
+      for (int s = 1; s < S; ++s) mv = fmax(mv, lt[s * SB + be]);
+      double acc = 0.0;
+      for (int s = 0; s < S; ++s) acc += exp(lt[s * SB + be] - mv);
+      const double l1 = mv + log(acc);
+      LLv += pb[be] * l1;
+      for (int s = 0; s < S; ++s) nu[s * SB + be] = pb[be] * exp(lt[s * SB + be] - l1);
+    }
+    p.LL[pair] = LLv;
+    for (int s = 0; s < S; ++s) {
+      double acc = 0.0;
+      for (int be = 0; be < SB; ++be) acc += nu[s * SB + be];
+      p.nu1[lp * S + s] = acc;
+    }
+    for (int k = 0; k < S * SB; ++k) tn[k] = nu[k];
+    double *xi = p.xi + lp * S * S;
+    for (int k = 0; k < S * S; ++k) xi[k] = 0.0;
+    for (int t = 1; t < T; ++t) {
+      double *foo = Ln;
+      for (int rho = 0; rho < S; ++rho)
+        for (int g = 0; g < SB; ++g) {
+          double acc = 0.0;
+          for (int be = 0; be < SB; ++be) acc += nu[rho * SB + be] * Ab[be * SB + g];
+          foo[rho * SB + g] = acc;
+        }
+      for (int s = 0; s < S; ++s) {
+        for (int rho = 0; rho < S; ++rho) {
+          double acc = 0.0;
+          for (int g = 0; g < SB; ++g)
+            acc += foo[rho * SB + g] * Th[(((size_t)t * S + rho) * S + s) * SB + g];
+          xi[rho * S + s] += acc;
+        }
+        for (int g = 0; g < SB; ++g) {
+          double acc = 0.0;
+          for (int rho = 0; rho < S; ++rho)
+            acc += foo[rho * SB + g] * Th[(((size_t)t * S + rho) * S + s) * SB + g];
+          nu[s * SB + g] = acc;
+        }
+      }
+      for (int k = 0; k < S * SB; ++k) tn[k] += nu[k];
+    }
+    for (int k = 0; k < S * SB; ++k) p.tnu[lp * S * SB + k] = tn[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// pair_emit_kernel: K5 per pair (mex.c:1348-1469), one thread per (pair, sigma).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pair_emit_kernel(EmitArgs p) {
+  const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)(p.i_end - p.i_begin) * p.K * p.S;
+  if (x >= total) return;
+  const int S = p.S, SB = p.SB, d = p.d;
+  const size_t pl = x / S;             // local pair index
+  const int s = (int)(x - pl * S);
+  const size_t pair = (size_t)p.i_begin * p.K + pl;
+  const int i = (int)(pair / p.K);
+  const double *tn = p.tnu + (pair * S + s) * SB;
+  const double *mu = p.centres + (size_t)i * SB * d;
+  double pr = 0.0;
+  for (int be = 0; be < SB; ++be) pr += tn[be];
+  p.emit_pr[pair * S + s] = pr;
+  for (int q = 0; q < d; ++q) {
+    double acc = 0.0;
+    for (int be = 0; be < SB; ++be) acc += tn[be] * mu[be * d + q];
+    p.emit_mu[(pair * S + s) * d + q] = acc;
+  }
+  if (p.covmode == kCovFull) {
+    const double *C = p.covars + (size_t)i * SB * d * d;
+    double *out = p.emit_Mu + (pair * S + s) * d * d;
+    for (int q = 0; q < d; ++q)
+      for (int r = 0; r < d; ++r) {
+        double acc = 0.0;
+        for (int be = 0; be < SB; ++be)
+          acc += tn[be] * (mu[be * d + q] * mu[be * d + r] + C[(be * d + q) * d + r]);
+        out[q * d + r] = acc;
+      }
+  } else {
+    const double *C = p.covars + (size_t)i * SB * d;
+    double *out = p.emit_Mu + (pair * S + s) * d;
+    for (int q = 0; q < d; ++q) {
+      double acc = 0.0;
+      for (int be = 0; be < SB; ++be) acc += tn[be] * (mu[be * d + q] * mu[be * d + q] + C[be * d + q]);
+      out[q] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// stats_kernel: responsibilities + gated, Z-weighted reduction over this
+// block's chunk of bases.  Slab (per chunk) += partial sums:
+//   [Nj K | N1 K*S | M K*S*S | Lt1 | Lt7 | U R*NU]     (R = K*S)
+// Tile group tg handles U tiles [tg*kTilesPerBlock, ...); group 0 also does
+// the Nj/N1/M/Lt terms and writes hat_Z.
+// ---------------------------------------------------------------------------
+constexpr int kStatsThreads = 256;
+constexpr int kTilesPerWave = 8;
+constexpr int kTilesPerBlock = kTilesPerWave * (kStatsThreads / 64);
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int chunk = blockIdx.x, tg = blockIdx.y;
+  const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU, R = K * S;
+  const int SBp = p.SBp, AST = p.AST, UST = p.UST;
+  const bool do_small = (tg == 0);
+  // per-block base range (relative to i_begin of this launch)
+  const int nb = p.i_end - p.i_begin;
+  const int per = (nb + gridDim.x - 1) / gridDim.x;
+  const int b0 = p.i_begin + chunk * per;
+  const int b1 = min(p.i_end, b0 + per);
+
+  double *As = lds;                              // [R][AST]   g*Z*tnu
+  double *Us = As + (size_t)R * AST;             // [SBp][UST] base moments
+  double *gz = Us + (size_t)SBp * UST;           // [K]
+  double *accNj = gz + K;                        // [K]
+  double *accN1 = accNj + K;                     // [K*S]
+  double *accM = accN1 + (size_t)K * S;          // [K*S*S]
+  double *accLt = accM + (size_t)K * S * S;      // [2]
+
+  if (do_small) {
+    for (int x = tid; x < K + K * S + K * S * S + 2; x += kStatsThreads) accNj[x] = 0.0;
+  }
+  // zero the padding of As/Us once (k >= SB rows/cols stay zero)
+  for (int x = tid; x < R * AST; x += kStatsThreads) As[x] = 0.0;
+  for (int x = tid; x < SBp * UST; x += kStatsThreads) Us[x] = 0.0;
+
+  double4_t acc[kTilesPerWave];
+#pragma unroll
+  for (int t = 0; t < kTilesPerWave; ++t) acc[t] = (double4_t){0.0, 0.0, 0.0, 0.0};
+  const int MT = (R + 15) / 16;
+  const int tile0 = tg * kTilesPerBlock;
+  __syncthreads();
+
+  for (int i = b0; i < b1; ++i) {
+    // -- responsibilities for base i (wave 0) --------------------------------
+    if (wave == 0) {
+      const double tn = p.tildeN[i];
+      double mx = -INFINITY;
+      for (int j = lane; j < K; j += 64) mx = fmax(mx, tn * (p.logOmega[j] + p.LL[(size_t)i * K + j]));
+      mx = wave_max(mx);
+      double sm = 0.0;
+      for (int j = lane; j < K; j += 64) sm += exp(tn * (p.logOmega[j] + p.LL[(size_t)i * K + j]) - mx);
+      sm = wave_sum(sm);
+      const double lse = mx + log(sm);
+      for (int j = lane; j < K; j += 64) {
+        const double ll = p.LL[(size_t)i * K + j];
+        const double hz = exp(tn * (p.logOmega[j] + ll) - lse) + 1e-50;
+        const double Z = hz * tn;
+        gz[j] = (Z > 1e-8) ? Z : 0.0;
+        if (do_small) {
+          p.hatZ[(size_t)i * K + j] = hz;
+          accNj[j] += Z;
+        }
+      }
+      if (do_small) {
+        double l1 = 0.0, l7 = 0.0;
+        for (int j = lane; j < K; j += 64) {
+          const double ll = p.LL[(size_t)i * K + j];
+          const double hz = exp(tn * (p.logOmega[j] + ll) - lse) + 1e-50;
+          l1 += hz * tn * ll;
+          l7 += hz * log(hz);
+        }
+        l1 = wave_sum(l1);
+        l7 = wave_sum(l7);
+        if (lane == 0) {
+          accLt[0] += l1;
+          accLt[1] += l7;
+        }
+      }
+    }
+    __syncthreads();
+    // -- stage A = gz * tnu (rows r = j*S + s, cols beta) and U --------------
+    const double *tnb = p.tnu + (size_t)(i - p.i_buf0) * K * S * SB;
+    for (int x = tid; x < R * SB; x += kStatsThreads) {
+      const int r = x / SB, be = x - r * SB;
+      As[r * AST + be] = gz[r / S] * tnb[x];
+    }
+    const double *mu = p.centres + (size_t)i * SB * d;
+    for (int x = tid; x < SB * NU; x += kStatsThreads) {
+      const int be = x / NU, col = x - be * NU;
+      double u;
+      if (col == 0) {
+        u = 1.0;
+      } else if (col <= d) {
+        u = mu[be * d + col - 1];
+      } else if (p.covmode == kCovFull) {
+        int k = col - 1 - d, a = 0;
+        while (k >= d - a) { k -= d - a; ++a; }
+        const int b = a + k;
+        u = p.covars[(((size_t)i * SB + be) * d + a) * d + b] + mu[be * d + a] * mu[be * d + b];
+      } else {
+        const int q = col - 1 - d;
+        u = p.covars[((size_t)i * SB + be) * d + q] + mu[be * d + q] * mu[be * d + q];
+      }
+      Us[be * UST + col] = u;
+    }
+    if (do_small) {
+      const double *n1 = p.nu1 + (size_t)(i - p.i_buf0) * K * S;
+      for (int x = tid; x < K * S; x += kStatsThreads) accN1[x] += gz[x / S] * n1[x];
+      const double *xi = p.xi + (size_t)(i - p.i_buf0) * K * S * S;
+      for (int x = tid; x < K * S * S; x += kStatsThreads) accM[x] += gz[x / (S * S)] * xi[x];
+    }
+    __syncthreads();
+    // -- MFMA: acc[tile] += A[rows, 4 betas] x U[4 betas, 16 cols] -------------
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) {
+      const int tile = tile0 + wave + t * (kStatsThreads / 64);
+      if (tile < p.ntiles) {
+        const int mt = tile % MT, nt = tile / MT;
+        const int row = mt * 16 + (lane & 15);
+        const int col = nt * 16 + (lane & 15);
+        for (int ks = 0; ks < SBp; ks += 4) {
+          const int k = ks + (lane >> 4);
+          const double av = (row < R) ? As[row * AST + k] : 0.0;
+          const double bv = Us[k * UST + col];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // -- write slab ------------------------------------------------------------
+  double *slab = p.slabs + (size_t)chunk * p.slab_len;
+  if (do_small) {
+    for (int x = tid; x < K + K * S + K * S * S + 2; x += kStatsThreads) slab[x] += accNj[x];
+  }
+  double *slabU = slab + (size_t)K + (size_t)K * S + (size_t)K * S * S + 2;
+#pragma unroll
+  for (int t = 0; t < kTilesPerWave; ++t) {
+    const int tile = tile0 + wave + t * (kStatsThreads / 64);
+    if (tile < p.ntiles) {
+      const int mt = tile % MT, nt = tile / MT;
+      const int col = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + (lane >> 4) + 4 * r;
+        if (row < R && col < NU) slabU[(size_t)row * NU + col] += acc[t][r];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab,
+                                                          int slab_len, double *out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= slab_len) return;
+  double acc = 0.0;
+  for (int c = 0; c < nslab; ++c) acc += slabs[(size_t)c * slab_len + x];
+  out[x] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+template <int D>
+static hipError_t launch_fb_d(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&fb_pairs_kernel<D>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fb_pairs_kernel<D>, grid, block, lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
+  switch (a.d) {
+    case 1: return launch_fb_d<1>(a, grid, block, lds, st);
+    case 2: return launch_fb_d<2>(a, grid, block, lds, st);
+    case 3: return launch_fb_d<3>(a, grid, block, lds, st);
+    case 4: return launch_fb_d<4>(a, grid, block, lds, st);
+    case 5: return launch_fb_d<5>(a, grid, block, lds, st);
+    case 6: return launch_fb_d<6>(a, grid, block, lds, st);
+    case 8: return launch_fb_d<8>(a, grid, block, lds, st);
+    case 12: return launch_fb_d<12>(a, grid, block, lds, st);
+    case 16: return launch_fb_d<16>(a, grid, block, lds, st);
+    default: return launch_fb_d<0>(a, grid, block, lds, st);
+  }
+}
+
+hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(fb_exact_kernel, dim3((nthreads + 63) / 64), dim3(64), 0, st, a, scratch, stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit(const EmitArgs &a, hipStream_t st) {
+  const size_t total = (size_t)(a.i_end - a.i_begin) * a.K * a.S;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats(const StatsArgs &a, int nchunk, int ntg, size_t lds, hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(stats_kernel, dim3(nchunk, ntg), dim3(kStatsThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + 255) / 256), dim3(256), 0, st, slabs,
+                     nslab, slab_len, out);
+  return hipGetLastError();
+}
+
+int stats_tiles_per_block() { return kTilesPerBlock; }
+int stats_threads() { return kStatsThreads; }
+
+}  // namespace vbhem

@@ -1,0 +1,97 @@
+"""VBHEM-H3M EM loop around the device E-step.
+
+:func:`vbhem_h3m_c_step_fc` mirrors src/vbhem/vbhem_h3m_c_step_fc.m:1-449:
+per iteration the psi prelude (:118-165), the E-step (:168-198) fused with the
+responsibilities (:270-283) and the statistics reduction
+(vbhem_compute_Statistics.m), the lower bound (:296, vbhemh3m_lb.m), the
+convergence test (:311-354) and the M-step (:396-419); then
+form_outputH3M.m.  With ``allreduce`` set, each rank runs the E-step on its
+shard of base HMMs and the packed statistics are summed across ranks once per
+iteration (the only collective); the host math is replicated on every rank.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Callable, List, Optional
+
+import numpy as np
+import torch
+
+from . import host
+from .estep import EStepEngine
+from .h3m import Posterior
+
+
+@dataclasses.dataclass
+class EMResult:
+    post: Posterior                 # h3m_r variational posteriors after the last M-step
+    LogLs: List[float]              # h3m_r.LogLs (ELBO per iteration, before its M-step)
+    LL: float                       # final lower bound (-inf if unstable)
+    iters: int
+    stable: bool
+    hatZ: torch.Tensor              # [N_shard, K] responsibilities of the last E-step
+    L_elbo: torch.Tensor            # [N_shard, K]
+    Nj: np.ndarray                  # [K]
+    syn: Optional[dict]             # Syn_STATS of the last M-step (Nj_rho1, Nj_rho2rho, Nj_rho, ...)
+    point: Optional[dict] = None    # convert_h3mrtoh3mb point estimates
+    label: Optional[torch.Tensor] = None  # argmax_j hat_Z (0-based), form_outputH3M.m:274-275
+
+
+def tilde_n(engine: EStepEngine, Nv: float, total_N: int) -> torch.Tensor:
+    """tilde_N_k = Nv * Kb * omega (step_fc.m:26-30) for the engine's shard;
+    omega is the global normalised weight vector sliced to the shard."""
+    return (float(Nv) * float(total_N)) * engine.base.omega.to(torch.float64)
+
+
+def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
+                        total_N: Optional[int] = None,
+                        allreduce: Optional[Callable[[torch.Tensor], None]] = None,
+                        max_iter: Optional[int] = None) -> EMResult:
+    covmode = engine.base.covmode
+    K, S, d = post.m.shape
+    total_N = engine.N if total_N is None else int(total_N)
+    tN = tilde_n(engine, opt["Nv"], total_N)
+    maxIter = opt["max_iter"] if max_iter is None else max_iter
+    minDiff = opt["minDiff"]
+    post = post.copy()
+    lastL = -np.finfo(float).max
+    it = 0
+    LogLs: List[float] = []
+    syn = None
+    stable = True
+    L = -np.inf
+    Nj = np.zeros(K)
+    while True:
+        consts = host.cluster_constants(post, covmode)
+        logOmega = host.log_omega_tilde(post.alpha)
+        engine.set_clusters(consts)
+        engine.set_log_omega(logOmega)
+        stats = engine.fused(tN)
+        if allreduce is not None:
+            allreduce(stats)
+        st = host.unpack_stats(stats.cpu().numpy(), K, S, d, covmode)
+        Nj = st["Nj"] + 1e-50
+        L = host.lower_bound(st["Lt1"], st["Lt7"], Nj, logOmega, post, consts, opt, covmode)
+        do_break = False
+        if it > 1 and abs((L - lastL) / lastL) <= minDiff:
+            do_break = True
+        if it == maxIter:
+            do_break = True
+        if np.isnan(L):
+            # step_fc.m:338-374: unstable model -> L = -inf, stop before the M-step
+            L = -np.inf
+            stable = False
+            break
+        syn = host.finish_statistics(st, covmode)
+        post = host.mstep(syn, Nj, opt, covmode, post.W0mode)
+        it += 1
+        LogLs.append(L)
+        lastL = L
+        if do_break:
+            break
+    res = EMResult(post=post, LogLs=LogLs, LL=L, iters=it, stable=stable, hatZ=engine.hatZ.clone(),
+                   L_elbo=engine.LL.clone(), Nj=Nj, syn=syn)
+    if stable:
+        res.point = host.convert_to_point(post, covmode)
+        res.label = torch.argmax(res.hatZ, dim=1)
+    return res

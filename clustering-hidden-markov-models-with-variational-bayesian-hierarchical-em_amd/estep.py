@@ -1,0 +1,134 @@
+"""Device-resident E-step engine (one shard of base HMMs on one GPU).
+
+:class:`EStepEngine` owns the HBM copies of the shard's base HMMs, the
+per-iteration cluster-constant buffers, the outputs and the workspace, and
+enqueues the C-ABI entry points of libvbhem_estep.so on torch's current
+stream.  It replaces, per EM iteration, the MEX call of
+src/vbhem/vbhem_h3m_c_step_fc.m:168-198 (``pairs``) or the MEX call plus
+the responsibilities, statistics reduction and ELBO partial sums
+(:270-296, vbhem_compute_Statistics.m) (``fused``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _capi
+from .h3m import COV_FULL, BaseSet
+
+F64 = torch.float64
+
+
+class EStepEngine:
+    def __init__(self, base: BaseSet, K: int, S: int, T: int, device=None):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("EStepEngine runs on a GPU (HIP); there is no CPU path")
+        self.lib = _capi.lib()
+        b = base.to(self.device)
+        self.base = BaseSet(b.nstates.to(torch.int32).contiguous(), b.prior.to(F64).contiguous(),
+                            b.A.to(F64).contiguous(), b.centres.to(F64).contiguous(),
+                            b.covars.to(F64).contiguous(), b.omega.to(F64).contiguous(), b.covmode)
+        self.K, self.S, self.T = int(K), int(S), int(T)
+        N, SB, d = self.base.N, self.base.SB, self.base.d
+        dv = self.device
+        dC = (d, d) if self.base.covmode == COV_FULL else (d,)
+        self.c_logA = torch.zeros((K, S, S), dtype=F64, device=dv)
+        self.c_logPi = torch.zeros((K, S), dtype=F64, device=dv)
+        self.c_m = torch.zeros((K, S, d), dtype=F64, device=dv)
+        self.c_P = torch.zeros((K, S) + dC, dtype=F64, device=dv)
+        self.c_c = torch.zeros((K, S), dtype=F64, device=dv)
+        self.logOmega = torch.zeros((K,), dtype=F64, device=dv)
+        bb = self.base
+        self._bt = _capi.BaseT(N, SB, d, bb.covmode, _capi.ptr(bb.nstates), _capi.ptr(bb.prior),
+                               _capi.ptr(bb.A), _capi.ptr(bb.centres), _capi.ptr(bb.covars))
+        self._ct = _capi.ClusterT(K, S, _capi.ptr(self.c_logA), _capi.ptr(self.c_logPi),
+                                  _capi.ptr(self.c_m), _capi.ptr(self.c_P), _capi.ptr(self.c_c))
+        self.stats_len = int(self.lib.vbhem_stats_len(K, S, d, bb.covmode))
+        self.stats = torch.zeros((self.stats_len,), dtype=F64, device=dv)
+        self.hatZ = torch.zeros((N, K), dtype=F64, device=dv)
+        self.LL = torch.zeros((N, K), dtype=F64, device=dv)
+        self._ws_fused = None
+        self._ws_pairs = None
+
+    # -- inputs -------------------------------------------------------------
+    @property
+    def N(self) -> int:
+        return self.base.N
+
+    def set_clusters(self, consts: dict) -> None:
+        """Upload the iteration's cluster constants (host.cluster_constants)."""
+        for dst, key in ((self.c_logA, "logA"), (self.c_logPi, "logPi"), (self.c_m, "m"),
+                         (self.c_P, "P"), (self.c_c, "c")):
+            src = consts[key]
+            if isinstance(src, np.ndarray):
+                src = torch.from_numpy(np.ascontiguousarray(src, dtype=np.float64))
+            dst.copy_(src.reshape(dst.shape))
+
+    def set_log_omega(self, logOmega) -> None:
+        src = logOmega
+        if isinstance(src, np.ndarray):
+            src = torch.from_numpy(np.ascontiguousarray(src, dtype=np.float64))
+        self.logOmega.copy_(src)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- MEX-equivalent per-pair outputs ------------------------------------
+    def pairs(self, want_tnu: bool = False) -> dict:
+        """LL_elbo, sum_nu_1, emit_pr, emit_mu, emit_Mu, sum_xi (+ sum_t_nu), [N][K][...]."""
+        N, K, S, d, SB = self.N, self.K, self.S, self.base.d, self.base.SB
+        dv = self.device
+        dC = (d, d) if self.base.covmode == COV_FULL else (d,)
+        out = dict(LL_elbo=torch.empty((N, K), dtype=F64, device=dv),
+                   sum_nu_1=torch.empty((N, K, S), dtype=F64, device=dv),
+                   emit_pr=torch.empty((N, K, S), dtype=F64, device=dv),
+                   emit_mu=torch.empty((N, K, S, d), dtype=F64, device=dv),
+                   emit_Mu=torch.empty((N, K, S) + dC, dtype=F64, device=dv),
+                   sum_xi=torch.empty((N, K, S, S), dtype=F64, device=dv))
+        if want_tnu:
+            out["sum_t_nu"] = torch.empty((N, K, S, SB), dtype=F64, device=dv)
+        if self._ws_pairs is None:
+            nb = int(self.lib.vbhem_pairs_workspace_bytes(ctypes.byref(self._bt),
+                                                          ctypes.byref(self._ct), self.T))
+            self._ws_pairs = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dv)
+        rc = self.lib.vbhem_estep_pairs(
+            ctypes.byref(self._bt), ctypes.byref(self._ct), self.T,
+            _capi.ptr(out["LL_elbo"]), _capi.ptr(out["sum_nu_1"]), _capi.ptr(out["emit_pr"]),
+            _capi.ptr(out["emit_mu"]), _capi.ptr(out["emit_Mu"]), _capi.ptr(out["sum_xi"]),
+            _capi.ptr(out.get("sum_t_nu")), _capi.ptr(self._ws_pairs),
+            self._ws_pairs.numel(), self._stream())
+        _capi.check(rc, "vbhem_estep_pairs")
+        return out
+
+    # -- fused E-step --------------------------------------------------------
+    def fused(self, tildeN: torch.Tensor) -> torch.Tensor:
+        """Pairs + responsibilities + gated Z-weighted sums + ELBO partials.
+
+        tildeN: [N] (device, fp64) virtual-sample counts of this shard.
+        Returns the packed statistics vector (device, [stats_len]); hat_Z and
+        L_elbo are left in ``self.hatZ`` / ``self.LL``."""
+        if self._ws_fused is None:
+            nb = int(self.lib.vbhem_fused_workspace_bytes(ctypes.byref(self._bt),
+                                                          ctypes.byref(self._ct), self.T))
+            self._ws_fused = torch.empty((max(nb, 1),), dtype=torch.uint8, device=self.device)
+        rc = self.lib.vbhem_estep_fused(
+            ctypes.byref(self._bt), ctypes.byref(self._ct), self.T, _capi.ptr(tildeN),
+            _capi.ptr(self.logOmega), _capi.ptr(self.stats), _capi.ptr(self.hatZ),
+            _capi.ptr(self.LL), _capi.ptr(self._ws_fused), self._ws_fused.numel(), self._stream())
+        _capi.check(rc, "vbhem_estep_fused")
+        return self.stats
+
+    def fallback_count(self) -> int:
+        """Pairs of the last fused call that needed the exact fallback (syncs)."""
+        ws = self._ws_fused if self._ws_fused is not None else self._ws_pairs
+        if ws is None:
+            return 0
+        n = self.lib.vbhem_last_fallback_count(self._stream(), ctypes.c_void_p(_capi.ptr(ws)))
+        if n < 0:
+            _capi.check(n, "vbhem_last_fallback_count")
+        return int(n)

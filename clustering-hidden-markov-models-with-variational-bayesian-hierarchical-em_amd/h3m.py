@@ -1,0 +1,317 @@
+"""Packed H3M containers, input conversion and synthetic workloads.
+
+* :class:`BaseSet` -- the N base HMMs ``h3m_b`` in the packed, zero-padded
+  layout the device E-step consumes (include/vbhem_estep.h).
+* :class:`Posterior` -- the K cluster HMMs' variational parameters ``h3m_r``
+  (eta, epsilon, lambda, v, m, W per cluster; alpha over clusters).
+* :func:`hmms_to_h3m_hem` -- src/vbhem/hmms_to_h3m_hem.m:1-144.
+* :func:`baseem_init` -- the 'baseem' initialisation of
+  src/vbhem/vbhemhmm_init.m:58-100 with the random draws injected.
+* :func:`synth_workload` -- the synthetic (N, K, S, d) grids of BASELINE.md.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+COV_DIAG, COV_FULL = 0, 1
+
+
+@dataclasses.dataclass
+class BaseSet:
+    """h3m_b, packed: nstates [N], prior [N,SB], A [N,SB,SB] (A[i][from][to]),
+    centres [N,SB,d], covars [N,SB,d,d] (full) | [N,SB,d] (diag), omega [N]."""
+    nstates: torch.Tensor
+    prior: torch.Tensor
+    A: torch.Tensor
+    centres: torch.Tensor
+    covars: torch.Tensor
+    omega: torch.Tensor
+    covmode: int
+
+    @property
+    def N(self) -> int:
+        return int(self.prior.shape[0])
+
+    @property
+    def SB(self) -> int:
+        return int(self.prior.shape[1])
+
+    @property
+    def d(self) -> int:
+        return int(self.centres.shape[2])
+
+    def to(self, device) -> "BaseSet":
+        f = lambda t: t.to(device).contiguous()
+        return BaseSet(f(self.nstates), f(self.prior), f(self.A), f(self.centres), f(self.covars),
+                       f(self.omega), self.covmode)
+
+    def shard(self, lo: int, hi: int) -> "BaseSet":
+        return BaseSet(self.nstates[lo:hi], self.prior[lo:hi], self.A[lo:hi], self.centres[lo:hi],
+                       self.covars[lo:hi], self.omega[lo:hi], self.covmode)
+
+    def numpy(self) -> dict:
+        return dict(nstates=self.nstates.cpu().numpy().astype(np.int32),
+                    prior=self.prior.cpu().numpy(), A=self.A.cpu().numpy(),
+                    centres=self.centres.cpu().numpy(), covars=self.covars.cpu().numpy(),
+                    omega=self.omega.cpu().numpy(), covmode=self.covmode)
+
+    @staticmethod
+    def from_numpy(d: dict) -> "BaseSet":
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64)
+        return BaseSet(torch.as_tensor(np.asarray(d["nstates"], dtype=np.int32)), t(d["prior"]),
+                       t(d["A"]), t(d["centres"]), t(d["covars"]), t(d["omega"]), int(d["covmode"]))
+
+
+@dataclasses.dataclass
+class Posterior:
+    """h3m_r variational parameters (vbhemhmm_init.m:77-99, vbhem_mstep_component.m:42-69):
+    alpha [K]; eta [K,S]; epsilon [K,S,S]; lam [K,S]; v [K,S]; m [K,S,d];
+    W [K,S,d,d] (full) | [K,S,d] (diag)."""
+    alpha: np.ndarray
+    eta: np.ndarray
+    epsilon: np.ndarray
+    lam: np.ndarray
+    v: np.ndarray
+    m: np.ndarray
+    W: np.ndarray
+    W0mode: str = "iid"
+
+    @property
+    def K(self) -> int:
+        return int(self.m.shape[0])
+
+    @property
+    def S(self) -> int:
+        return int(self.m.shape[1])
+
+    def copy(self) -> "Posterior":
+        return Posterior(*(np.array(getattr(self, f.name)) if f.name != "W0mode" else self.W0mode
+                           for f in dataclasses.fields(self)))
+
+    def asdict(self) -> dict:
+        return {f.name: getattr(self, f.name) for f in dataclasses.fields(self)}
+
+
+# ----------------------------------------------------------------------------
+# input conversion (hmms_to_h3m_hem.m)
+# ----------------------------------------------------------------------------
+def hmms_to_h3m_hem(hmms: List[Optional[dict]], covmode: int = COV_FULL,
+                    use_post: bool = True) -> BaseSet:
+    """Convert a list of VB-HMMs (dicts with prior, trans, pdf[{mean,cov}],
+    varpar{alpha,epsilon,beta}) into a packed :class:`BaseSet`.
+
+    use_post=True (the vbhem_h3m_cluster default, :237): prior/A become
+    exp(E[log]) -- sub-stochastic, never renormalised (:42-58) -- and each
+    covariance is inflated by (beta+1)/beta (:82,88).  Empty entries (None)
+    become a one-state dummy with weight 0 (:113-133)."""
+    from scipy.special import digamma
+
+    nin = next(len(h["pdf"][0]["mean"]) for h in hmms if h is not None)
+    N = len(hmms)
+    SB = max(len(h["prior"]) if h is not None else 1 for h in hmms)
+    d = nin
+    ns = np.ones(N, dtype=np.int32)
+    prior = np.zeros((N, SB))
+    A = np.zeros((N, SB, SB))
+    cen = np.zeros((N, SB, d))
+    cov = np.zeros((N, SB, d, d) if covmode == COV_FULL else (N, SB, d))
+    omega = np.ones(N)
+    for j, h in enumerate(hmms):
+        if h is None:
+            prior[j, 0] = 1.0
+            A[j, 0, 0] = 1.0
+            cov[j, 0] = np.eye(d) if covmode == COV_FULL else 1.0
+            omega[j] = 0.0
+            continue
+        S = len(h["prior"])
+        ns[j] = S
+        if use_post:
+            al = np.asarray(h["varpar"]["alpha"], float)
+            ep = np.asarray(h["varpar"]["epsilon"], float)
+            prior[j, :S] = np.exp(digamma(al) - digamma(al.sum()))
+            A[j, :S, :S] = np.exp(digamma(ep) - digamma(ep.sum(1, keepdims=True)))
+            infl = (np.asarray(h["varpar"]["beta"], float) + 1) / np.asarray(h["varpar"]["beta"], float)
+        else:
+            prior[j, :S] = h["prior"]
+            A[j, :S, :S] = h["trans"]
+            infl = np.ones(S)
+        for s in range(S):
+            cen[j, s] = h["pdf"][s]["mean"]
+            c = np.asarray(h["pdf"][s]["cov"], float)
+            cov[j, s] = infl[s] * (np.diag(c) if covmode == COV_DIAG else c)
+    omega = omega / omega.sum()
+    return BaseSet.from_numpy(dict(nstates=ns, prior=prior, A=A, centres=cen, covars=cov,
+                                   omega=omega, covmode=covmode))
+
+
+# ----------------------------------------------------------------------------
+# options (vbhem_h3m_cluster.m defaults consumed by the EM loop)
+# ----------------------------------------------------------------------------
+def default_options(K: int, S: int, d: int, **over) -> dict:
+    """vbhem_h3m_cluster.m:150-229 (the subset the EM loop reads)."""
+    m0 = {2: [256.0, 192.0], 3: [256.0, 192.0, 150.0]}.get(d, [0.0] * d)
+    opt = dict(K=K, S=S, alpha0=1.0, eta0=1.0, epsilon0=1.0, m0=m0, W0=0.005, lambda0=1.0, v0=5.0,
+               max_iter=200, minDiff=1e-5, Nv=100, tau=10, covmode=COV_FULL, verbose=0)
+    opt["hyps_max"] = dict(alpha0=1.0686e13, eta0=1.0686e13, epsilon0=1.0686e13, v0=1e4,
+                           lambda0=1.0686e13, W0=1.0686e13)
+    opt["hyps_min"] = dict(alpha0=1.0686e-13, eta0=1.0686e-13, epsilon0=1.0686e-13,
+                           v0=2.0612e-09 + d - 1, lambda0=1.0686e-13, W0=1.0686e-13)
+    opt.update(over)
+    opt["m0"] = np.asarray(opt["m0"], dtype=float).reshape(-1)
+    if opt["v0"] <= d - 1:
+        raise ValueError("v0 not large enough...should be > D-1")  # vbhem_h3m_cluster.m:233
+    return opt
+
+
+def clip_hyps(opt: dict) -> dict:
+    """vbhem_clip_hyps.m:20-85."""
+    out = dict(opt)
+    for name in ("alpha0", "eta0", "epsilon0", "v0", "lambda0", "W0"):
+        val = np.array(opt[name], dtype=float, ndmin=1)
+        val = np.where(val >= opt["hyps_max"][name], opt["hyps_max"][name], val)
+        val = np.where(val <= opt["hyps_min"][name], opt["hyps_min"][name], val)
+        out[name] = val if np.ndim(opt[name]) else float(val[0])
+    return out
+
+
+def baseem_init(base: BaseSet, opt: dict, randomb: np.ndarray, randomg: np.ndarray,
+                omega_rand: np.ndarray) -> Posterior:
+    """'baseem' initialisation (vbhemhmm_init.m:58-100, initopt.mode='u').
+
+    randomb/randomg [K,S]: 0-based base-HMM / state draws (MATLAB randi);
+    omega_rand [K]: uniform draws (MATLAB rand)."""
+    opt = clip_hyps(opt)
+    K, S = opt["K"], opt["S"]
+    Kb, d = base.N, base.d
+    Nv = opt["Nv"] * Kb
+    NLr = Nv / K
+    lam = np.full((K, S), opt["lambda0"] + NLr / S)
+    v = np.full((K, S), opt["v0"] + NLr / S + 1)
+    rb = np.asarray(randomb, dtype=np.int64)
+    rg = np.asarray(randomg, dtype=np.int64)
+    cen = base.centres[torch.as_tensor(rb.reshape(-1)), torch.as_tensor(rg.reshape(-1))]
+    cov = base.covars[torch.as_tensor(rb.reshape(-1)), torch.as_tensor(rg.reshape(-1))]
+    m = cen.cpu().numpy().reshape(K, S, d)
+    cov = cov.cpu().numpy()
+    scale = (v.reshape(-1) - d - 1)
+    if base.covmode == COV_DIAG:
+        W = (1.0 / (scale[:, None] * cov)).reshape(K, S, d)
+    else:
+        W = np.linalg.inv(scale[:, None, None] * cov).reshape(K, S, d, d)
+    eta = np.full((K, S), (1.0 / S) * NLr + opt["eta0"])
+    epsilon = np.full((K, S, S), ((1.0 / S) * NLr) / S + opt["epsilon0"])
+    omega = np.asarray(omega_rand, dtype=float)
+    omega = omega / omega.sum()
+    alpha = opt["alpha0"] + omega * Nv
+    return Posterior(alpha=alpha, eta=eta, epsilon=epsilon, lam=lam, v=v, m=m, W=W,
+                     W0mode="iid" if np.size(opt["W0"]) == 1 else "diag")
+
+
+def baseem_draws(base: BaseSet, K: int, S: int, seed: int):
+    """Seeded stand-in for MATLAB's randi/rand in baseem (numpy PCG64)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rb = rng.integers(0, base.N, size=(K, S))
+    ns = base.nstates.cpu().numpy()
+    rg = np.floor(rng.random((K, S)) * ns[rb]).astype(np.int64)
+    om = rng.random(K)
+    return rb, rg, om
+
+
+# ----------------------------------------------------------------------------
+# synthetic workloads
+# ----------------------------------------------------------------------------
+CONFIGS = {
+    # name: (N, K, S, Sb, d, covmode, tau, Nv, option overrides)
+    "C2": dict(N=100, K=4, S=3, Sb=2, d=2, covmode=COV_FULL, tau=50, Nv=100,
+               opt=dict(alpha0=1e6, eta0=1.0, epsilon0=1.0, lambda0=1.0, v0=5.0, W0=1.0,
+                        m0=[1.5, 1.5])),
+    "C3": dict(N=10_000, K=8, S=5, Sb=5, d=2, covmode=COV_DIAG, tau=10, Nv=100, opt={}),
+    # v0 must exceed d-1 (vbhem_h3m_cluster.m:233); the default 5 only suits d <= 5
+    "C4": dict(N=100_000, K=16, S=8, Sb=8, d=8, covmode=COV_FULL, tau=10, Nv=100, opt=dict(v0=10.0)),
+    "C5": dict(N=1_000_000, K=32, S=12, Sb=12, d=16, covmode=COV_FULL, tau=10, Nv=100,
+               opt=dict(v0=18.0)),
+}
+
+
+def _digamma(x: torch.Tensor) -> torch.Tensor:
+    return torch.special.digamma(x)
+
+
+def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
+                   device="cpu", exprmt1: bool = False, ragged: bool = False) -> BaseSet:
+    """Synthetic h3m_b built directly in packed form (use_post=1 semantics).
+
+    Ground truth: K HMMs, base i is a noisy copy of GT g = i mod K: means
+    U[0,5]^d + N(0,0.1^2) per base, covariance L L'/d + 0.5 I (full) or
+    U[0.5,1.5] (diag), prior and A rows ~ Dirichlet(1); VB counts
+    alpha = 1+25*pi, epsilon = 1+250*A, beta = 1+250/Sb, then the
+    hmms_to_h3m_hem(use_post=1) transform.  exprmt1=True uses the two GT HMMs
+    of Synthetic_experiment/exprmt1_sampledata.m:20-43 instead (Sb=d=2).
+    ragged=True draws per-base state counts in [1, Sb] (zero-padded)."""
+    g = torch.Generator(device="cpu").manual_seed(int(seed))
+    dt = torch.float64
+    if exprmt1:
+        G = 2
+        gt_prior = torch.tensor([[0.5, 0.5], [0.5, 0.5]], dtype=dt)
+        gt_A = torch.tensor([[[0.6, 0.4], [0.4, 0.6]], [[0.4, 0.6], [0.6, 0.4]]], dtype=dt)
+        gt_mu = torch.tensor([[[0.0, 0.0], [3.0, 3.0]]] * 2, dtype=dt)
+        eye = torch.eye(2, dtype=dt)
+        gt_cov = eye.expand(G, 2, 2, 2).clone() if covmode == COV_FULL else torch.ones(G, 2, 2, dtype=dt)
+    else:
+        G = K
+        gt_prior = _dirichlet(g, (G,), Sb)
+        gt_A = _dirichlet(g, (G, Sb), Sb)
+        gt_mu = torch.rand((G, Sb, d), generator=g, dtype=dt) * 5.0
+        if covmode == COV_FULL:
+            Lm = torch.randn((G, Sb, d, d), generator=g, dtype=dt)
+            gt_cov = Lm @ Lm.transpose(-1, -2) / d + 0.5 * torch.eye(d, dtype=dt)
+        else:
+            gt_cov = 0.5 + torch.rand((G, Sb, d), generator=g, dtype=dt)
+    gi = torch.arange(N) % G
+    alpha = 1.0 + 25.0 * gt_prior[gi]
+    eps = 1.0 + 250.0 * gt_A[gi]
+    beta = 1.0 + 250.0 / Sb
+    prior = torch.exp(_digamma(alpha) - _digamma(alpha.sum(-1, keepdim=True)))
+    A = torch.exp(_digamma(eps) - _digamma(eps.sum(-1, keepdim=True)))
+    centres = gt_mu[gi] + 0.1 * torch.randn((N, Sb, d), generator=g, dtype=dt)
+    covars = ((beta + 1.0) / beta) * gt_cov[gi]
+    nstates = torch.full((N,), Sb, dtype=torch.int32)
+    if ragged and Sb > 1:
+        nstates = torch.randint(1, Sb + 1, (N,), generator=g, dtype=torch.int32)
+        mask = torch.arange(Sb)[None, :] < nstates[:, None].long()
+        prior = prior * mask
+        A = A * mask[:, :, None] * mask[:, None, :]
+        centres = centres * mask[:, :, None]
+        if covmode == COV_FULL:
+            covars = torch.where(mask[:, :, None, None], covars, torch.eye(d, dtype=dt).expand_as(covars))
+        else:
+            covars = torch.where(mask[:, :, None], covars, torch.ones_like(covars))
+    omega = torch.full((N,), 1.0 / N, dtype=dt)
+    return BaseSet(nstates, prior.contiguous(), A.contiguous(), centres.contiguous(),
+                   covars.contiguous(), omega, covmode).to(device)
+
+
+def _dirichlet(g: torch.Generator, batch, n: int) -> torch.Tensor:
+    # Dirichlet(1) = normalised Exp(1) draws
+    e = -torch.log(torch.rand(tuple(batch) + (n,), generator=g, dtype=torch.float64).clamp_min(1e-300))
+    return e / e.sum(-1, keepdim=True)
+
+
+def synth_workload(name: str, seed: Optional[int] = None, device="cpu", N: Optional[int] = None):
+    """(BaseSet, Posterior, options) for a named config; seed = 1001 + index
+    (BASELINE.md).  ``N`` overrides the number of base HMMs (sub-sampling)."""
+    cfg = CONFIGS[name]
+    idx = list(CONFIGS).index(name) + 1
+    seed = 1001 + idx if seed is None else seed
+    n = cfg["N"] if N is None else N
+    base = synth_base_set(n, cfg["K"], cfg["Sb"], cfg["d"], cfg["covmode"], seed, device=device,
+                          exprmt1=(name == "C2"))
+    opt = default_options(cfg["K"], cfg["S"], cfg["d"], tau=cfg["tau"], Nv=cfg["Nv"],
+                          covmode=cfg["covmode"], **cfg["opt"])
+    rb, rg, om = baseem_draws(base, cfg["K"], cfg["S"], seed)
+    post = baseem_init(base, opt, rb, rg, om)
+    return base, post, opt

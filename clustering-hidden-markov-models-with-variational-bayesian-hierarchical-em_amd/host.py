@@ -1,0 +1,187 @@
+"""Host-side math around the device E-step (vectorised over clusters/states).
+
+Everything here is O(K*S*d^3) per EM iteration -- tiny next to the E-step --
+and mirrors the MATLAB code that surrounds the MEX call:
+
+* :func:`cluster_constants` -- psi prelude, vbhem_h3m_c_step_fc.m:118-165, 180-191
+* :func:`log_omega_tilde`   -- vbhem_h3m_c_step_fc.m:271-273
+* :func:`unpack_stats` / :func:`finish_statistics` -- vbhem_compute_Statistics.m:57-82
+* :func:`mstep`             -- vbhem_mstep_component.m:42-70 and step_fc.m:396
+* :func:`lower_bound`       -- vbhemh3m_lb.m:64-186
+* :func:`convert_to_point`  -- convert_h3mrtoh3mb.m:9-79
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.special import digamma, gammaln
+
+from .h3m import COV_DIAG, COV_FULL, Posterior
+
+
+def cluster_constants(post: Posterior, covmode: int) -> dict:
+    """Per-cluster E-step constants for this iteration.
+
+    logLambdaTilde = sum_q psi((v+1-q)/2) + d log 2 + log|W|  (:136,146)
+    c  = -logLambdaTilde + d/lambda                              (:154)
+    logA = psi(eps) - psi(sum_sigma eps);  logPi = psi(eta) - psi(sum eta)  (:156-161)
+    P  = v * W                                                   (:189)
+    Diag mode uses sum(log W): MATLAB's sum(log(diag(W))) on a 1xd row only
+    runs for d == 1, where both agree."""
+    K, S, d = post.m.shape
+    q = np.arange(1, d + 1)
+    t1 = digamma(0.5 * (post.v[..., None] + 1.0) - 0.5 * q).sum(-1)
+    if covmode == COV_FULL:
+        logdet = np.log(np.linalg.det(post.W))
+    else:
+        logdet = np.log(post.W).sum(-1)
+    lLT = t1 + d * np.log(2.0) + logdet
+    eps = post.epsilon
+    logA = digamma(eps) - digamma(eps.sum(-1, keepdims=True))
+    logPi = digamma(post.eta) - digamma(post.eta.sum(-1, keepdims=True))
+    P = post.v[..., None, None] * post.W if covmode == COV_FULL else post.v[..., None] * post.W
+    return dict(logLambdaTilde=lLT, c=-lLT + d / post.lam, logA=logA, logPi=logPi,
+                m=np.ascontiguousarray(post.m), P=np.ascontiguousarray(P))
+
+
+def log_omega_tilde(alpha: np.ndarray) -> np.ndarray:
+    return digamma(alpha) - digamma(alpha.sum())
+
+
+def stats_nu(d: int, covmode: int) -> int:
+    return 1 + d + d * (d + 1) // 2 if covmode == COV_FULL else 1 + 2 * d
+
+
+def stats_len(K: int, S: int, d: int, covmode: int) -> int:
+    return K + K * S + K * S * S + 2 + K * S * stats_nu(d, covmode)
+
+
+def unpack_stats(vec: np.ndarray, K: int, S: int, d: int, covmode: int) -> dict:
+    """Split the packed E-step statistics (include/vbhem_estep.h) into arrays."""
+    vec = np.asarray(vec, dtype=np.float64)
+    o = 0
+    Nj = vec[o:o + K]; o += K
+    N1 = vec[o:o + K * S].reshape(K, S); o += K * S
+    M = vec[o:o + K * S * S].reshape(K, S, S); o += K * S * S
+    Lt1, Lt7 = vec[o], vec[o + 1]; o += 2
+    NU = stats_nu(d, covmode)
+    U = vec[o:o + K * S * NU].reshape(K, S, NU)
+    Nr = U[..., 0]
+    Y = U[..., 1:1 + d]
+    if covmode == COV_FULL:
+        SC = np.zeros((K, S, d, d))
+        iu = np.triu_indices(d)
+        SC[..., iu[0], iu[1]] = U[..., 1 + d:]
+        SC[..., iu[1], iu[0]] = U[..., 1 + d:]
+    else:
+        SC = U[..., 1 + d:1 + 2 * d].copy()
+    return dict(Nj=Nj.copy(), N1=N1.copy(), M=M.copy(), Lt1=float(Lt1), Lt7=float(Lt7),
+                Nr=Nr.copy(), Y=Y.copy(), SC=SC)
+
+
+def finish_statistics(st: dict, covmode: int) -> dict:
+    """vbhem_compute_Statistics.m:57-82 on the gated sums (all clusters)."""
+    S = st["N1"].shape[1]
+    Nr = st["Nr"] + 1e-50
+    y = st["Y"] / Nr[..., None]
+    if covmode == COV_FULL:
+        SC = st["SC"] / Nr[..., None, None] - y[..., :, None] * y[..., None, :]
+    else:
+        SC = st["SC"] / Nr[..., None] - y * y
+    M = st["M"] if S > 1 else np.full_like(st["M"], 1e-12)
+    return dict(Nj_rho1=st["N1"], Nj_rho2rho=M, Nj_rho=Nr, y_bar=y, S_plus_C=SC)
+
+
+def _W0(opt: dict, d: int) -> np.ndarray:
+    W0 = np.asarray(opt["W0"], dtype=float)
+    return W0 * np.eye(d) if W0.size == 1 else np.diag(W0)
+
+
+def mstep(syn: dict, Nj: np.ndarray, opt: dict, covmode: int, W0mode: str) -> Posterior:
+    """vbhem_mstep_component.m:42-70 for every cluster, alpha = alpha0 + Nj (step_fc.m:396)."""
+    d = syn["y_bar"].shape[-1]
+    m0 = np.asarray(opt["m0"], dtype=float)
+    lam0 = opt["lambda0"]
+    W0inv = np.linalg.inv(_W0(opt, d))
+    Nk = syn["Nj_rho"]
+    lam = lam0 + Nk
+    v = opt["v0"] + Nk + 1.0
+    m = (lam0 * m0 + Nk[..., None] * syn["y_bar"]) / (lam0 + Nk)[..., None]
+    mult1 = lam0 * Nk / (lam0 + Nk)
+    diff = syn["y_bar"] - m0
+    outer = diff[..., :, None] * diff[..., None, :]
+    if covmode == COV_FULL:
+        tW = np.linalg.inv(W0inv + Nk[..., None, None] * syn["S_plus_C"] + mult1[..., None, None] * outer)
+        W = (tW + np.swapaxes(tW, -1, -2)) / 2
+    else:
+        diagSC = syn["S_plus_C"][..., :, None] * np.eye(d)
+        tW = np.linalg.inv(W0inv + Nk[..., None, None] * diagSC + mult1[..., None, None] * outer)
+        W = np.diagonal((tW + np.swapaxes(tW, -1, -2)) / 2, axis1=-2, axis2=-1).copy()
+    eta = opt["eta0"] + syn["Nj_rho1"]
+    epsilon = opt["epsilon0"] + syn["Nj_rho2rho"]
+    return Posterior(alpha=opt["alpha0"] + Nj, eta=eta, epsilon=epsilon, lam=lam, v=v, m=m, W=W,
+                     W0mode=W0mode)
+
+
+def lower_bound(Lt1: float, Lt7: float, Nj: np.ndarray, logOmega: np.ndarray, post: Posterior,
+                consts: dict, opt: dict, covmode: int) -> float:
+    """vbhemh3m_lb.m:64-186 (value only).  Lt1 = sum Z.*L_elbo and
+    Lt7 = sum hat_Z.*log(hat_Z) come reduced from the device."""
+    K, S = post.K, opt["S"]
+    d = len(opt["m0"])
+    a0, e0, ep0, l0, v0 = opt["alpha0"], opt["eta0"], opt["epsilon0"], opt["lambda0"], opt["v0"]
+    m0 = np.asarray(opt["m0"], dtype=float)
+    W0inv = np.linalg.inv(_W0(opt, d))
+    if np.size(opt["W0"]) == 1:
+        logdetW0inv = d * np.log(W0inv[0, 0])
+    else:
+        logdetW0inv = np.log(np.diag(W0inv)).sum()
+    q = np.arange(1, d + 1)
+    logCalpha0 = gammaln(K * a0) - K * gammaln(a0)
+    logCeta0 = gammaln(S * e0) - S * gammaln(e0)
+    logCepsilon0 = gammaln(S * ep0) - S * gammaln(ep0)
+    logB0 = (v0 / 2) * logdetW0inv - (v0 * d / 2) * np.log(2) - (d * (d - 1) / 4) * np.log(np.pi) \
+        - gammaln(0.5 * (v0 + 1 - q)).sum()
+    const2 = d * np.log(l0 / (2 * np.pi))
+    alpha = post.alpha
+    logCalpha = gammaln(alpha.sum()) - gammaln(alpha).sum()
+    lLT = consts["logLambdaTilde"]
+    Lt2 = Nj @ logOmega
+    Lt3 = K * logCeta0 + (e0 - 1) * consts["logPi"].sum()
+    Lt4 = K * S * logCepsilon0 + (ep0 - 1) * consts["logA"].sum()
+    Lt6 = logCalpha0 + (a0 - 1) * logOmega.sum()
+    Lt8 = logCalpha + (alpha - 1) @ logOmega
+    Wf = post.W if covmode == COV_FULL else post.W[..., :, None] * np.eye(d)
+    v, lam = post.v, post.lam
+    logBk = -(v / 2) * np.log(np.linalg.det(Wf)) - (v * d / 2) * np.log(2) \
+        - (d * (d - 1) / 4) * np.log(np.pi) - gammaln(0.5 * (v[..., None] + 1 - q)).sum(-1)
+    H = (-logBk - 0.5 * (v - d - 1) * lLT + 0.5 * v * d).sum(-1)
+    diff = post.m - m0
+    mWm = np.einsum("ksa,ksab,ksb->ks", diff, Wf, diff)
+    trW = np.einsum("ab,ksba->ks", W0inv, Wf)
+    Lt51 = 0.5 * (const2 + lLT - d * l0 / lam - l0 * v * mWm).sum(-1)
+    Lt52 = S * logB0 + 0.5 * (v0 - d - 1) * lLT.sum(-1) - 0.5 * (v * trW).sum(-1)
+    Lt5 = (Lt51 + Lt52).sum()
+    eta, eps = post.eta, post.epsilon
+    logCeta = gammaln(eta.sum(-1)) - gammaln(eta).sum(-1)
+    logCeps = gammaln(eps.sum(-1)) - gammaln(eps).sum(-1)
+    Lt9 = (logCeta + ((eta - 1) * consts["logPi"]).sum(-1)).sum() \
+        + (logCeps + ((eps - 1) * consts["logA"]).sum(-1)).sum()
+    Lt10 = (0.5 * (lLT + d * np.log(lam / (2 * np.pi))).sum(-1) - 0.5 * d * S - H).sum()
+    return float(Lt1 + Lt2 + Lt3 + Lt4 + Lt5 + Lt6 - Lt7 - Lt8 - Lt9 - Lt10)
+
+
+def convert_to_point(post: Posterior, covmode: int) -> dict:
+    """convert_h3mrtoh3mb.m:9-79: prior, A, centres, covars, omega point estimates."""
+    K, S, d = post.m.shape
+    prior = post.eta / post.eta.sum(-1, keepdims=True)
+    sc = post.epsilon.sum(-1, keepdims=True)
+    A = post.epsilon / np.where(sc == 0, 1.0, sc)
+    den = np.where(post.v > d + 1, post.v - d - 1, post.v)
+    if covmode == COV_FULL:
+        tC = np.linalg.inv(post.W) / den[..., None, None]
+        cov = (tC + np.swapaxes(tC, -1, -2)) / 2
+    else:
+        tC = (1.0 / post.W) / den[..., None]
+        cov = (tC + tC) / 2
+    return dict(prior=prior, A=A, centres=post.m.copy(), covars=cov,
+                omega=post.alpha / post.alpha.sum())

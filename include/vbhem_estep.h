@@ -1,0 +1,125 @@
+/*
+ * include/vbhem_estep.h -- C ABI of the MI355X-native VBHEM-H3M E-step
+ * (libvbhem_estep.so, gfx950).
+ *
+ * Drop-in boundary for the reference's only native call on the EM path:
+ *   [LL_elbo, nu_1, emit_pr, emit_mu, emit_Mu, sum_xi] =
+ *       vbhem_hmm_bwd_fwd_mex(h3m_b.hmm, h3m_r.hmm, T, maxN, maxN2
+ *                             [, logdetCovPlusDdivlamR, invCovR])
+ *   called at src/vbhem/vbhem_h3m_c_step_fc.m:175-176 (diag) and :193-194 (full),
+ *   implemented by src/vbhem/vbhem_hmm_bwd_fwd_mex.c:288-1472.
+ * The MATLAB-facing gateway that binds these entry points lives in
+ * integration/vbhem_hmm_bwd_fwd_mex.c.
+ *
+ * Conventions
+ *   - All arrays are dense, row-major (C order), IEEE fp64 unless noted.
+ *   - Base HMMs are zero-padded to SB = max states (maxN in the reference);
+ *     nstates[i] <= SB holds the true count.  Zero prior/A rows and columns are
+ *     exact no-ops in the recursions (mex.c:964-971, 1054-1058, 1196-1206).
+ *   - covmode: VBHEM_COV_DIAG (covars/P are [..][d]) or VBHEM_COV_FULL ([..][d][d]).
+ *   - Pointers inside vbhem_base_t / vbhem_cluster_t and every *_dev argument
+ *     are DEVICE pointers; `stream` is a hipStream_t (NULL = default stream).
+ *   - Functions return VBHEM_OK (0) or a negative status; vbhem_last_error()
+ *     gives a message.  Nothing synchronises the stream except the *_host
+ *     convenience entry point.
+ */
+#ifndef VBHEM_ESTEP_H
+#define VBHEM_ESTEP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VBHEM_COV_DIAG 0
+#define VBHEM_COV_FULL 1
+
+#define VBHEM_OK 0
+#define VBHEM_ERR_ARG (-1)       /* invalid sizes / pointers                    */
+#define VBHEM_ERR_UNSUPPORTED (-2) /* shape outside the built kernels' limits   */
+#define VBHEM_ERR_WORKSPACE (-3) /* workspace too small                          */
+#define VBHEM_ERR_HIP (-4)       /* HIP runtime error (message has details)     */
+
+/* h3m_b: the N base HMMs (reference fields hmm_b.prior/A/emit{k}.centres/covars,
+ * read at mex.c:459-473). */
+typedef struct {
+  int N;                 /* number of base HMMs (Kb)                           */
+  int SB;                /* padded states per base HMM (maxN)                  */
+  int d;                 /* emission dimension                                 */
+  int covmode;           /* VBHEM_COV_DIAG | VBHEM_COV_FULL                    */
+  const int *nstates;    /* [N]        true state counts (<= SB)               */
+  const double *prior;   /* [N][SB]    hmm_b.prior (may be sub-stochastic)     */
+  const double *A;       /* [N][SB][SB] hmm_b.A, A[i][from][to]                */
+  const double *centres; /* [N][SB][d] emit{k}.centres                          */
+  const double *covars;  /* [N][SB][d][d] | [N][SB][d]   emit{k}.covars         */
+} vbhem_base_t;
+
+/* h3m_r: the K cluster HMMs' variational constants for this EM iteration
+ * (mex.c:433-457; built on the MATLAB side at step_fc.m:118-165, 180-191). */
+typedef struct {
+  int K;                 /* number of clusters (Kr)                            */
+  int S;                 /* states per cluster (maxN2; all clusters equal)     */
+  const double *logA;    /* [K][S][S]  logATilde[rho][sigma]                   */
+  const double *logPi;   /* [K][S]     logPiTilde                              */
+  const double *m;       /* [K][S][d]  emit{k}.m                               */
+  const double *P;       /* [K][S][d][d] invCovR = v.*W  | [K][S][d] v*W (diag) */
+  const double *c;       /* [K][S]     logdetCovPlusDdivlamR = -logLambdaTilde + d/lambda */
+} vbhem_cluster_t;
+
+/* Per-pair outputs of the reference MEX (mex.c:396-409), laid out [N][K][...]:
+ *   LL_elbo [N][K]; sum_nu_1 [N][K][S]; emit_pr [N][K][S]; emit_mu [N][K][S][d];
+ *   emit_Mu [N][K][S][d][d] (full) | [N][K][S][d] (diag); sum_xi [N][K][S][S].
+ * sum_t_nu [N][K][S][SB] (the forward occupancy sum, mex.c:1148-1297) is an
+ * optional extra output (NULL to skip). */
+size_t vbhem_pairs_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T);
+int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
+                      double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
+                      double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
+                      void *stream);
+
+/* Same as vbhem_estep_pairs, with HOST arrays in and out (allocates, copies,
+ * computes on `device`, copies back, frees).  This is what the MEX gateway
+ * calls; base/clus pointers are host pointers here. */
+int vbhem_estep_pairs_host(int device, const vbhem_base_t *base_host,
+                           const vbhem_cluster_t *clus_host, int T, double *LL_elbo,
+                           double *sum_nu_1, double *emit_pr, double *emit_mu,
+                           double *emit_Mu, double *sum_xi);
+
+/* Fused E-step for one EM iteration on this device's shard of base HMMs:
+ *   pairs (mex.c) -> responsibilities (step_fc.m:271-283) -> gated, Z-weighted
+ *   statistic sums (vbhem_compute_Statistics.m:33-55) -> ELBO partials
+ *   (vbhemh3m_lb.m:90,107).
+ * Inputs: tildeN_dev [N] = Nv*Kb*omega (step_fc.m:26-30) for this shard,
+ *         logOmega_dev [K] = psi(alpha) - psi(sum alpha) (step_fc.m:271-273).
+ * Outputs: hatZ_dev [N][K] (hat_Z incl. +1e-50), LL_elbo_dev [N][K],
+ *          stats_dev [vbhem_stats_len(...)] laid out as
+ *   [ Nj[K] | N1[K][S] | M[K][S][S] | Lt1 | Lt7 | U[K][S][NU] ]
+ *   where Nj = sum_i Z (no gate, no +1e-50), N1 = sum_i g Z nu_1, M = sum_i g Z sum_xi,
+ *   Lt1 = sum Z.*L_elbo, Lt7 = sum hat_Z.*log(hat_Z), g = [Z > 1e-8], and
+ *   U[j][s][:] = sum_i g Z(i,j) sum_b sum_t_nu(i,j,s,b) * u(i,b,:) with
+ *   u = [1, mu (d), Sigma+mu mu' packed upper-triangular (d(d+1)/2)] (full) or
+ *   u = [1, mu (d), mu.^2 + sigma (d)] (diag); NU = vbhem_stats_nu(d, covmode).
+ * All terms are plain sums over this shard's bases: shards combine by summation
+ * (one all-reduce).  Results are deterministic for a fixed shard. */
+size_t vbhem_stats_nu(int d, int covmode);
+size_t vbhem_stats_len(int K, int S, int d, int covmode);
+size_t vbhem_fused_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T);
+int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      const double *tildeN_dev, const double *logOmega_dev,
+                      double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
+                      void *workspace_dev, size_t workspace_bytes, void *stream);
+
+/* Number of pairs the last call on this thread had to recompute with the
+ * exact (reference-order, Theta-storing) fallback because the factorised
+ * log-sum-exp fell below its safe range.  Synchronises `stream`. */
+int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
+
+const char *vbhem_last_error(void);
+const char *vbhem_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBHEM_ESTEP_H */
