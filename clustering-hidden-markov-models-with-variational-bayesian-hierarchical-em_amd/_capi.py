@@ -43,6 +43,10 @@ EXPORTS = {
     "vbhem_estep_fused": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "vbhem_last_fallback_count": (_c_int, [_vp, _vp]),
+    "vbhem_timing_enable": (_c_int, [_c_int]),
+    "vbhem_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                                   ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_last_error": (ctypes.c_char_p, []),
     "vbhem_version": (ctypes.c_char_p, []),
 }
@@ -79,3 +83,17 @@ def check(rc: int, what: str):
 
 def ptr(t) -> int:
     return 0 if t is None else int(t.data_ptr())
+
+
+def timing_enable(on: bool = True) -> None:
+    lib().vbhem_timing_enable(1 if on else 0)
+
+
+def timing_read() -> dict:
+    """Summed HIP-event times of the fb/stats kernel launches since the last read."""
+    fb, st = ctypes.c_double(), ctypes.c_double()
+    nf, npairs, ns = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong()
+    check(lib().vbhem_timing_read(ctypes.byref(fb), ctypes.byref(nf), ctypes.byref(npairs),
+                                  ctypes.byref(st), ctypes.byref(ns)), "vbhem_timing_read")
+    return dict(fb_ms=fb.value, fb_launches=nf.value, fb_pairs=npairs.value,
+                stats_ms=st.value, stats_launches=ns.value)

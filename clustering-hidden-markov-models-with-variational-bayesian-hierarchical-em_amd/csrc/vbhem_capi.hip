@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "vbhem_estep.h"
 #include "vbhem_internal.h"
@@ -17,6 +19,23 @@
 namespace {
 
 thread_local std::string g_err;
+
+// Optional kernel timing (bench/profiling): hipEvents recorded on the launch
+// stream around each fb_pairs_kernel / stats_kernel launch; read back (and
+// synchronised) only by vbhem_timing_read.  Off by default (graph capture).
+struct TimingState {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats;
+  std::vector<long long> fb_pairs;
+};
+TimingState g_timing;
+
+hipEvent_t timing_event(hipStream_t st) {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+  (void)hipEventRecord(ev, st);
+  return ev;
+}
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
@@ -99,6 +118,51 @@ bool plan_fb(int SB, int d, int covmode, int K, int S, int T, FbPlan &out) {
   return found;
 }
 
+struct SplitPlan {
+  bool ok = false;
+  vbhem::SplitArgs a{};
+  size_t lds = 0;
+  int ppb = 0;
+};
+
+// Geometry of fb_split_kernel; must match SplitLayout<S, LPC> (vbhem_internal.h).
+SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
+  SplitPlan sp;
+  if (!vbhem::split_supported(S, SB, d)) return sp;
+  const int LPC = vbhem::split_lpc(S);
+  const int SH = (S + LPC - 1) / LPC;
+  const int LPP = S * LPC;
+  const int D = vbhem::split_dim_bucket(d);
+  const int NPF = D * (D + 1) / 2;
+  const int XCS = (LPC * SH + 1) / 2 * 2 + 2;
+  const int XP = S * XCS + 2;
+  const int OFF_X = (2 * S * S + 2 * S + 1) / 2 * 2;
+  double best = -1.0;
+  for (int nwb = 1; nwb <= 4; ++nwb) {
+    const int NT = nwb * 64;
+    const int ppb = NT / LPP;
+    if (ppb < 1) continue;
+    const int off_Y = OFF_X + ppb * XP;
+    const int off_F = (off_Y + ppb * S + 1) / 2 * 2;
+    const int off_R = (off_F + (ppb + 1) / 2 + 1) / 2 * 2;
+    const size_t lattice = (size_t)std::max(0, T - 2) * SH * NT;
+    const size_t staging = (size_t)S * D + 2 * (size_t)S * NPF + S;
+    const size_t lds = ((size_t)off_R + std::max(lattice, staging)) * sizeof(double);
+    if (lds > kLdsLimit) continue;
+    const double util = double(ppb * LPP) / NT;
+    if (util > best + 0.02) {
+      best = util;
+      vbhem::SplitArgs &x = sp.a;
+      x.SB = SB; x.d = d; x.covmode = covmode; x.K = K; x.S = S; x.T = T; x.D = D; x.nwb = nwb;
+      x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R;
+      sp.lds = lds;
+      sp.ppb = ppb;
+      sp.ok = true;
+    }
+  }
+  return sp;
+}
+
 size_t exact_stride(int S, int SB, int T) {
   return (size_t)6 * S * SB + SB + (size_t)S * S * SB * T;
 }
@@ -179,11 +243,35 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   return cv.off + 256;
 }
 
-int run_fb(const vbhem::FbArgs &proto, const FbPlan &plan, int i_begin, int i_end, int i_buf0,
-           double *LL, double *nu1, double *xi, double *tnu, int *flags, double *scratch,
-           hipStream_t st) {
+struct FbCtx {
+  FbPlan plan;      // generic element-per-lane kernel
+  SplitPlan split;  // column-per-LPC-lanes kernel (preferred when it applies)
+};
+
+int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T) {
+  c.split = plan_split(b->SB, b->d, b->covmode, cl->K, cl->S, T);
+  const bool have_elems = plan_fb(b->SB, b->d, b->covmode, cl->K, cl->S, T, c.plan);
+  if (!c.split.ok && !have_elems)
+    return fail(VBHEM_ERR_UNSUPPORTED,
+                "no launch geometry fits (S*SB must be <= 512 and the per-pair lattice "
+                "(2*(T-1)+3)*S*SB doubles must fit in 160 KiB of LDS)");
+  if (!have_elems) c.plan = FbPlan{};
+  fill_inputs(c.plan.a, b, cl);
+  // fields the exact fallback kernel needs even when the generic plan is unused
+  c.plan.a.SB = b->SB; c.plan.a.d = b->d; c.plan.a.covmode = b->covmode;
+  c.plan.a.K = cl->K; c.plan.a.S = cl->S; c.plan.a.T = T;
+  if (c.split.ok) {
+    vbhem::SplitArgs &a = c.split.a;
+    a.prior = b->prior; a.A = b->A; a.centres = b->centres; a.covars = b->covars;
+    a.logA = cl->logA; a.logPi = cl->logPi; a.m = cl->m; a.P = cl->P; a.c = cl->c;
+  }
+  return VBHEM_OK;
+}
+
+int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, double *nu1,
+           double *xi, double *tnu, int *flags, double *scratch, hipStream_t st) {
   if (i_end <= i_begin) return VBHEM_OK;
-  vbhem::FbArgs a = proto;
+  vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin;
   a.i_end = i_end;
   a.i_buf0 = i_buf0;
@@ -192,10 +280,26 @@ int run_fb(const vbhem::FbArgs &proto, const FbPlan &plan, int i_begin, int i_en
   a.flag_list = flags + 2;
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
-  const int nib = (i_end - i_begin + a.BI - 1) / a.BI;
-  const dim3 grid((unsigned)nib * (unsigned)a.njb);
-  e = vbhem::launch_fb(a, grid, plan.block, plan.lds, st);
-  if (e != hipSuccess) return hip_fail(e, "fb_pairs_kernel");
+  hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
+  if (c.split.ok) {
+    vbhem::SplitArgs ca = c.split.a;
+    ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
+    ca.LL = LL; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
+    ca.flag_count = flags; ca.flag_list = flags + 2;
+    const unsigned grid =
+        (unsigned)((i_end - i_begin + c.split.ppb - 1) / c.split.ppb) * (unsigned)ca.K;
+    e = vbhem::launch_split(ca, grid, c.split.lds, st);
+    if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
+  } else {
+    const int nib = (i_end - i_begin + a.BI - 1) / a.BI;
+    const dim3 grid((unsigned)nib * (unsigned)a.njb);
+    e = vbhem::launch_fb(a, grid, c.plan.block, c.plan.lds, st);
+    if (e != hipSuccess) return hip_fail(e, "fb_pairs_kernel");
+  }
+  if (g_timing.on) {
+    g_timing.fb.emplace_back(ev0, timing_event(st));
+    g_timing.fb_pairs.push_back((long long)(i_end - i_begin) * a.K);
+  }
   e = vbhem::launch_fb_exact(a, scratch, exact_stride(a.S, a.SB, a.T), kExactThreads, st);
   if (e != hipSuccess) return hip_fail(e, "fb_exact_kernel");
   return VBHEM_OK;
@@ -233,11 +337,6 @@ int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   if (base->N == 0) return VBHEM_OK;
   if (!LL_elbo_dev || !sum_nu_1_dev || !emit_pr_dev || !emit_mu_dev || !emit_Mu_dev || !sum_xi_dev)
     return fail(VBHEM_ERR_ARG, "null output array");
-  FbPlan plan;
-  if (!plan_fb(base->SB, base->d, base->covmode, clus->K, clus->S, T, plan))
-    return fail(VBHEM_ERR_UNSUPPORTED,
-                "no launch geometry fits (S*SB must be <= 512 and the per-pair lattice "
-                "(2*(T-1)+3)*S*SB doubles must fit in 160 KiB of LDS)");
   PairsWs w;
   const size_t need = carve_pairs(nullptr, base, clus, T, sum_t_nu_dev == nullptr, w);
   if (!workspace_dev || workspace_bytes < need)
@@ -245,9 +344,12 @@ int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   carve_pairs(workspace_dev, base, clus, T, sum_t_nu_dev == nullptr, w);
   double *tnu = sum_t_nu_dev ? sum_t_nu_dev : w.tnu;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  vbhem::FbArgs proto = plan.a;
-  fill_inputs(proto, base, clus);
-  rc = run_fb(proto, plan, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.flags,
+  FbCtx ctx;
+  rc = prepare_fb(ctx, base, clus, T);
+  if (rc != VBHEM_OK) return rc;
+  hipError_t e0 = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
+  if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
+  rc = run_fb(ctx, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.flags,
               w.scratch, st);
   if (rc != VBHEM_OK) return rc;
   vbhem::EmitArgs ea{};
@@ -274,11 +376,6 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   if (rc != VBHEM_OK) return rc;
   if (!tildeN_dev || !logOmega_dev || !stats_dev || !hatZ_dev || !LL_elbo_dev)
     return fail(VBHEM_ERR_ARG, "null fused argument");
-  FbPlan plan;
-  if (!plan_fb(base->SB, base->d, base->covmode, clus->K, clus->S, T, plan))
-    return fail(VBHEM_ERR_UNSUPPORTED,
-                "no launch geometry fits (S*SB must be <= 512 and the per-pair lattice "
-                "(2*(T-1)+3)*S*SB doubles must fit in 160 KiB of LDS)");
   FusedWs w;
   const size_t need = carve_fused(nullptr, base, clus, T, w);
   if (!workspace_dev || workspace_bytes < need)
@@ -311,20 +408,61 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   e = hipMemsetAsync(w.flags + 1, 0, sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flag total)");
 
-  vbhem::FbArgs proto = plan.a;
-  fill_inputs(proto, base, clus);
+  FbCtx ctx;
+  rc = prepare_fb(ctx, base, clus, T);
+  if (rc != VBHEM_OK) return rc;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);
-    rc = run_fb(proto, plan, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.flags, w.scratch, st);
+    rc = run_fb(ctx, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.flags, w.scratch, st);
     if (rc != VBHEM_OK) return rc;
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     const int nchunk = std::min(w.nslab, g1 - g0);
+    hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
     e = vbhem::launch_stats(sa, nchunk, ntg, slds, st);
     if (e != hipSuccess) return hip_fail(e, "stats_kernel");
+    if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
   e = vbhem::launch_stats_final(w.slabs, w.nslab, w.slab_len, stats_dev, st);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
   return VBHEM_OK;
+}
+
+int vbhem_timing_enable(int on) {
+  g_timing.on = on != 0;
+  return VBHEM_OK;
+}
+
+int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs, double *stats_ms,
+                      long long *stats_launches) {
+  double f = 0.0, s = 0.0;
+  long long np = 0;
+  int rc = VBHEM_OK;
+  auto drain = [&rc](std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, double &acc) {
+    for (auto &pr : v) {
+      float ms = 0.f;
+      if (pr.first && pr.second) {
+        hipError_t e = hipEventSynchronize(pr.second);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
+        if (e != hipSuccess) rc = hip_fail(e, "vbhem_timing_read");
+        acc += ms;
+      }
+      if (pr.first) (void)hipEventDestroy(pr.first);
+      if (pr.second) (void)hipEventDestroy(pr.second);
+    }
+  };
+  const long long nf = (long long)g_timing.fb.size(), ns = (long long)g_timing.stats.size();
+  drain(g_timing.fb, f);
+  drain(g_timing.stats, s);
+  for (long long x : g_timing.fb_pairs) np += x;
+  g_timing.fb.clear();
+  g_timing.stats.clear();
+  g_timing.fb_pairs.clear();
+  if (fb_ms) *fb_ms = f;
+  if (fb_launches) *fb_launches = nf;
+  if (fb_pairs) *fb_pairs = np;
+  if (stats_ms) *stats_ms = s;
+  if (stats_launches) *stats_launches = ns;
+  return rc;
 }
 
 int vbhem_last_fallback_count(void *stream, const void *workspace_dev) {

@@ -1,0 +1,620 @@
+// vbhem_fb_split.hip -- the E-step recursion, one base-state column per LPC lanes.
+//
+// Mapping (gfx950, wave64).  A workgroup of NWB wavefronts owns PPB pairs
+// (consecutive bases) x ONE cluster j.  Within a pair, base state b (padded to S
+// columns) is owned by a group of LPC adjacent lanes; lane h of the group holds
+// rows sigma in [h*SH, h*SH+SH) (SH = ceil(S/LPC)) of every S x Sb pair matrix
+// column in registers:   E, L, G, nu, tnu   (SH each)  and  H (SH x S).
+// * cluster-side contractions (Z = A' G, nu' = G .* (A'^T g)): each lane forms
+//   partial sums over its rows for all S outputs, then a DPP reduce-scatter
+//   across the LPC lanes (quad_perm swaps, no LDS);
+// * max / sum over sigma: DPP all-reduce;
+// * base-side contractions (L = Ab s, f = nu Ab): columns exchanged through a
+//   per-pair LDS slab (ds_read_b128);
+// * backward lattice G_t (t = 1..T-2): lane-private LDS; G_{T-1} = exp(E-max E)
+//   recomputed in the forward sweep;
+// * sum_xi: per-lane outer products H += g G^T (G all-gathered by DPP),
+//   reduced over the pair's columns once at the end.
+// LPC = 1 (S <= 4), 2 (S <= 8), 4 (S <= 16) keeps per-lane registers ~<= 256
+// and per-wave LDS ~<= 20 KB so two or more waves share each SIMD.
+//
+// Padded base states (b >= SB) and padded rows (sigma >= S when LPC does not
+// divide S) are exact no-ops: zero prior / Ab rows & columns; E = -inf rows
+// give G = 0 (mex.c:964-971, 1054-1058, 1196-1206).
+//
+// Reference: src/vbhem/vbhem_hmm_bwd_fwd_mex.c  K1 :715-865, K2 :915-1015,
+// K3 :1020-1080, K4 :1093-1298.  Factorised log-sum-exp: vbhem_kernels.hip, DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "vbhem_internal.h"
+#include "vbhem_math.h"
+
+namespace vbhem {
+
+namespace {
+
+constexpr double kLog2PiS = 1.8378770664093454835606594728112353;
+constexpr double kZMinS = 1e-200;
+
+// ---- DPP lane exchange inside aligned lane quads -------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int lo2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi2, lo2);
+}
+constexpr int kXor1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int kXor2 = 0x4E;  // quad_perm [2,3,0,1]
+
+template <int M>
+__device__ __forceinline__ double xchg(double v) {
+  if constexpr (M == 1) return dpp_d<kXor1>(v);
+  else return dpp_d<kXor2>(v);
+}
+
+template <int LPC>
+__device__ __forceinline__ double allmax(double v) {
+  if constexpr (LPC >= 2) v = fmax(v, xchg<1>(v));
+  if constexpr (LPC >= 4) v = fmax(v, xchg<2>(v));
+  return v;
+}
+template <int LPC>
+__device__ __forceinline__ double allsum(double v) {
+  if constexpr (LPC >= 2) v += xchg<1>(v);
+  if constexpr (LPC >= 4) v += xchg<2>(v);
+  return v;
+}
+
+// Reduce-scatter: in[LPC*SH] holds this lane's partial sums for every owner's
+// rows (owner o, index k at o*SH+k); out[SH] = sum over the group for rows
+// owned by lane h.  Butterfly: mask 2 then mask 1.
+template <int LPC, int SH>
+__device__ __forceinline__ void reduce_scatter(const double (&in)[LPC * SH], double (&out)[SH], int h) {
+  if constexpr (LPC == 1) {
+#pragma unroll
+    for (int k = 0; k < SH; ++k) out[k] = in[k];
+  } else if constexpr (LPC == 2) {
+    const bool hi = h & 1;
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const double mine = hi ? in[SH + k] : in[k];
+      const double send = hi ? in[k] : in[SH + k];
+      out[k] = mine + xchg<1>(send);
+    }
+  } else {
+    // round 1 (mask 2): keep owners with bit1 == mine (o = (h&2) + {0,1})
+    const bool b1 = h & 2, b0 = h & 1;
+    double t[2 * SH];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        const double keep = b1 ? in[(2 + q) * SH + k] : in[q * SH + k];
+        const double send = b1 ? in[q * SH + k] : in[(2 + q) * SH + k];
+        t[q * SH + k] = keep + xchg<2>(send);
+      }
+    // round 2 (mask 1): keep owner o = h
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const double keep = b0 ? t[SH + k] : t[k];
+      const double send = b0 ? t[k] : t[SH + k];
+      out[k] = keep + xchg<1>(send);
+    }
+  }
+}
+
+// All-gather: in[SH] (rows of lane h) -> out[LPC*SH] (all rows, owner-major).
+template <int LPC, int SH>
+__device__ __forceinline__ void all_gather(const double (&in)[SH], double (&out)[LPC * SH], int h) {
+  if constexpr (LPC == 1) {
+#pragma unroll
+    for (int k = 0; k < SH; ++k) out[k] = in[k];
+  } else if constexpr (LPC == 2) {
+    const bool hi = h & 1;
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const double other = xchg<1>(in[k]);
+      out[k] = hi ? other : in[k];
+      out[SH + k] = hi ? in[k] : other;
+    }
+  } else {
+    const bool b0 = h & 1, b1 = h & 2;
+    double t[2 * SH];  // rows of owners (h & 2) + {0, 1}
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const double other = xchg<1>(in[k]);
+      t[k] = b0 ? other : in[k];
+      t[SH + k] = b0 ? in[k] : other;
+    }
+#pragma unroll
+    for (int q = 0; q < 2 * SH; ++q) {
+      const double other = xchg<2>(t[q]);
+      out[q] = b1 ? other : t[q];
+      out[2 * SH + q] = b1 ? t[q] : other;
+    }
+  }
+}
+
+template <int n>
+__device__ __forceinline__ void lds_ld(double (&dst)[n], const double *src) {
+  if constexpr (n % 2 == 0) {
+    const double2 *s2 = reinterpret_cast<const double2 *>(__builtin_assume_aligned(src, 16));
+#pragma unroll
+    for (int k = 0; k < n / 2; ++k) {
+      const double2 v = s2[k];
+      dst[2 * k] = v.x;
+      dst[2 * k + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < n; ++k) dst[k] = src[k];
+  }
+}
+
+template <int n>
+__device__ __forceinline__ void lds_st(double *dst, const double (&src)[n]) {
+  if constexpr (n % 2 == 0) {
+    double2 *d2 = reinterpret_cast<double2 *>(__builtin_assume_aligned(dst, 16));
+#pragma unroll
+    for (int k = 0; k < n / 2; ++k) d2[k] = make_double2(src[2 * k], src[2 * k + 1]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < n; ++k) dst[k] = src[k];
+  }
+}
+
+// row[r0 .. r0+SH) of an S-wide LDS row (clamped to S-1 beyond the end)
+template <int S, int SH, int LPC>
+__device__ __forceinline__ void load_row(double (&dst)[SH], const double *row, int r0) {
+  if constexpr (S % LPC == 0 && SH % 2 == 0 && S % 2 == 0) {
+    lds_ld<SH>(dst, row + r0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const int s = r0 + k < S ? r0 + k : S - 1;
+      dst[k] = row[s];
+    }
+  }
+}
+
+}  // namespace
+
+template <int S, int LPC, int D>
+__global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using LY = SplitLayout<S, LPC>;
+  constexpr int SH = LY::SH;
+  constexpr int NPF = D * (D + 1) / 2;
+  constexpr int LPP = S * LPC;  // lanes per pair
+  const int tid = threadIdx.x;
+  const int NT = p.nwb * 64;
+  const int PPB = NT / LPP;
+  const int SB = p.SB, T = p.T, d = p.d, K = p.K;
+  const int j = blockIdx.x % K;
+  const int i0 = p.i_begin + (blockIdx.x / K) * PPB;
+  const int q = tid / LPP;
+  const int w = tid - q * LPP;
+  const int b = w / LPC;
+  const int h = w - b * LPC;
+  const bool valid = q < PPB;
+  const int i = i0 + q;
+  const bool active = valid && i < p.i_end;
+  const int ic = active ? i : p.i_begin;
+  const bool bvalid = b < SB;
+  const int bc = bvalid ? b : SB - 1;
+  const bool full = p.covmode == kCovFull;
+  const int r0 = h * SH;  // first row owned by this lane
+
+  double *At = lds;              // [S][S]
+  double *AtT = At + S * S;      // [S][S]
+  double *amax = AtT + S * S;    // [S]
+  double *lpi = amax + S;        // [S]
+  double *X = lds + LY::OFF_X + (valid ? q : 0) * LY::XP;   // slab [col][XCS]
+  double *Y = lds + p.off_Y + (valid ? q : 0) * S;
+  double *R = lds + p.off_R;     // K1 staging | lattice [(T-2)][SH][NT]
+  int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
+
+  // ---------------- stage the cluster constants ------------------------------------
+  {
+    const double *la = p.logA + (size_t)j * S * S;
+    if (tid < S) {
+      double mx = la[tid * S];
+      for (int s = 1; s < S; ++s) mx = fmax(mx, la[tid * S + s]);
+      amax[tid] = mx;
+      lpi[tid] = p.logPi[(size_t)j * S + tid];
+    }
+    double *km = R;              // [S][D]
+    double *kP = km + S * D;     // [S][NPF]
+    double *kPT = kP + S * NPF;  // [NPF][S]
+    double *kc = kPT + S * NPF;  // [S]
+    for (int x = tid; x < S * D; x += NT) {
+      const int s = x / D, qd = x - s * D;
+      const double v = p.m[((size_t)j * S + s) * d + (qd < d ? qd : d - 1)];
+      km[x] = qd < d ? v : 0.0;
+    }
+    if (full) {
+      for (int x = tid; x < S * NPF; x += NT) {
+        const int s = x / NPF;
+        int k = x - s * NPF, a = 0;
+        while (k >= D - a) {
+          k -= D - a;
+          ++a;
+        }
+        const int c2 = a + k;
+        const int aa = a < d ? a : d - 1, cc = c2 < d ? c2 : d - 1;
+        const double v = p.P[(((size_t)j * S + s) * d + aa) * d + cc];
+        const double val = (a < d && c2 < d) ? v : 0.0;
+        kP[x] = val;
+        kPT[(x - s * NPF) * S + s] = val;
+      }
+    } else {
+      for (int x = tid; x < S * D; x += NT) {
+        const int s = x / D, qd = x - s * D;
+        const double v = p.P[((size_t)j * S + s) * d + (qd < d ? qd : d - 1)];
+        kP[x] = qd < d ? v : 0.0;
+      }
+    }
+    if (tid < S) kc[tid] = p.c[(size_t)j * S + tid];
+    for (int x = tid; x < PPB; x += NT) F[x] = 0;
+  }
+  __syncthreads();
+  for (int x = tid; x < S * S; x += NT) {
+    const int r = x / S, s = x - r * S;
+    const double a = exp_nonpos(p.logA[(size_t)j * S * S + x] - amax[r]);
+    At[x] = a;
+    AtT[s * S + r] = a;
+  }
+
+  // ---------------- K1: E[k] for rows sigma = r0 + k ---------------------------------------
+  double E[SH];
+  {
+    const double *km = R;
+    const double *kP = km + S * D;
+    const double *kPT = kP + S * NPF;
+    const double *kc = kPT + S * NPF;
+    double mu[D];
+    const double *mub = p.centres + ((size_t)ic * SB + bc) * d;
+#pragma unroll
+    for (int qd = 0; qd < D; ++qd) {
+      const double v = mub[qd < d ? qd : d - 1];
+      mu[qd] = (qd < d && bvalid) ? v : 0.0;
+    }
+    double acc[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) acc[k] = 0.0;
+    if (full) {
+      const double *C = p.covars + ((size_t)ic * SB + bc) * d * d;
+      int kk = 0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) {
+#pragma unroll
+        for (int c2 = a; c2 < D; ++c2, ++kk) {
+          const int aa = a < d ? a : d - 1, cc = c2 < d ? c2 : d - 1;
+          const double v1 = C[aa * d + cc], v2 = C[cc * d + aa];
+          const double cs = (a < d && c2 < d && bvalid) ? (a == c2 ? v1 : v1 + v2) : 0.0;
+          const double *pk = kPT + kk * S;
+#pragma unroll
+          for (int k = 0; k < SH; ++k) {
+            const int r = r0 + k < S ? r0 + k : S - 1;
+            acc[k] = fma(pk[r], cs, acc[k]);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        const int r = r0 + k < S ? r0 + k : S - 1;
+        double x[D];
+#pragma unroll
+        for (int qd = 0; qd < D; ++qd) x[qd] = mu[qd] - km[r * D + qd];
+        const double *ps = kP + r * NPF;
+        double t = 0.0;
+        int k2 = 0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+#pragma unroll
+          for (int c2 = a; c2 < D; ++c2, ++k2) {
+            const double wv = (a == c2) ? x[a] * x[a] : 2.0 * x[a] * x[c2];
+            t = fma(ps[k2], wv, t);
+          }
+        }
+        acc[k] += t;
+      }
+    } else {
+      const double *C = p.covars + ((size_t)ic * SB + bc) * d;
+#pragma unroll
+      for (int qd = 0; qd < D; ++qd) {
+        const double v = C[qd < d ? qd : d - 1];
+        const double cq = (qd < d && bvalid) ? v : 0.0;
+#pragma unroll
+        for (int k = 0; k < SH; ++k) {
+          const int r = r0 + k < S ? r0 + k : S - 1;
+          const double x = mu[qd] - km[r * D + qd];
+          acc[k] = fma(kP[r * D + qd], fma(x, x, cq), acc[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const int r = r0 + k < S ? r0 + k : S - 1;
+      E[k] = (r0 + k < S) ? -0.5 * (d * kLog2PiS + kc[r] + acc[k]) : -INFINITY;
+    }
+  }
+  double arow[S], acol[S];
+  {
+    const double *Ai = p.A + (size_t)ic * SB * SB;
+#pragma unroll
+    for (int be = 0; be < S; ++be) {
+      const int bb = be < SB ? be : SB - 1;
+      const double r1 = Ai[bc * SB + bb], c1 = Ai[bb * SB + bc];
+      const bool ok = bvalid && be < SB;
+      arow[be] = ok ? r1 : 0.0;
+      acol[be] = ok ? c1 : 0.0;
+    }
+  }
+  const double pb0 = p.prior[(size_t)ic * SB + bc];
+  const double pb = bvalid ? pb0 : 0.0;
+  __syncthreads();  // K1 staging is dead from here on
+
+  // ---------------- K2: backward recursion -------------------------------------------------
+  double L[SH];
+#pragma unroll
+  for (int k = 0; k < SH; ++k) L[k] = 0.0;
+  bool bad = false;
+  for (int t = T - 1; t >= 1; --t) {
+    double G[SH], M = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < SH; ++k) M = fmax(M, E[k] + L[k]);
+    M = allmax<LPC>(M);
+#pragma unroll
+    for (int k = 0; k < SH; ++k) G[k] = exp_nonpos((E[k] + L[k]) - M);
+    // partial Z for every owner's rows, then reduce-scatter
+    double Pz[LPC * SH];
+#pragma unroll
+    for (int r = 0; r < LPC * SH; ++r) {
+      const int rr = r < S ? r : S - 1;
+      double ar[SH];
+      load_row<S, SH, LPC>(ar, At + rr * S, r0);
+      double z = 0.0;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
+      Pz[r] = z;
+    }
+    double Z[SH];
+    reduce_scatter<LPC, SH>(Pz, Z, h);
+    double sv[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const bool rv = r0 + k < S;
+      const int r = rv ? r0 + k : S - 1;
+      bad |= rv && !(Z[k] >= kZMinS);
+      const double zz = rv ? Z[k] : 1.0;
+      sv[k] = M + amax[r] + log_pos(zz);
+    }
+    if (t <= T - 2) {
+      double *slot = R + (size_t)(t - 1) * SH * NT + tid;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) slot[k * NT] = G[k];
+    }
+    if (valid) lds_st<SH>(X + b * LY::XCS + r0, sv);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SH; ++k) L[k] = 0.0;
+#pragma unroll
+    for (int be = 0; be < S; ++be) {
+      double xs[SH];
+      lds_ld<SH>(xs, X + be * LY::XCS + r0);
+#pragma unroll
+      for (int k = 0; k < SH; ++k) L[k] = fma(arow[be], xs[k], L[k]);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- K3: termination ----------------------------------------------------------
+  double nu[SH];
+  {
+    double v1[SH], M1 = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      const int r = r0 + k < S ? r0 + k : S - 1;
+      v1[k] = lpi[r] + E[k] + L[k];
+      M1 = fmax(M1, v1[k]);
+    }
+    M1 = allmax<LPC>(M1);
+    double zs = 0.0;
+#pragma unroll
+    for (int k = 0; k < SH; ++k) zs += exp_nonpos(v1[k] - M1);
+    zs = allsum<LPC>(zs);
+    const double s1 = M1 + log_pos(zs);
+#pragma unroll
+    for (int k = 0; k < SH; ++k) nu[k] = pb * exp_nonpos(v1[k] - s1);
+    if (valid) {
+      if (h == 0) Y[b] = pb * s1;
+      lds_st<SH>(X + b * LY::XCS + r0, nu);
+    }
+  }
+  __syncthreads();
+  const size_t pair = (size_t)i * K + j;
+  const size_t lp = (size_t)(i - p.i_buf0) * K + j;
+  if (active) {
+    if (w == 0) {
+      double ll = 0.0;
+      for (int be = 0; be < SB; ++be) ll += Y[be];
+      p.LL[pair] = ll;
+    }
+    if (w < S) {
+      double n1 = 0.0;
+#pragma unroll
+      for (int be = 0; be < S; ++be) n1 += X[be * LY::XCS + w];
+      p.nu1[lp * S + w] = n1;
+    }
+  }
+
+  // ---------------- K4: forward recursion ----------------------------------------------------
+  double tn[SH], H[SH][LPC * SH];
+#pragma unroll
+  for (int k = 0; k < SH; ++k) {
+    tn[k] = nu[k];
+#pragma unroll
+    for (int s = 0; s < LPC * SH; ++s) H[k][s] = 0.0;
+  }
+  for (int t = 1; t < T; ++t) {
+    double G[SH];
+    if (t == T - 1) {
+      double M = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) M = fmax(M, E[k]);
+      M = allmax<LPC>(M);
+#pragma unroll
+      for (int k = 0; k < SH; ++k) G[k] = exp_nonpos(E[k] - M);
+    } else {
+      const double *slot = R + (size_t)(t - 1) * SH * NT + tid;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) G[k] = slot[k * NT];
+    }
+    __syncthreads();  // X holds nu
+    double f[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) f[k] = 0.0;
+#pragma unroll
+    for (int be = 0; be < S; ++be) {
+      double xs[SH];
+      lds_ld<SH>(xs, X + be * LY::XCS + r0);
+#pragma unroll
+      for (int k = 0; k < SH; ++k) f[k] = fma(xs[k], acol[be], f[k]);
+    }
+    // Z recomputed exactly as in the backward pass
+    double Pz[LPC * SH];
+#pragma unroll
+    for (int r = 0; r < LPC * SH; ++r) {
+      const int rr = r < S ? r : S - 1;
+      double ar[SH];
+      load_row<S, SH, LPC>(ar, At + rr * S, r0);
+      double z = 0.0;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
+      Pz[r] = z;
+    }
+    double Z[SH], g[SH];
+    reduce_scatter<LPC, SH>(Pz, Z, h);
+#pragma unroll
+    for (int k = 0; k < SH; ++k) g[k] = (r0 + k < S) ? f[k] * rcp_pos(Z[k]) : 0.0;
+    // nu'(s) = G(s) * sum_r A'(r, s) g(r): partial over my rows r for every s
+    double Pn[LPC * SH];
+#pragma unroll
+    for (int s = 0; s < LPC * SH; ++s) {
+      const int ss = s < S ? s : S - 1;
+      double ac[SH];
+      load_row<S, SH, LPC>(ac, AtT + ss * S, r0);
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) a = fma(ac[k], g[k], a);
+      Pn[s] = a;
+    }
+    double Q[SH];
+    reduce_scatter<LPC, SH>(Pn, Q, h);
+#pragma unroll
+    for (int k = 0; k < SH; ++k) {
+      nu[k] = G[k] * Q[k];
+      tn[k] += nu[k];
+    }
+    double Ga[LPC * SH];
+    all_gather<LPC, SH>(G, Ga, h);
+#pragma unroll
+    for (int k = 0; k < SH; ++k)
+#pragma unroll
+      for (int s = 0; s < LPC * SH; ++s) H[k][s] = fma(g[k], Ga[s], H[k][s]);
+    __syncthreads();  // all reads of X done
+    if (valid) lds_st<SH>(X + b * LY::XCS + r0, nu);
+  }
+
+  // ---------------- outputs -------------------------------------------------------------------
+  if (active && bvalid) {
+#pragma unroll
+    for (int k = 0; k < SH; ++k)
+      if (r0 + k < S) p.tnu[(lp * S + r0 + k) * SB + b] = tn[k];
+  }
+  // sum_xi(r, s) = A'(r, s) * sum_b H_b(r, s): one pair-wide reduction per row r
+#pragma unroll
+  for (int r = 0; r < S; ++r) {
+    __syncthreads();
+    if (valid && h == r / SH) {
+      double hr[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) hr[s] = H[r % SH][s];
+      lds_st<S>(X + b * LY::XCS, hr);
+    }
+    __syncthreads();
+    if (active && w < S) {
+      double acc = 0.0;
+#pragma unroll
+      for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + w];
+      p.xi[(lp * S + r) * S + w] = At[r * S + w] * acc;
+    }
+  }
+  // fallback flags (one per pair)
+  if (bad && active) F[q] = 1;
+  __syncthreads();
+  if (active && w == 0 && F[q]) {
+    const int slot = atomicAdd(p.flag_count, 1);
+    atomicAdd(p.flag_count + 1, 1);
+    p.flag_list[slot] = (int)pair;
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <int S, int LPC, int D>
+static hipError_t launch_split_sld(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  auto *fn = &fb_split_kernel<S, LPC, D>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((fb_split_kernel<S, LPC, D>), dim3(grid), dim3(a.nwb * 64), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int S>
+static hipError_t launch_split_s(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  constexpr int LPC = SplitLPC<S>::value;
+  switch (a.D) {
+    case 2: return launch_split_sld<S, LPC, 2>(a, grid, lds, st);
+    case 4: return launch_split_sld<S, LPC, 4>(a, grid, lds, st);
+    case 8: return launch_split_sld<S, LPC, 8>(a, grid, lds, st);
+    case 16: return launch_split_sld<S, LPC, 16>(a, grid, lds, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  switch (a.S) {
+    case 1: return launch_split_s<1>(a, grid, lds, st);
+    case 2: return launch_split_s<2>(a, grid, lds, st);
+    case 3: return launch_split_s<3>(a, grid, lds, st);
+    case 4: return launch_split_s<4>(a, grid, lds, st);
+    case 5: return launch_split_s<5>(a, grid, lds, st);
+    case 6: return launch_split_s<6>(a, grid, lds, st);
+    case 7: return launch_split_s<7>(a, grid, lds, st);
+    case 8: return launch_split_s<8>(a, grid, lds, st);
+    case 9: return launch_split_s<9>(a, grid, lds, st);
+    case 10: return launch_split_s<10>(a, grid, lds, st);
+    case 11: return launch_split_s<11>(a, grid, lds, st);
+    case 12: return launch_split_s<12>(a, grid, lds, st);
+    case 13: return launch_split_s<13>(a, grid, lds, st);
+    case 14: return launch_split_s<14>(a, grid, lds, st);
+    case 15: return launch_split_s<15>(a, grid, lds, st);
+    case 16: return launch_split_s<16>(a, grid, lds, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+bool split_supported(int S, int SB, int d) {
+  return S >= 1 && S <= kSplitMaxS && SB >= 1 && SB <= S && d >= 1 && d <= 16;
+}
+
+int split_dim_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : 16; }
+
+int split_lpc(int S) { return S <= 4 ? 1 : S <= 8 ? 2 : 4; }
+
+}  // namespace vbhem

@@ -40,6 +40,34 @@ struct StatsArgs {
   double *hatZ, *slabs;
 };
 
+// fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).
+constexpr int kSplitMaxS = 16;
+template <int S>
+struct SplitLPC {
+  static constexpr int value = S <= 4 ? 1 : S <= 8 ? 2 : 4;
+};
+template <int S, int LPC>
+struct SplitLayout {
+  static constexpr int SH = (S + LPC - 1) / LPC;           // rows per lane
+  static constexpr int XCS = (LPC * SH + 1) / 2 * 2 + 2;   // slab column stride (even)
+  static constexpr int XP = S * XCS + 2;                    // per-pair slab
+  static constexpr int HEAD = 2 * S * S + 2 * S;            // At, AtT, amax, lpi
+  static constexpr int OFF_X = (HEAD + 1) / 2 * 2;
+};
+struct SplitArgs {
+  int SB, d, covmode, K, S, T, D, nwb;
+  int i_begin, i_end, i_buf0;
+  int off_Y, off_F, off_R;  // LDS layout (doubles), depends on pairs per block
+  const double *prior, *A, *centres, *covars;
+  const double *logA, *logPi, *m, *P, *c;
+  double *LL, *nu1, *xi, *tnu;
+  int *flag_count, *flag_list;
+};
+bool split_supported(int S, int SB, int d);
+int split_dim_bucket(int d);
+int split_lpc(int S);
+hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
+
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
                            hipStream_t st);

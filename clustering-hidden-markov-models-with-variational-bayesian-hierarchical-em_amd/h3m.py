@@ -179,22 +179,25 @@ def clip_hyps(opt: dict) -> dict:
 
 
 def baseem_init(base: BaseSet, opt: dict, randomb: np.ndarray, randomg: np.ndarray,
-                omega_rand: np.ndarray) -> Posterior:
+                omega_rand: np.ndarray, n_total: Optional[int] = None) -> Posterior:
     """'baseem' initialisation (vbhemhmm_init.m:58-100, initopt.mode='u').
 
     randomb/randomg [K,S]: 0-based base-HMM / state draws (MATLAB randi);
-    omega_rand [K]: uniform draws (MATLAB rand)."""
+    omega_rand [K]: uniform draws (MATLAB rand).  ``n_total`` = Kb when the
+    draws come from a subset of a larger base set."""
     opt = clip_hyps(opt)
     K, S = opt["K"], opt["S"]
-    Kb, d = base.N, base.d
+    Kb, d = (base.N if n_total is None else int(n_total)), base.d
     Nv = opt["Nv"] * Kb
     NLr = Nv / K
     lam = np.full((K, S), opt["lambda0"] + NLr / S)
     v = np.full((K, S), opt["v0"] + NLr / S + 1)
     rb = np.asarray(randomb, dtype=np.int64)
     rg = np.asarray(randomg, dtype=np.int64)
-    cen = base.centres[torch.as_tensor(rb.reshape(-1)), torch.as_tensor(rg.reshape(-1))]
-    cov = base.covars[torch.as_tensor(rb.reshape(-1)), torch.as_tensor(rg.reshape(-1))]
+    ib = torch.as_tensor(rb.reshape(-1), device=base.centres.device)
+    ig = torch.as_tensor(rg.reshape(-1), device=base.centres.device)
+    cen = base.centres[ib, ig]
+    cov = base.covars[ib, ig]
     m = cen.cpu().numpy().reshape(K, S, d)
     cov = cov.cpu().numpy()
     scale = (v.reshape(-1) - d - 1)
@@ -242,7 +245,8 @@ def _digamma(x: torch.Tensor) -> torch.Tensor:
 
 
 def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
-                   device="cpu", exprmt1: bool = False, ragged: bool = False) -> BaseSet:
+                   device="cpu", exprmt1: bool = False, ragged: bool = False,
+                   n_total: Optional[int] = None, i_offset: int = 0) -> BaseSet:
     """Synthetic h3m_b built directly in packed form (use_post=1 semantics).
 
     Ground truth: K HMMs, base i is a noisy copy of GT g = i mod K: means
@@ -251,9 +255,14 @@ def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
     alpha = 1+25*pi, epsilon = 1+250*A, beta = 1+250/Sb, then the
     hmms_to_h3m_hem(use_post=1) transform.  exprmt1=True uses the two GT HMMs
     of Synthetic_experiment/exprmt1_sampledata.m:20-43 instead (Sb=d=2).
-    ragged=True draws per-base state counts in [1, Sb] (zero-padded)."""
-    g = torch.Generator(device="cpu").manual_seed(int(seed))
+    ragged=True draws per-base state counts in [1, Sb] (zero-padded).
+    Generated on ``device``; ``n_total``/``i_offset`` place this block of N
+    bases inside a larger set (omega = 1/n_total, GT index (i_offset+i) mod K)."""
+    device = torch.device(device)
+    gcpu = torch.Generator(device="cpu").manual_seed(int(seed))
+    g = torch.Generator(device=device).manual_seed(int(seed) + 1)
     dt = torch.float64
+    n_total = N if n_total is None else int(n_total)
     if exprmt1:
         G = 2
         gt_prior = torch.tensor([[0.5, 0.5], [0.5, 0.5]], dtype=dt)
@@ -263,36 +272,38 @@ def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
         gt_cov = eye.expand(G, 2, 2, 2).clone() if covmode == COV_FULL else torch.ones(G, 2, 2, dtype=dt)
     else:
         G = K
-        gt_prior = _dirichlet(g, (G,), Sb)
-        gt_A = _dirichlet(g, (G, Sb), Sb)
-        gt_mu = torch.rand((G, Sb, d), generator=g, dtype=dt) * 5.0
+        gt_prior = _dirichlet(gcpu, (G,), Sb)
+        gt_A = _dirichlet(gcpu, (G, Sb), Sb)
+        gt_mu = torch.rand((G, Sb, d), generator=gcpu, dtype=dt) * 5.0
         if covmode == COV_FULL:
-            Lm = torch.randn((G, Sb, d, d), generator=g, dtype=dt)
+            Lm = torch.randn((G, Sb, d, d), generator=gcpu, dtype=dt)
             gt_cov = Lm @ Lm.transpose(-1, -2) / d + 0.5 * torch.eye(d, dtype=dt)
         else:
-            gt_cov = 0.5 + torch.rand((G, Sb, d), generator=g, dtype=dt)
-    gi = torch.arange(N) % G
+            gt_cov = 0.5 + torch.rand((G, Sb, d), generator=gcpu, dtype=dt)
+    gt_prior, gt_A, gt_mu, gt_cov = (x.to(device) for x in (gt_prior, gt_A, gt_mu, gt_cov))
+    gi = (torch.arange(N, device=device) + int(i_offset)) % G
     alpha = 1.0 + 25.0 * gt_prior[gi]
     eps = 1.0 + 250.0 * gt_A[gi]
     beta = 1.0 + 250.0 / Sb
     prior = torch.exp(_digamma(alpha) - _digamma(alpha.sum(-1, keepdim=True)))
     A = torch.exp(_digamma(eps) - _digamma(eps.sum(-1, keepdim=True)))
-    centres = gt_mu[gi] + 0.1 * torch.randn((N, Sb, d), generator=g, dtype=dt)
+    centres = gt_mu[gi] + 0.1 * torch.randn((N, Sb, d), generator=g, dtype=dt, device=device)
     covars = ((beta + 1.0) / beta) * gt_cov[gi]
-    nstates = torch.full((N,), Sb, dtype=torch.int32)
+    nstates = torch.full((N,), Sb, dtype=torch.int32, device=device)
     if ragged and Sb > 1:
-        nstates = torch.randint(1, Sb + 1, (N,), generator=g, dtype=torch.int32)
-        mask = torch.arange(Sb)[None, :] < nstates[:, None].long()
+        nstates = torch.randint(1, Sb + 1, (N,), generator=g, dtype=torch.int32, device=device)
+        mask = torch.arange(Sb, device=device)[None, :] < nstates[:, None].long()
         prior = prior * mask
         A = A * mask[:, :, None] * mask[:, None, :]
         centres = centres * mask[:, :, None]
         if covmode == COV_FULL:
-            covars = torch.where(mask[:, :, None, None], covars, torch.eye(d, dtype=dt).expand_as(covars))
+            covars = torch.where(mask[:, :, None, None], covars,
+                                 torch.eye(d, dtype=dt, device=device).expand_as(covars))
         else:
             covars = torch.where(mask[:, :, None], covars, torch.ones_like(covars))
-    omega = torch.full((N,), 1.0 / N, dtype=dt)
+    omega = torch.full((N,), 1.0 / n_total, dtype=dt, device=device)
     return BaseSet(nstates, prior.contiguous(), A.contiguous(), centres.contiguous(),
-                   covars.contiguous(), omega, covmode).to(device)
+                   covars.contiguous(), omega, covmode)
 
 
 def _dirichlet(g: torch.Generator, batch, n: int) -> torch.Tensor:
@@ -301,17 +312,29 @@ def _dirichlet(g: torch.Generator, batch, n: int) -> torch.Tensor:
     return e / e.sum(-1, keepdim=True)
 
 
-def synth_workload(name: str, seed: Optional[int] = None, device="cpu", N: Optional[int] = None):
+def synth_workload(name: str, seed: Optional[int] = None, device="cpu", N: Optional[int] = None,
+                   shard: Optional[tuple] = None, ragged: bool = False):
     """(BaseSet, Posterior, options) for a named config; seed = 1001 + index
-    (BASELINE.md).  ``N`` overrides the number of base HMMs (sub-sampling)."""
+    (BASELINE.md).  ``N`` overrides the number of base HMMs (sub-sampling).
+    ``shard=(lo, hi)`` generates only bases [lo, hi) of the N (seeded per
+    shard); the Posterior is identical for every shard (baseem over the first
+    min(N, 4096) bases of shard 0's seed)."""
     cfg = CONFIGS[name]
     idx = list(CONFIGS).index(name) + 1
     seed = 1001 + idx if seed is None else seed
     n = cfg["N"] if N is None else N
-    base = synth_base_set(n, cfg["K"], cfg["Sb"], cfg["d"], cfg["covmode"], seed, device=device,
-                          exprmt1=(name == "C2"))
+    lo, hi = (0, n) if shard is None else shard
+    args = (cfg["K"], cfg["Sb"], cfg["d"], cfg["covmode"])
+    ex = name == "C2"
+    base = synth_base_set(hi - lo, *args, seed + 7919 * lo, device=device, exprmt1=ex,
+                          ragged=ragged, n_total=n, i_offset=lo)
     opt = default_options(cfg["K"], cfg["S"], cfg["d"], tau=cfg["tau"], Nv=cfg["Nv"],
                           covmode=cfg["covmode"], **cfg["opt"])
-    rb, rg, om = baseem_draws(base, cfg["K"], cfg["S"], seed)
-    post = baseem_init(base, opt, rb, rg, om)
+    if lo == 0 and (hi - lo) >= min(n, 4096):
+        init = base
+    else:
+        init = synth_base_set(min(n, 4096), *args, seed, device=device, exprmt1=ex, ragged=ragged,
+                              n_total=n)
+    rb, rg, om = baseem_draws(init, cfg["K"], cfg["S"], seed)
+    post = baseem_init(init, opt, rb, rg, om, n_total=n)
     return base, post, opt

@@ -116,6 +116,15 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
  * log-sum-exp fell below its safe range.  Synchronises `stream`. */
 int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
 
+/* Kernel timing for benchmarking/profiling (not for graph capture): while
+ * enabled, hipEvents are recorded on the launch stream around every
+ * fb_pairs_kernel and stats_kernel launch of this process.  vbhem_timing_read
+ * synchronises on them, returns the summed elapsed milliseconds, the launch
+ * counts and the number of (i,j) pairs the fb launches covered, and resets. */
+int vbhem_timing_enable(int on);
+int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs,
+                      double *stats_ms, long long *stats_launches);
+
 const char *vbhem_last_error(void);
 const char *vbhem_version(void);
 
