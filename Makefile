@@ -9,7 +9,7 @@ SRCS     := $(PKG)/csrc/vbhem_kernels.hip $(PKG)/csrc/vbhem_fb_split.hip $(PKG)/
 HDRS     := include/vbhem_estep.h $(PKG)/csrc/vbhem_internal.h $(PKG)/csrc/vbhem_math.h
 OBJS     := $(patsubst $(PKG)/csrc/%.hip,$(LIBDIR)/%.o,$(SRCS))
 
-all: lib oracle
+all: lib oracle mex mathcheck
 
 lib: $(LIBDIR)/libvbhem_estep.so
 
@@ -32,8 +32,14 @@ tests/mxshim/libmxshim.so: tests/mxshim/mxshim.c tests/mxshim/mex.h
 $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so: integration/vbhem_hmm_bwd_fwd_mex.c include/vbhem_estep.h $(LIBDIR)/libvbhem_estep.so tests/mxshim/mex.h
 	gcc -O2 -fPIC -shared -Iinclude -Itests/mxshim -o $@ $< -L$(LIBDIR) -lvbhem_estep -Wl,-rpath,'$$ORIGIN'
 
+# test-only: the restricted-domain exp/log/rcp of vbhem_math.h, host and device
+mathcheck: tests/mathcheck/libmathcheck.so
+
+tests/mathcheck/libmathcheck.so: tests/mathcheck/mathcheck.hip $(PKG)/csrc/vbhem_math.h
+	$(HIPCC) $(HIPFLAGS) -I$(PKG)/csrc -shared -o $@ $<
+
 clean:
-	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so tests/mxshim/libmxshim.so
+	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so tests/mxshim/libmxshim.so tests/mathcheck/libmathcheck.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle mex clean
+.PHONY: all lib oracle mex mathcheck clean

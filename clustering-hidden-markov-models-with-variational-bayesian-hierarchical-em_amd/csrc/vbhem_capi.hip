@@ -374,7 +374,8 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
                       size_t workspace_bytes, void *stream) {
   int rc = check_inputs(base, clus, T);
   if (rc != VBHEM_OK) return rc;
-  if (!tildeN_dev || !logOmega_dev || !stats_dev || !hatZ_dev || !LL_elbo_dev)
+  if (!logOmega_dev || !stats_dev ||
+      (base->N > 0 && (!tildeN_dev || !hatZ_dev || !LL_elbo_dev)))
     return fail(VBHEM_ERR_ARG, "null fused argument");
   FusedWs w;
   const size_t need = carve_fused(nullptr, base, clus, T, w);

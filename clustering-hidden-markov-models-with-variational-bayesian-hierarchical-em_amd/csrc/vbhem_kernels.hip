@@ -582,6 +582,10 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
   for (int i = b0; i < b1; ++i) {
     // -- responsibilities for base i (wave 0) --------------------------------
     if (wave == 0) {
+      // log_Z = tilde_N .* (logOmega + L_elbo) is rounded before the shift, as in
+      // step_fc.m:275-276 (an fma-contracted shift would let the winning entry
+      // exceed 1 by ~ulp(log_Z)).
+#pragma clang fp contract(off)
       const double tn = p.tildeN[i];
       double mx = -INFINITY;
       for (int j = lane; j < K; j += 64) mx = fmax(mx, tn * (p.logOmega[j] + p.LL[(size_t)i * K + j]));

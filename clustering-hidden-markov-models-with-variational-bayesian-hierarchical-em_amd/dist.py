@@ -4,7 +4,7 @@ Each (base i, cluster j) pair is independent and hat_Z(i,:) depends only on
 L_elbo(i,:) (vbhem_h3m_c_step_fc.m:275-276), so rank r owns a contiguous block
 of base HMMs and everything up to the packed statistics vector is local.  The
 only exchange is ONE all-reduce (sum, fp64) of that vector per EM iteration
-(84 KB at K=16,S=8,d=8); cluster posteriors are replicated and every rank
+(6,930 doubles = 55 KB at K=16,S=8,d=8); cluster posteriors are replicated and every rank
 runs the identical host M-step.  On ROCm the "nccl" backend is RCCL (xGMI);
 "gloo" serves CPU tests.
 """

@@ -1,0 +1,72 @@
+"""Multi-rank EM (vbhem_amd.dist + vbhem_amd.em) on the CPU with gloo.
+
+Each rank owns a contiguous shard of base HMMs and runs the E-step on it (the
+oracle stand-in engine here, the HIP engine on GPUs); the packed statistics are
+SUM-all-reduced once per iteration.  All ranks must end with identical
+posteriors, equal to a single-process run up to summation order.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from cases import post_dict  # noqa: F401  (ensures tests/ is importable in workers)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_em(name, N, world, rank, outdir, port):
+    import torch
+    import torch.distributed as dist
+
+    import pkgload
+    from oracle_engine import OracleEngine
+
+    vb = pkgload.load()
+    from vbhem_amd.dist import make_allreduce, shard_range
+    from vbhem_amd.em import vbhem_h3m_c_step_fc
+
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    base, P, opt = vb.synth_workload(name, N=N)
+    lo, hi = shard_range(N, rank, world)
+    eng = OracleEngine(base.shard(lo, hi), P.K, P.S, opt["tau"], nthreads=1)
+    res = vbhem_h3m_c_step_fc(P, eng, dict(opt, max_iter=8), total_N=N,
+                              allreduce=make_allreduce())
+    np.savez(os.path.join(outdir, f"r{rank}_w{world}.npz"), LogLs=np.array(res.LogLs),
+             m=res.post.m, W=res.post.W, alpha=res.post.alpha, epsilon=res.post.epsilon,
+             hatZ=res.hatZ.numpy(), lo=lo, hi=hi)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    del torch
+
+
+def _worker(rank, name, N, world, outdir, port):
+    _run_em(name, N, world, rank, outdir, port)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_gloo_two_ranks_match_single_process(tmp_path, name):
+    N = 30
+    _run_em(name, N, 1, 0, str(tmp_path), 0)
+    port = _free_port()
+    mp.spawn(_worker, args=(name, N, 2, str(tmp_path), port), nprocs=2, join=True)
+    single = np.load(tmp_path / "r0_w1.npz")
+    r0 = np.load(tmp_path / "r0_w2.npz")
+    r1 = np.load(tmp_path / "r1_w2.npz")
+    for k in ("LogLs", "m", "W", "alpha", "epsilon"):
+        np.testing.assert_array_equal(r0[k], r1[k])         # replicated host math
+        np.testing.assert_allclose(r0[k], single[k], rtol=1e-10, err_msg=k)
+    hz = np.concatenate([r0["hatZ"], r1["hatZ"]])
+    np.testing.assert_allclose(hz, single["hatZ"], rtol=1e-9, atol=1e-300)
+    assert int(r0["hi"]) == int(r1["lo"])

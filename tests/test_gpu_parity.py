@@ -1,0 +1,259 @@
+"""GPU parity of the HIP E-step (through the C-ABI) against the oracle.
+
+* per-pair MEX outputs (vbhem_estep_pairs) over every shape in cases.SHAPES;
+* fused statistics / hat_Z / L_elbo (vbhem_estep_fused) over the same shapes;
+* the exact fallback (forced by an adversarial cluster whose factorised
+  log-sum-exp normaliser underflows);
+* the host-pointer entry point the MEX gateway uses;
+* full-size (C4, N = 100,000) size-independent properties: determinism, shard
+  additivity, normalisation and mass rules, and a sampled oracle comparison.
+
+Tolerances: per-pair outputs RTOL_PAIRS = 1e-10 (normwise relative);
+statistics 1e-9; hat_Z / ELBO the north-star 1e-5 (conftest.py).
+"""
+import ctypes
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from cases import SHAPES, make_case
+from conftest import RTOL_NORTH_STAR, RTOL_PAIRS, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PAIR_KEYS = ("LL_elbo", "sum_nu_1", "sum_xi", "emit_pr", "emit_mu", "emit_Mu")
+
+
+def engine(vb, base_np, consts, T, K=None, S=None):
+    from vbhem_amd.estep import EStepEngine
+    K0, S0 = consts["logPi"].shape
+    eng = EStepEngine(vb.BaseSet.from_numpy(base_np), K0, S0, T, device=DEV)
+    eng.set_clusters(consts)
+    return eng
+
+
+def seed_of(name):
+    return zlib.crc32(name.encode()) % 1000
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
+def test_pairs_match_oracle(vb, vo, shape):
+    name, N, K, S, Sb, d, cov, T, ragged = shape
+    cs = make_case(N, K, S, Sb, d, cov, seed=seed_of(name), ragged=ragged, tau=T)
+    ref = vo.c_estep_pairs(cs["base"], cs["consts"], T, nthreads=4, want_tnu=True)
+    eng = engine(vb, cs["base"], cs["consts"], T)
+    got = eng.pairs(want_tnu=True)
+    torch.cuda.synchronize()
+    for k in PAIR_KEYS + ("sum_t_nu",):
+        e = rel_err(got[k].cpu().numpy(), ref[k])
+        assert e < RTOL_PAIRS, (name, k, e)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
+def test_fused_matches_oracle(vb, vo, shape):
+    name, N, K, S, Sb, d, cov, T, ragged = shape
+    cs = make_case(N, K, S, Sb, d, cov, seed=seed_of(name) + 1, ragged=ragged, tau=T)
+    base, consts = cs["base"], cs["consts"]
+    pairs = vo.c_estep_pairs(base, consts, T, nthreads=4)
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, pairs, cov)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    vec = eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy()
+    got = vb.host.unpack_stats(vec, K, S, d, cov)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert rel_err(got[k], st[k]) < 1e-9, (name, k, rel_err(got[k], st[k]))
+    Lt1 = float((Z * pairs["LL_elbo"]).sum())
+    Lt7 = float((hz * np.log(hz)).sum())
+    assert abs(got["Lt1"] - Lt1) <= 1e-10 * abs(Lt1)
+    assert abs(got["Lt7"] - Lt7) <= 1e-9 * abs(Lt7) + 1e-9
+    assert rel_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
+    assert rel_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
+def adversarial_case(cov=1, S=4, Sb=4, d=3, N=4, K=3, T=6):
+    """Cluster 0's transitions put all mass on sigma+1 while its emissions put
+    all mass on state 0: the factorised normaliser Z ~ e^-600 underflows the
+    safe range (kZMin = 1e-200), so those pairs take the exact fallback."""
+    cs = make_case(N, K, S, Sb, d, cov, seed=99, tau=T)
+    c = {k: np.array(v, copy=True) for k, v in cs["consts"].items()}
+    lA = np.full((S, S), -600.0)
+    for r in range(S):
+        lA[r, (r + 1) % S] = 0.0
+    c["logA"][0] = lA
+    c["c"][0] = 1200.0
+    c["c"][0, 0] = 0.0
+    return cs, c
+
+
+@pytest.mark.parametrize("cov", [0, 1])
+def test_exact_fallback_pairs(vb, vo, cov):
+    cs, consts = adversarial_case(cov)
+    T = cs["T"]
+    ref = vo.c_estep_pairs(cs["base"], consts, T, want_tnu=True)
+    eng = engine(vb, cs["base"], consts, T)
+    got = eng.pairs(want_tnu=True)
+    nfb = eng.fallback_count()
+    assert nfb > 0
+    for k in PAIR_KEYS + ("sum_t_nu",):
+        assert rel_err(got[k].cpu().numpy(), ref[k]) < RTOL_PAIRS, k
+
+
+def test_exact_fallback_fused(vb, vo):
+    cs, consts = adversarial_case(1)
+    base, T = cs["base"], cs["T"]
+    N, K = base["prior"].shape[0], consts["logPi"].shape[0]
+    S, d = consts["logPi"].shape[1], base["centres"].shape[2]
+    pairs = vo.c_estep_pairs(base, consts, T)
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, pairs, 1)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
+    assert eng.fallback_count() > 0
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert rel_err(got[k], st[k]) < 1e-9, k
+
+
+def test_host_pointer_entry_point(vb, vo, capi_lib):
+    """vbhem_estep_pairs_host (what the MEX gateway calls): host arrays in/out."""
+    from vbhem_amd import _capi
+    cs = make_case(5, 3, 4, 3, 3, 1, seed=12, ragged=True, tau=7)
+    base, consts, T = cs["base"], cs["consts"], 7
+    N, K, S, SB, d = 5, 3, 4, 3, 3
+    keep = {k: np.ascontiguousarray(base[k], dtype=np.float64)
+            for k in ("prior", "A", "centres", "covars")}
+    ns = np.ascontiguousarray(base["nstates"], dtype=np.int32)
+    ck = {k: np.ascontiguousarray(consts[k], dtype=np.float64) for k in ("logA", "logPi", "m", "P", "c")}
+    b = _capi.BaseT(N, SB, d, 1, ns.ctypes.data, keep["prior"].ctypes.data, keep["A"].ctypes.data,
+                    keep["centres"].ctypes.data, keep["covars"].ctypes.data)
+    c = _capi.ClusterT(K, S, *[ck[k].ctypes.data for k in ("logA", "logPi", "m", "P", "c")])
+    out = dict(LL_elbo=np.zeros((N, K)), sum_nu_1=np.zeros((N, K, S)), emit_pr=np.zeros((N, K, S)),
+               emit_mu=np.zeros((N, K, S, d)), emit_Mu=np.zeros((N, K, S, d, d)),
+               sum_xi=np.zeros((N, K, S, S)))
+    rc = capi_lib.vbhem_estep_pairs_host(0, ctypes.byref(b), ctypes.byref(c), T,
+                                         *[out[k].ctypes.data for k in ("LL_elbo", "sum_nu_1", "emit_pr",
+                                                                        "emit_mu", "emit_Mu", "sum_xi")])
+    assert rc == 0, capi_lib.vbhem_last_error()
+    ref = vo.c_estep_pairs(base, consts, T)
+    for k in PAIR_KEYS:
+        assert rel_err(out[k], ref[k]) < RTOL_PAIRS, k
+
+
+def test_side_stream_and_timing(vb, vo):
+    from vbhem_amd import _capi
+    cs = make_case(64, 4, 3, 3, 2, 1, seed=13, tau=10)
+    eng = engine(vb, cs["base"], cs["consts"], 10)
+    ref = vo.c_estep_pairs(cs["base"], cs["consts"], 10)
+    _capi.timing_enable(True)
+    try:
+        s = torch.cuda.Stream(device=DEV)
+        with torch.cuda.stream(s):
+            got = eng.pairs()
+        s.synchronize()
+        t = _capi.timing_read()
+    finally:
+        _capi.timing_enable(False)
+    assert t["fb_launches"] >= 1 and t["fb_pairs"] == 64 * 4 and t["fb_ms"] > 0
+    assert rel_err(got["LL_elbo"].cpu().numpy(), ref["LL_elbo"]) < RTOL_PAIRS
+
+
+def test_empty_shard(vb):
+    cs = make_case(3, 2, 3, 3, 2, 1, seed=1)
+    base = {k: (v[:0] if isinstance(v, np.ndarray) else v) for k, v in cs["base"].items()}
+    eng = engine(vb, base, cs["consts"], 5)
+    eng.set_log_omega(np.zeros(2))
+    eng.stats.fill_(7.0)                 # the output must be overwritten with zeros
+    vec = eng.fused(torch.zeros(0, dtype=torch.float64, device=DEV)).cpu().numpy()
+    assert np.all(vec == 0)
+    out = eng.pairs()
+    assert out["LL_elbo"].shape == (0, 2)
+
+
+# ----------------------------------------------------------------------------
+# full size: C4 (N = 100,000, K = 16, S = Sb = d = 8, full covariances, tau = 10)
+# ----------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c4_full(vb):
+    from vbhem_amd.em import tilde_n
+    from vbhem_amd.estep import EStepEngine
+    base, P, opt = vb.synth_workload("C4", device=DEV)
+    eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+    consts = vb.host.cluster_constants(P, 1)
+    eng.set_clusters(consts)
+    eng.set_log_omega(vb.host.log_omega_tilde(P.alpha))
+    tN = tilde_n(eng, opt["Nv"], base.N)
+    return dict(base=base, P=P, opt=opt, eng=eng, consts=consts, tN=tN)
+
+
+def test_c4_deterministic(c4_full):
+    eng, tN = c4_full["eng"], c4_full["tN"]
+    a = eng.fused(tN).clone()
+    hz_a = eng.hatZ.clone()
+    b = eng.fused(tN).clone()
+    assert torch.equal(a, b)
+    assert torch.equal(hz_a, eng.hatZ)
+    assert eng.fallback_count() == 0
+
+
+def test_c4_shard_additivity(vb, c4_full):
+    """Shards combine by summation (the multi-GPU all-reduce contract)."""
+    from vbhem_amd.estep import EStepEngine
+    base, P, opt, tN = c4_full["base"], c4_full["P"], c4_full["opt"], c4_full["tN"]
+    full = c4_full["eng"].fused(tN).clone()
+    acc = torch.zeros_like(full)
+    N = base.N
+    for lo, hi in ((0, 37_123), (37_123, N)):
+        e = EStepEngine(base.shard(lo, hi), P.K, P.S, opt["tau"], device=DEV)
+        e.set_clusters(c4_full["consts"])
+        e.set_log_omega(vb.host.log_omega_tilde(P.alpha))
+        acc += e.fused(tN[lo:hi])
+        del e
+    assert rel_err(acc.cpu().numpy(), full.cpu().numpy()) < 1e-12
+
+
+def test_c4_normalisation_and_mass(vb, c4_full):
+    eng, tN, P = c4_full["eng"], c4_full["tN"], c4_full["P"]
+    vec = eng.fused(tN).cpu().numpy()
+    st = vb.host.unpack_stats(vec, P.K, P.S, 8, 1)
+    hz = eng.hatZ.cpu().numpy()
+    # log_Z = tilde_N (logOmega + L_elbo) ~ 1e5..1e6 carries ~1e-11 absolute rounding,
+    # so rows sum to 1 within ~1e-12 (the oracle behaves the same)
+    np.testing.assert_allclose(hz.sum(1), 1.0, rtol=1e-10)
+    assert abs(st["Nj"].sum() - tN.sum().item()) <= 1e-10 * tN.sum().item()
+    assert np.isfinite(vec).all()
+    # symmetric second moments, positive occupancies
+    assert (st["Nr"] >= 0).all()
+    LL = eng.LL.cpu().numpy()
+    assert np.isfinite(LL).all() and (LL < 0).all()
+
+
+def test_c4_sampled_oracle(vb, vo, c4_full):
+    eng, base, consts = c4_full["eng"], c4_full["base"], c4_full["consts"]
+    eng.fused(c4_full["tN"])
+    LL = eng.LL.cpu().numpy()
+    idx = np.random.default_rng(0).choice(base.N, 48, replace=False)
+    sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == base.N else v)
+           for k, v in base.shard(0, base.N).numpy().items()}
+    ref = vo.c_estep_pairs(sub, consts, c4_full["opt"]["tau"], nthreads=8)
+    assert rel_err(LL[idx], ref["LL_elbo"]) < RTOL_PAIRS
+
+
+def test_c4_em_iterations_vs_oracle_sample(vb, vo):
+    """Three EM iterations on a 2,000-base C4 slice: GPU EM vs oracle EM."""
+    from vbhem_amd.em import vbhem_h3m_c_step_fc
+    from vbhem_amd.estep import EStepEngine
+    from cases import post_dict
+    base, P, opt = vb.synth_workload("C4", N=2000)
+    opt = dict(opt, max_iter=3)
+    eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+    res = vbhem_h3m_c_step_fc(P, eng, opt)
+    ref = vo.em_step_fc(post_dict(P), base.numpy(), opt)
+    np.testing.assert_allclose(res.LogLs, ref["LogLs"], rtol=RTOL_NORTH_STAR)
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert rel_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, k
+    assert rel_err(res.hatZ.cpu().numpy(), ref["hat_Z"]) < RTOL_NORTH_STAR

@@ -1,0 +1,59 @@
+"""Restricted-domain fp64 exp/log/reciprocal of csrc/vbhem_math.h (the
+transcendentals of the recursions) against libm: <= 1 ulp on their domains.
+Host build on the CPU; the gfx950 build (v_rcp_f64 seed) on the GPU."""
+import ctypes
+
+import numpy as np
+import pytest
+
+N = 400_000
+
+
+def _samples():
+    rng = np.random.default_rng(123)
+    # exp(-x): x in [0, 700] (log-uniform and uniform); log/rcp: z in [1e-200, 1e3]
+    x = np.concatenate([rng.uniform(0, 700, N // 4), 10 ** rng.uniform(-18, np.log10(700), N // 4),
+                        10 ** rng.uniform(-200, 3, N // 4), rng.uniform(0.5, 2.0, N // 4)])
+    x[:4] = [1e-300, 0.5, 1.0, 2.0]
+    return np.ascontiguousarray(x)
+
+
+def _run(fn, x):
+    dp = ctypes.POINTER(ctypes.c_double)
+    e, l, r = (np.zeros_like(x) for _ in range(3))
+    rc = fn(len(x), x.ctypes.data_as(dp), e.ctypes.data_as(dp), l.ctypes.data_as(dp),
+            r.ctypes.data_as(dp))
+    return rc, e, l, r
+
+
+def _ulps(a, b):
+    return np.abs(a - b) / np.spacing(np.abs(b))
+
+
+def _check(x, e, l, r):
+    m = x <= 700
+    assert _ulps(e[m], np.exp(-x[m])).max() <= 1.0
+    pos = x >= 1e-200
+    assert _ulps(l[pos], np.log(x[pos])).max() <= 1.0
+    assert _ulps(r[pos], 1.0 / x[pos]).max() <= 1.0
+    assert l[2] == 0.0 and e[2] == np.exp(-1.0)
+
+
+def test_host_build(mathcheck):
+    x = _samples()
+    rc, e, l, r = _run(mathcheck.mathcheck_host, x)
+    _check(x, e, l, r)
+
+
+def test_exp_clamps_far_tail(mathcheck):
+    x = np.array([745.0, 800.0, 1e4, 1e300])
+    rc, e, l, r = _run(mathcheck.mathcheck_host, x)
+    assert (e <= 5e-324).all() and (e >= 0).all()
+
+
+@pytest.mark.gpu
+def test_device_build(mathcheck):
+    x = _samples()
+    rc, e, l, r = _run(mathcheck.mathcheck_device, x)
+    assert rc == 0
+    _check(x, e, l, r)
