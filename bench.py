@@ -56,6 +56,29 @@ def fb_bytes_per_pair(S, Sb, d, covmode, K):
     return base / K + out
 
 
+def committed_traffic(config, N, world, split):
+    """HBM bytes per launch of the E-step kernel from the newest committed PMC
+    summary for this config (profiles/rNN_<config>.json, made by
+    scripts/profile.sh + scripts/prof_summary.py; FETCH_SIZE x2 + WRITE_SIZE per
+    MI355X_MICROARCH.md).  The counters cannot be collected inside the timed
+    run, so the value is read back here; None when no summary matches."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config.lower()}.json")))
+    want = "vbhem::fb_split_kernel" if split else "vbhem::fb_pairs_kernel"
+    for path in reversed(cands):
+        try:
+            with open(path) as f:
+                summ = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if summ.get("N") not in (None, N) or summ.get("n_gpus", 1) != world:
+            continue
+        for name, k in summ.get("kernels", {}).items():
+            if name.startswith(want) and "hbm_bytes_per_launch" in k:
+                return k["hbm_bytes_per_launch"]["traffic"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(vo, base_np, consts, T, N_total, K, target_s):
     """Time the oracle's C port of mex.c (1 thread) + responsibilities + stats
     on a bounded sample of bases and scale linearly to N_total."""
@@ -174,6 +197,8 @@ def main():
     achieved = fpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e12
     bpp = fb_bytes_per_pair(S, Sb, d, cov, K)
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
+    split = S <= 16 and Sb <= S and d <= 16
+    traffic, traffic_src = committed_traffic(args.config, N, world, split)
     res = {
         "metric": METRIC,
         "value": args.steps / dt,
@@ -199,8 +224,9 @@ def main():
             "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP64_TFLOPS,
-            "traffic": None,
-            "kernel": "fb_pairs_kernel",
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": "fb_split_kernel" if split else "fb_pairs_kernel",
             "kernel_ms": fb_launch_ms,
             "flops_per_pair": fpp,
             "pairs_per_launch": pairs_per_launch,

@@ -693,13 +693,26 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
   }
 }
 
+// 256 threads = 32 columns x 8 slab partitions: partition p sums slabs
+// p, p+8, p+16, ... (coalesced 256-B rows), then the 8 partials are added in
+// fixed order -- deterministic, and ~slab_len/32 blocks fill the chip.
+constexpr int kFinalCols = 32, kFinalParts = 8;
 __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab,
                                                           int slab_len, double *out) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= slab_len) return;
+  __shared__ double part[kFinalParts][kFinalCols];
+  const int c = threadIdx.x % kFinalCols, p = threadIdx.x / kFinalCols;
+  const int x = blockIdx.x * kFinalCols + c;
   double acc = 0.0;
-  for (int c = 0; c < nslab; ++c) acc += slabs[(size_t)c * slab_len + x];
-  out[x] = acc;
+  if (x < slab_len)
+    for (int k = p; k < nslab; k += kFinalParts) acc += slabs[(size_t)k * slab_len + x];
+  part[p][c] = acc;
+  __syncthreads();
+  if (p == 0 && x < slab_len) {
+    double s = part[0][c];
+#pragma unroll
+    for (int q = 1; q < kFinalParts; ++q) s += part[q][c];
+    out[x] = s;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -752,7 +765,7 @@ hipError_t launch_stats(const StatsArgs &a, int nchunk, int ntg, size_t lds, hip
 
 hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
                               hipStream_t st) {
-  hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + 255) / 256), dim3(256), 0, st, slabs,
+  hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + kFinalCols - 1) / kFinalCols), dim3(256), 0, st, slabs,
                      nslab, slab_len, out);
   return hipGetLastError();
 }
