@@ -50,7 +50,7 @@ constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
 constexpr int kExactThreads = 256;                // fallback kernel threads
 constexpr size_t kGroupBudget = (size_t)2 << 30;  // per-pair buffers per group (fused)
-constexpr int kMaxSlabs = 1024;
+constexpr int kMaxSlabs = 512;    // statistics chunks (= resp/stats blocks per group)
 
 inline int odd_up(int x) { return (x % 2 == 0) ? x + 1 : x; }
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -222,7 +222,7 @@ struct FusedWs {
   int nslab;
   int slab_len;
   int *flags;
-  double *scratch, *nu1, *xi, *tnu, *slabs;
+  double *scratch, *nu1, *xi, *tnu, *Z, *slabs;
 };
 
 size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, FusedWs &w) {
@@ -239,6 +239,7 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.nu1 = cv.take<double>(g * K * S);
   w.xi = cv.take<double>(g * K * S * S);
   w.tnu = cv.take<double>(g * K * S * SB);
+  w.Z = cv.take<double>(g * K);
   w.slabs = cv.take<double>((size_t)w.nslab * w.slab_len);
   return cv.off + 256;
 }
@@ -384,25 +385,19 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   carve_fused(workspace_dev, base, clus, T, w);
   hipStream_t st = static_cast<hipStream_t>(stream);
 
-  // stats kernel geometry
+  // statistics kernels' geometry
   const int K = clus->K, S = clus->S, SB = base->SB, d = base->d;
   vbhem::StatsArgs sa{};
-  sa.K = K; sa.S = S; sa.SB = SB; sa.SBp = (SB + 3) / 4 * 4; sa.d = d; sa.covmode = base->covmode;
+  sa.K = K; sa.S = S; sa.SB = SB; sa.d = d; sa.covmode = base->covmode;
   sa.NU = (int)vbhem_stats_nu(d, base->covmode);
-  sa.AST = odd_up(sa.SBp);
-  const int NT = (sa.NU + 15) / 16;
-  sa.UST = NT * 16;
-  const int R = K * S, MT = (R + 15) / 16;
-  sa.ntiles = MT * NT;
   sa.slab_len = w.slab_len;
   sa.centres = base->centres; sa.covars = base->covars; sa.LL = LL_elbo_dev;
   sa.nu1 = w.nu1; sa.xi = w.xi; sa.tnu = w.tnu; sa.tildeN = tildeN_dev; sa.logOmega = logOmega_dev;
-  sa.hatZ = hatZ_dev; sa.slabs = w.slabs;
-  const size_t slds = ((size_t)R * sa.AST + (size_t)sa.SBp * sa.UST + 2 * (size_t)K + (size_t)K * S +
-                       (size_t)K * S * S + 2) * sizeof(double);
-  if (slds > kLdsLimit)
-    return fail(VBHEM_ERR_UNSUPPORTED, "statistics tile does not fit in LDS (K*S too large)");
-  const int ntg = (sa.ntiles + vbhem::stats_tiles_per_block() - 1) / vbhem::stats_tiles_per_block();
+  sa.Z = w.Z; sa.hatZ = hatZ_dev; sa.slabs = w.slabs;
+  size_t slds = 0;
+  int ngroups = 1;
+  if (!vbhem::plan_stats(sa, slds, ngroups))
+    return fail(VBHEM_ERR_UNSUPPORTED, "statistics tile does not fit (S or d too large)");
 
   hipError_t e = hipMemsetAsync(w.slabs, 0, sizeof(double) * (size_t)w.nslab * w.slab_len, st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(slabs)");
@@ -419,7 +414,9 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     const int nchunk = std::min(w.nslab, g1 - g0);
     hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
-    e = vbhem::launch_stats(sa, nchunk, ntg, slds, st);
+    e = vbhem::launch_resp(sa, nchunk, st);
+    if (e != hipSuccess) return hip_fail(e, "resp_kernel");
+    e = vbhem::launch_stats(sa, nchunk, ngroups, slds, st);
     if (e != hipSuccess) return hip_fail(e, "stats_kernel");
     if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
   }

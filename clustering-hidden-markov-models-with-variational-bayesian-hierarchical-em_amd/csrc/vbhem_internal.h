@@ -34,9 +34,14 @@ struct EmitArgs {
 };
 
 struct StatsArgs {
-  int K, S, SB, SBp, d, covmode, NU, AST, UST, ntiles;
+  int K, S, SB, SBp, d, covmode, NU;
+  int JG;   // clusters per row group (grid.y)
+  int NBB;  // bases per batch (MFMA K-dim = NBB*SBp)
+  int AST;  // LDS row stride of A = NBB*SBp + 1
+  int UST;  // LDS row stride of U = 16*ceil(NU/16)
   int i_begin, i_end, i_buf0, slab_len;
   const double *centres, *covars, *LL, *nu1, *xi, *tnu, *tildeN, *logOmega;
+  double *Z;  // [group][K] hat_Z * tilde_N (resp_kernel -> stats_kernel)
   double *hatZ, *slabs;
 };
 
@@ -72,10 +77,10 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
                            hipStream_t st);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t st);
-hipError_t launch_stats(const StatsArgs &a, int nchunk, int ntg, size_t lds, hipStream_t st);
+bool plan_stats(StatsArgs &a, size_t &lds, int &ngroups);
+hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st);
+hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds, hipStream_t st);
 hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
                               hipStream_t st);
-int stats_tiles_per_block();
-int stats_threads();
 
 }  // namespace vbhem

@@ -15,10 +15,7 @@
 //                       step) for pairs whose factorised normaliser left its
 //                       safe range (only with pathological hyperparameters).
 //   pair_emit_kernel    K5 per pair (MEX-equivalent emit_pr/mu/Mu outputs).
-//   stats_kernel        fused responsibilities + gated Z-weighted reduction;
-//                       the (K*S) x (Sb) x (1+d+d(d+1)/2) emission-moment
-//                       contraction runs on v_mfma_f64_16x16x4f64.
-//   stats_final_kernel  deterministic fixed-order sum of per-block slabs.
+//   (the fused epilogue -- responsibilities and statistics -- is in vbhem_stats.hip)
 //
 // Factorised backward step (exact algebra):
 //   l(rho,sig,b) = logA(rho,sig) + v(sig,b),  v = E + L
@@ -38,7 +35,6 @@
 
 namespace vbhem {
 
-typedef double double4_t __attribute__((ext_vector_type(4)));
 
 constexpr double kLog2Pi = 1.8378770664093454835606594728112353;  // log(2*pi)
 constexpr double kZMin = 1e-200;  // below: fall back to the exact reference order
@@ -523,199 +519,6 @@ __global__ __launch_bounds__(256) void pair_emit_kernel(EmitArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// stats_kernel: responsibilities + gated, Z-weighted reduction over this
-// block's chunk of bases.  Slab (per chunk) += partial sums:
-//   [Nj K | N1 K*S | M K*S*S | Lt1 | Lt7 | U R*NU]     (R = K*S)
-// Tile group tg handles U tiles [tg*kTilesPerBlock, ...); group 0 also does
-// the Nj/N1/M/Lt terms and writes hat_Z.
-// ---------------------------------------------------------------------------
-constexpr int kStatsThreads = 256;
-constexpr int kTilesPerWave = 8;
-constexpr int kTilesPerBlock = kTilesPerWave * (kStatsThreads / 64);
-
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-__global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p) {
-  extern __shared__ double lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int chunk = blockIdx.x, tg = blockIdx.y;
-  const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU, R = K * S;
-  const int SBp = p.SBp, AST = p.AST, UST = p.UST;
-  const bool do_small = (tg == 0);
-  // per-block base range (relative to i_begin of this launch)
-  const int nb = p.i_end - p.i_begin;
-  const int per = (nb + gridDim.x - 1) / gridDim.x;
-  const int b0 = p.i_begin + chunk * per;
-  const int b1 = min(p.i_end, b0 + per);
-
-  double *As = lds;                              // [R][AST]   g*Z*tnu
-  double *Us = As + (size_t)R * AST;             // [SBp][UST] base moments
-  double *gz = Us + (size_t)SBp * UST;           // [K]
-  double *accNj = gz + K;                        // [K]
-  double *accN1 = accNj + K;                     // [K*S]
-  double *accM = accN1 + (size_t)K * S;          // [K*S*S]
-  double *accLt = accM + (size_t)K * S * S;      // [2]
-
-  if (do_small) {
-    for (int x = tid; x < K + K * S + K * S * S + 2; x += kStatsThreads) accNj[x] = 0.0;
-  }
-  // zero the padding of As/Us once (k >= SB rows/cols stay zero)
-  for (int x = tid; x < R * AST; x += kStatsThreads) As[x] = 0.0;
-  for (int x = tid; x < SBp * UST; x += kStatsThreads) Us[x] = 0.0;
-
-  double4_t acc[kTilesPerWave];
-#pragma unroll
-  for (int t = 0; t < kTilesPerWave; ++t) acc[t] = (double4_t){0.0, 0.0, 0.0, 0.0};
-  const int MT = (R + 15) / 16;
-  const int tile0 = tg * kTilesPerBlock;
-  __syncthreads();
-
-  for (int i = b0; i < b1; ++i) {
-    // -- responsibilities for base i (wave 0) --------------------------------
-    if (wave == 0) {
-      // log_Z = tilde_N .* (logOmega + L_elbo) is rounded before the shift, as in
-      // step_fc.m:275-276 (an fma-contracted shift would let the winning entry
-      // exceed 1 by ~ulp(log_Z)).
-#pragma clang fp contract(off)
-      const double tn = p.tildeN[i];
-      double mx = -INFINITY;
-      for (int j = lane; j < K; j += 64) mx = fmax(mx, tn * (p.logOmega[j] + p.LL[(size_t)i * K + j]));
-      mx = wave_max(mx);
-      double sm = 0.0;
-      for (int j = lane; j < K; j += 64) sm += exp(tn * (p.logOmega[j] + p.LL[(size_t)i * K + j]) - mx);
-      sm = wave_sum(sm);
-      const double lse = mx + log(sm);
-      for (int j = lane; j < K; j += 64) {
-        const double ll = p.LL[(size_t)i * K + j];
-        const double hz = exp(tn * (p.logOmega[j] + ll) - lse) + 1e-50;
-        const double Z = hz * tn;
-        gz[j] = (Z > 1e-8) ? Z : 0.0;
-        if (do_small) {
-          p.hatZ[(size_t)i * K + j] = hz;
-          accNj[j] += Z;
-        }
-      }
-      if (do_small) {
-        double l1 = 0.0, l7 = 0.0;
-        for (int j = lane; j < K; j += 64) {
-          const double ll = p.LL[(size_t)i * K + j];
-          const double hz = exp(tn * (p.logOmega[j] + ll) - lse) + 1e-50;
-          l1 += hz * tn * ll;
-          l7 += hz * log(hz);
-        }
-        l1 = wave_sum(l1);
-        l7 = wave_sum(l7);
-        if (lane == 0) {
-          accLt[0] += l1;
-          accLt[1] += l7;
-        }
-      }
-    }
-    __syncthreads();
-    // -- stage A = gz * tnu (rows r = j*S + s, cols beta) and U --------------
-    const double *tnb = p.tnu + (size_t)(i - p.i_buf0) * K * S * SB;
-    for (int x = tid; x < R * SB; x += kStatsThreads) {
-      const int r = x / SB, be = x - r * SB;
-      As[r * AST + be] = gz[r / S] * tnb[x];
-    }
-    const double *mu = p.centres + (size_t)i * SB * d;
-    for (int x = tid; x < SB * NU; x += kStatsThreads) {
-      const int be = x / NU, col = x - be * NU;
-      double u;
-      if (col == 0) {
-        u = 1.0;
-      } else if (col <= d) {
-        u = mu[be * d + col - 1];
-      } else if (p.covmode == kCovFull) {
-        int k = col - 1 - d, a = 0;
-        while (k >= d - a) { k -= d - a; ++a; }
-        const int b = a + k;
-        u = p.covars[(((size_t)i * SB + be) * d + a) * d + b] + mu[be * d + a] * mu[be * d + b];
-      } else {
-        const int q = col - 1 - d;
-        u = p.covars[((size_t)i * SB + be) * d + q] + mu[be * d + q] * mu[be * d + q];
-      }
-      Us[be * UST + col] = u;
-    }
-    if (do_small) {
-      const double *n1 = p.nu1 + (size_t)(i - p.i_buf0) * K * S;
-      for (int x = tid; x < K * S; x += kStatsThreads) accN1[x] += gz[x / S] * n1[x];
-      const double *xi = p.xi + (size_t)(i - p.i_buf0) * K * S * S;
-      for (int x = tid; x < K * S * S; x += kStatsThreads) accM[x] += gz[x / (S * S)] * xi[x];
-    }
-    __syncthreads();
-    // -- MFMA: acc[tile] += A[rows, 4 betas] x U[4 betas, 16 cols] -------------
-#pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) {
-      const int tile = tile0 + wave + t * (kStatsThreads / 64);
-      if (tile < p.ntiles) {
-        const int mt = tile % MT, nt = tile / MT;
-        const int row = mt * 16 + (lane & 15);
-        const int col = nt * 16 + (lane & 15);
-        for (int ks = 0; ks < SBp; ks += 4) {
-          const int k = ks + (lane >> 4);
-          const double av = (row < R) ? As[row * AST + k] : 0.0;
-          const double bv = Us[k * UST + col];
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[t], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();
-  }
-
-  // -- write slab ------------------------------------------------------------
-  double *slab = p.slabs + (size_t)chunk * p.slab_len;
-  if (do_small) {
-    for (int x = tid; x < K + K * S + K * S * S + 2; x += kStatsThreads) slab[x] += accNj[x];
-  }
-  double *slabU = slab + (size_t)K + (size_t)K * S + (size_t)K * S * S + 2;
-#pragma unroll
-  for (int t = 0; t < kTilesPerWave; ++t) {
-    const int tile = tile0 + wave + t * (kStatsThreads / 64);
-    if (tile < p.ntiles) {
-      const int mt = tile % MT, nt = tile / MT;
-      const int col = nt * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + (lane >> 4) + 4 * r;
-        if (row < R && col < NU) slabU[(size_t)row * NU + col] += acc[t][r];
-      }
-    }
-  }
-}
-
-// 256 threads = 32 columns x 8 slab partitions: partition p sums slabs
-// p, p+8, p+16, ... (coalesced 256-B rows), then the 8 partials are added in
-// fixed order -- deterministic, and ~slab_len/32 blocks fill the chip.
-constexpr int kFinalCols = 32, kFinalParts = 8;
-__global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab,
-                                                          int slab_len, double *out) {
-  __shared__ double part[kFinalParts][kFinalCols];
-  const int c = threadIdx.x % kFinalCols, p = threadIdx.x / kFinalCols;
-  const int x = blockIdx.x * kFinalCols + c;
-  double acc = 0.0;
-  if (x < slab_len)
-    for (int k = p; k < nslab; k += kFinalParts) acc += slabs[(size_t)k * slab_len + x];
-  part[p][c] = acc;
-  __syncthreads();
-  if (p == 0 && x < slab_len) {
-    double s = part[0][c];
-#pragma unroll
-    for (int q = 1; q < kFinalParts; ++q) s += part[q][c];
-    out[x] = s;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // launch helpers
 // ---------------------------------------------------------------------------
 template <int D>
@@ -754,23 +557,5 @@ hipError_t launch_emit(const EmitArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
-
-hipError_t launch_stats(const StatsArgs &a, int nchunk, int ntg, size_t lds, hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(stats_kernel, dim3(nchunk, ntg), dim3(kStatsThreads), lds, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
-                              hipStream_t st) {
-  hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + kFinalCols - 1) / kFinalCols), dim3(256), 0, st, slabs,
-                     nslab, slab_len, out);
-  return hipGetLastError();
-}
-
-int stats_tiles_per_block() { return kTilesPerBlock; }
-int stats_threads() { return kStatsThreads; }
 
 }  // namespace vbhem
