@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <utility>
 #include <vector>
@@ -129,7 +130,11 @@ struct SplitPlan {
 SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
   SplitPlan sp;
   if (!vbhem::split_supported(S, SB, d)) return sp;
-  const int LPC = vbhem::split_lpc(S);
+  int LPC = vbhem::split_lpc(S);
+  if (const char *ev = std::getenv("VBHEM_SPLIT_LPC")) {
+    const int v = std::atoi(ev);
+    if (v == 4 && S >= 5 && S <= 8) LPC = 4;
+  }
   const int SH = (S + LPC - 1) / LPC;
   const int LPP = S * LPC;
   const int D = vbhem::split_dim_bucket(d);
@@ -154,6 +159,7 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
       best = util;
       vbhem::SplitArgs &x = sp.a;
       x.SB = SB; x.d = d; x.covmode = covmode; x.K = K; x.S = S; x.T = T; x.D = D; x.nwb = nwb;
+      x.lpc = LPC;
       x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R;
       sp.lds = lds;
       sp.ppb = ppb;

@@ -138,6 +138,21 @@ __device__ __forceinline__ void all_gather(const double (&in)[SH], double (&out)
   }
 }
 
+// Barrier for the per-pair LDS exchange.  When a pair's lanes never straddle a
+// wavefront (lanes per pair a power of two) the exchange is wave-local: LDS
+// requests of one wave are processed in issue order, so a code-motion barrier
+// with wavefront-scope fences suffices and the waves of a block run decoupled.
+template <bool WAVE>
+__device__ __forceinline__ void pair_sync() {
+  if constexpr (WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 template <int n>
 __device__ __forceinline__ void lds_ld(double (&dst)[n], const double *src) {
   if constexpr (n % 2 == 0) {
@@ -189,6 +204,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   constexpr int SH = LY::SH;
   constexpr int NPF = D * (D + 1) / 2;
   constexpr int LPP = S * LPC;  // lanes per pair
+  constexpr bool kWaveLocal = (LPP & (LPP - 1)) == 0;  // pairs never straddle a wave
   const int tid = threadIdx.x;
   const int NT = p.nwb * 64;
   const int PPB = NT / LPP;
@@ -206,6 +222,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   const bool bvalid = b < SB;
   const int bc = bvalid ? b : SB - 1;
   const bool full = p.covmode == kCovFull;
+  __builtin_assume(h >= 0 && h < LPC);
   const int r0 = h * SH;  // first row owned by this lane
 
   double *At = lds;              // [S][S]
@@ -359,6 +376,9 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   __syncthreads();  // K1 staging is dead from here on
 
   // ---------------- K2: backward recursion -------------------------------------------------
+  double am[SH];  // amax of my rows (LDS -> registers once)
+#pragma unroll
+  for (int k = 0; k < SH; ++k) am[k] = amax[r0 + k < S ? r0 + k : S - 1];
   double L[SH];
 #pragma unroll
   for (int k = 0; k < SH; ++k) L[k] = 0.0;
@@ -368,8 +388,12 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
 #pragma unroll
     for (int k = 0; k < SH; ++k) M = fmax(M, E[k] + L[k]);
     M = allmax<LPC>(M);
+    {
+      double ex[SH];
 #pragma unroll
-    for (int k = 0; k < SH; ++k) G[k] = exp_nonpos((E[k] + L[k]) - M);
+      for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
+      exp_nonpos_n<SH>(G, ex);
+    }
     // partial Z for every owner's rows, then reduce-scatter
     double Pz[LPC * SH];
 #pragma unroll
@@ -384,22 +408,23 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     }
     double Z[SH];
     reduce_scatter<LPC, SH>(Pz, Z, h);
-    double sv[SH];
+    double sv[SH], zz[SH], lz[SH];
 #pragma unroll
     for (int k = 0; k < SH; ++k) {
       const bool rv = r0 + k < S;
-      const int r = rv ? r0 + k : S - 1;
       bad |= rv && !(Z[k] >= kZMinS);
-      const double zz = rv ? Z[k] : 1.0;
-      sv[k] = M + amax[r] + log_pos(zz);
+      zz[k] = rv ? Z[k] : 1.0;
     }
+    log_pos_n<SH>(lz, zz);
+#pragma unroll
+    for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];
     if (t <= T - 2) {
       double *slot = R + (size_t)(t - 1) * SH * NT + tid;
 #pragma unroll
       for (int k = 0; k < SH; ++k) slot[k * NT] = G[k];
     }
     if (valid) lds_st<SH>(X + b * LY::XCS + r0, sv);
-    __syncthreads();
+    pair_sync<kWaveLocal>();
 #pragma unroll
     for (int k = 0; k < SH; ++k) L[k] = 0.0;
 #pragma unroll
@@ -409,7 +434,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
 #pragma unroll
       for (int k = 0; k < SH; ++k) L[k] = fma(arow[be], xs[k], L[k]);
     }
-    __syncthreads();
+    pair_sync<kWaveLocal>();
   }
 
   // ---------------- K3: termination ----------------------------------------------------------
@@ -423,19 +448,26 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
       M1 = fmax(M1, v1[k]);
     }
     M1 = allmax<LPC>(M1);
+    double ex[SH], ev[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) ex[k] = v1[k] - M1;
+    exp_nonpos_n<SH>(ev, ex);
     double zs = 0.0;
 #pragma unroll
-    for (int k = 0; k < SH; ++k) zs += exp_nonpos(v1[k] - M1);
+    for (int k = 0; k < SH; ++k) zs += ev[k];
     zs = allsum<LPC>(zs);
     const double s1 = M1 + log_pos(zs);
 #pragma unroll
-    for (int k = 0; k < SH; ++k) nu[k] = pb * exp_nonpos(v1[k] - s1);
+    for (int k = 0; k < SH; ++k) ex[k] = v1[k] - s1;
+    exp_nonpos_n<SH>(ev, ex);
+#pragma unroll
+    for (int k = 0; k < SH; ++k) nu[k] = pb * ev[k];
     if (valid) {
       if (h == 0) Y[b] = pb * s1;
       lds_st<SH>(X + b * LY::XCS + r0, nu);
     }
   }
-  __syncthreads();
+  pair_sync<kWaveLocal>();
   const size_t pair = (size_t)i * K + j;
   const size_t lp = (size_t)(i - p.i_buf0) * K + j;
   if (active) {
@@ -467,14 +499,16 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
 #pragma unroll
       for (int k = 0; k < SH; ++k) M = fmax(M, E[k]);
       M = allmax<LPC>(M);
+      double ex[SH];
 #pragma unroll
-      for (int k = 0; k < SH; ++k) G[k] = exp_nonpos(E[k] - M);
+      for (int k = 0; k < SH; ++k) ex[k] = E[k] - M;
+      exp_nonpos_n<SH>(G, ex);
     } else {
       const double *slot = R + (size_t)(t - 1) * SH * NT + tid;
 #pragma unroll
       for (int k = 0; k < SH; ++k) G[k] = slot[k * NT];
     }
-    __syncthreads();  // X holds nu
+    pair_sync<kWaveLocal>();  // X holds nu
     double f[SH];
 #pragma unroll
     for (int k = 0; k < SH; ++k) f[k] = 0.0;
@@ -499,8 +533,14 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     }
     double Z[SH], g[SH];
     reduce_scatter<LPC, SH>(Pz, Z, h);
+    {
+      double zr[SH], rz[SH];
 #pragma unroll
-    for (int k = 0; k < SH; ++k) g[k] = (r0 + k < S) ? f[k] * rcp_pos(Z[k]) : 0.0;
+      for (int k = 0; k < SH; ++k) zr[k] = (r0 + k < S) ? Z[k] : 1.0;
+      rcp_pos_n<SH>(rz, zr);
+#pragma unroll
+      for (int k = 0; k < SH; ++k) g[k] = (r0 + k < S) ? f[k] * rz[k] : 0.0;
+    }
     // nu'(s) = G(s) * sum_r A'(r, s) g(r): partial over my rows r for every s
     double Pn[LPC * SH];
 #pragma unroll
@@ -526,7 +566,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     for (int k = 0; k < SH; ++k)
 #pragma unroll
       for (int s = 0; s < LPC * SH; ++s) H[k][s] = fma(g[k], Ga[s], H[k][s]);
-    __syncthreads();  // all reads of X done
+    pair_sync<kWaveLocal>();  // all reads of X done
     if (valid) lds_st<SH>(X + b * LY::XCS + r0, nu);
   }
 
@@ -539,14 +579,14 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   // sum_xi(r, s) = A'(r, s) * sum_b H_b(r, s): one pair-wide reduction per row r
 #pragma unroll
   for (int r = 0; r < S; ++r) {
-    __syncthreads();
+    pair_sync<kWaveLocal>();
     if (valid && h == r / SH) {
       double hr[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) hr[s] = H[r % SH][s];
       lds_st<S>(X + b * LY::XCS, hr);
     }
-    __syncthreads();
+    pair_sync<kWaveLocal>();
     if (active && w < S) {
       double acc = 0.0;
 #pragma unroll
@@ -556,7 +596,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   }
   // fallback flags (one per pair)
   if (bad && active) F[q] = 1;
-  __syncthreads();
+  pair_sync<kWaveLocal>();
   if (active && w == 0 && F[q]) {
     const int slot = atomicAdd(p.flag_count, 1);
     atomicAdd(p.flag_count + 1, 1);
@@ -575,9 +615,8 @@ static hipError_t launch_split_sld(const SplitArgs &a, unsigned grid, size_t lds
   return hipGetLastError();
 }
 
-template <int S>
-static hipError_t launch_split_s(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
-  constexpr int LPC = SplitLPC<S>::value;
+template <int S, int LPC>
+static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
   switch (a.D) {
     case 2: return launch_split_sld<S, LPC, 2>(a, grid, lds, st);
     case 4: return launch_split_sld<S, LPC, 4>(a, grid, lds, st);
@@ -585,6 +624,15 @@ static hipError_t launch_split_s(const SplitArgs &a, unsigned grid, size_t lds, 
     case 16: return launch_split_sld<S, LPC, 16>(a, grid, lds, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+template <int S>
+static hipError_t launch_split_s(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  if constexpr (S >= 5 && S <= 8) {
+    if (a.lpc == 4) return launch_split_sl<S, 4>(a, grid, lds, st);
+  }
+  if (a.lpc != SplitLPC<S>::value) return hipErrorInvalidValue;
+  return launch_split_sl<S, SplitLPC<S>::value>(a, grid, lds, st);
 }
 
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {

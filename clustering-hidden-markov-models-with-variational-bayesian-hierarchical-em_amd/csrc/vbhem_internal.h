@@ -60,7 +60,7 @@ struct SplitLayout {
   static constexpr int OFF_X = (HEAD + 1) / 2 * 2;
 };
 struct SplitArgs {
-  int SB, d, covmode, K, S, T, D, nwb;
+  int SB, d, covmode, K, S, T, D, nwb, lpc;
   int i_begin, i_end, i_buf0;
   int off_Y, off_F, off_R;  // LDS layout (doubles), depends on pairs per block
   const double *prior, *A, *centres, *covars;
@@ -70,7 +70,7 @@ struct SplitArgs {
 };
 bool split_supported(int S, int SB, int d);
 int split_dim_bucket(int d);
-int split_lpc(int S);
+int split_lpc(int S);  // default lanes per column (VBHEM_SPLIT_LPC=4 overrides for S = 5..8)
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
 
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);

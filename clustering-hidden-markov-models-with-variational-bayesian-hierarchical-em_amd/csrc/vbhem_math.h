@@ -82,4 +82,90 @@ __host__ __device__ __forceinline__ double log_pos(double z) {
          ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
+// ---- N-wide versions: the same operations, stepped in lockstep over N
+// independent arguments so the dependent polynomial chains interleave (a lone
+// Horner chain issues one fp64 op per pipeline latency; N chains fill it).
+template <int N>
+__host__ __device__ __forceinline__ void exp_nonpos_n(double (&y)[N], const double (&xin)[N]) {
+  double r[N], k[N], p[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double x = fmax(xin[i], -800.0);
+    k[i] = rint(x * 1.4426950408889634074);
+    r[i] = fma(-k[i], 6.93147180369123816490e-01, x);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = fma(-k[i], 1.90821492927058770002e-10, r[i]);
+  constexpr double c[13] = {1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0,
+                            1.0 / 3628800.0,    1.0 / 362880.0,    1.0 / 40320.0,
+                            1.0 / 5040.0,       1.0 / 720.0,       1.0 / 120.0,
+                            1.0 / 24.0,         1.0 / 6.0,         0.5,
+                            1.0};
+#pragma unroll
+  for (int i = 0; i < N; ++i) p[i] = fma(c[0], r[i], c[1]);
+#pragma unroll
+  for (int t = 2; t < 13; ++t)
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = fma(p[i], r[i], c[t]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) y[i] = ldexp(fma(p[i], r[i], 1.0), (int)k[i]);
+}
+
+template <int N>
+__host__ __device__ __forceinline__ void rcp_pos_n(double (&y)[N], const double (&b)[N]) {
+  double r[N], e[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    r[i] = __builtin_amdgcn_rcp(b[i]);
+#else
+    r[i] = 1.0 / b[i];
+#endif
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = fma(-b[i], r[i], 1.0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = fma(r[i], e[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = fma(-b[i], r[i], 1.0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) y[i] = fma(r[i], e[i], r[i]);
+}
+
+template <int N>
+__host__ __device__ __forceinline__ void log_pos_n(double (&y)[N], const double (&z)[N]) {
+  double f[N], dk[N], den[N], s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    int e;
+    double m = frexp(z[i], &e);
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? 2.0 * m : m;
+    e = lo ? e - 1 : e;
+    f[i] = m - 1.0;
+    dk[i] = (double)e;
+    den[i] = 2.0 + f[i];
+  }
+  double rd[N];
+  rcp_pos_n<N>(rd, den);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double q = f[i] * rd[i];
+    s[i] = fma(rd[i], fma(-den[i], q, f[i]), q);   // f / (2 + f), ~1 ulp
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double hfsq = 0.5 * f[i] * f[i];
+    const double zz = s[i] * s[i], w = zz * zz;
+    const double t1 = w * (3.999999999940941908e-01 +
+                           w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+    const double t2 = zz * (6.666666666666735130e-01 +
+                            w * (2.857142874366239149e-01 +
+                                 w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double R = t2 + t1;
+    y[i] = dk[i] * 6.93147180369123816490e-01 -
+           ((hfsq - (s[i] * (hfsq + R) + dk[i] * 1.90821492927058770002e-10)) - f[i]);
+  }
+}
+
 }  // namespace vbhem
