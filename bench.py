@@ -36,9 +36,21 @@ def flops_per_pair(S, Sb, d, T, covmode):
     else:
         k1 = 2 * Sb * S * (3 * d)
         k5 = 2 * S * Sb * (1 + 2 * d)
+    return k1 + fb_flops_per_pair(S, Sb, T) + k5
+
+
+def fb_flops_per_pair(S, Sb, T):
+    """The part fb_split_kernel executes: K2 backward + K3 termination + K4
+    forward (K1 runs in emission_kernel, K5 in stats_kernel)."""
     k2 = (T - 1) * S * (2 * S * Sb + 2 * Sb * Sb + S * Sb)
     k4 = (T - 1) * (2 * S * Sb * Sb + 3 * S * S * Sb)
-    return k1 + k2 + k4 + 2 * S * Sb + k5
+    return k2 + k4 + 2 * S * Sb
+
+
+def emission_flops_per_pair(S, Sb, d, covmode):
+    """K1 as executed by emission_kernel: a GEMM with inner dimension KD."""
+    kd = d * (d + 1) // 2 + d if covmode == 1 else 2 * d
+    return 2 * S * Sb * kd
 
 
 def transcendentals_per_pair(S, Sb, T):
@@ -46,14 +58,15 @@ def transcendentals_per_pair(S, Sb, T):
     return T * S * S * Sb, T * S * Sb
 
 
-def fb_bytes_per_pair(S, Sb, d, covmode, K):
-    """Algorithmic HBM bytes of one fb_pairs_kernel pair: its share of the base
-    parameters (read once per base, shared by K clusters) + its outputs
-    (LL, nu_1, sum_xi, sum_t_nu)."""
-    dC = d * d if covmode == 1 else d
-    base = (Sb + Sb * Sb + Sb * d + Sb * dC) * 8
+def fb_bytes_per_pair(S, Sb, d, covmode, K, split=True):
+    """Algorithmic HBM bytes of one fb-kernel pair.  Split path: its 1/K share
+    of the base transitions/prior + its E tile (emission_kernel output) + its
+    outputs (LL, nu_1, sum_xi, sum_t_nu).  Generic path: base emissions instead of E."""
     out = (1 + S + S * S + S * Sb) * 8
-    return base / K + out
+    if split:
+        return (Sb + Sb * Sb) * 8 / K + S * Sb * 8 + out
+    dC = d * d if covmode == 1 else d
+    return (Sb + Sb * Sb + Sb * d + Sb * dC) * 8 / K + out
 
 
 def committed_traffic(config, N, world, split):
@@ -193,11 +206,11 @@ def main():
     n_local_pairs = (hi - lo) * K
     fb_launch_ms = tk["fb_ms"] / max(1, tk["fb_launches"])
     pairs_per_launch = tk["fb_pairs"] / max(1, tk["fb_launches"])
-    fpp = flops_per_pair(S, Sb, d, T, cov)
+    split = S <= 16 and Sb <= S and d <= 64
+    fpp = fb_flops_per_pair(S, Sb, T) if split else flops_per_pair(S, Sb, d, T, cov)
     achieved = fpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e12
-    bpp = fb_bytes_per_pair(S, Sb, d, cov, K)
+    bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split)
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
-    split = S <= 16 and Sb <= S and d <= 16
     traffic, traffic_src = committed_traffic(args.config, N, world, split)
     res = {
         "metric": METRIC,
@@ -232,14 +245,16 @@ def main():
             "pairs_per_launch": pairs_per_launch,
             "note": ("fp64 compute-bound (VALU + software exp/log); peak = MI355X FP64 dense "
                      "78.6 TF/s (vector = matrix rate); flops counted on the reference "
-                     "recurrences excluding exp/log"),
+                     "recurrences this kernel runs (K2-K4), excluding exp/log"),
             "hbm": {"algorithmic_bytes_per_launch": bpp * pairs_per_launch,
                     "achieved_GBs": bpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e9,
                     "peak_GBs": PEAK_HBM_GBS,
                     "frac": bpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
             "exp_log_per_pair_reference": [n_exp, n_log],
         },
+        "emission_kernel_ms": tk["em_ms"] / max(1, tk["em_launches"]),
         "stats_kernel_ms": tk["stats_ms"] / max(1, tk["stats_launches"]),
+        "algorithmic_tflops_per_s_whole_estep": flops_per_pair(S, Sb, d, T, cov) * N * K * args.steps / dt / 1e12,
         "host_mstep_ms": host_ms,
         "elbo": L,
     }

@@ -47,6 +47,8 @@ EXPORTS = {
     "vbhem_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                    ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_longlong)]),
+    "vbhem_timing_read_emission": (_c_int, [ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_last_error": (ctypes.c_char_p, []),
     "vbhem_version": (ctypes.c_char_p, []),
 }
@@ -95,5 +97,8 @@ def timing_read() -> dict:
     nf, npairs, ns = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong()
     check(lib().vbhem_timing_read(ctypes.byref(fb), ctypes.byref(nf), ctypes.byref(npairs),
                                   ctypes.byref(st), ctypes.byref(ns)), "vbhem_timing_read")
+    em, ne = ctypes.c_double(), ctypes.c_longlong()
+    check(lib().vbhem_timing_read_emission(ctypes.byref(em), ctypes.byref(ne)),
+          "vbhem_timing_read_emission")
     return dict(fb_ms=fb.value, fb_launches=nf.value, fb_pairs=npairs.value,
-                stats_ms=st.value, stats_launches=ns.value)
+                stats_ms=st.value, stats_launches=ns.value, em_ms=em.value, em_launches=ne.value)

@@ -26,7 +26,7 @@ thread_local std::string g_err;
 // synchronised) only by vbhem_timing_read.  Off by default (graph capture).
 struct TimingState {
   bool on = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em;
   std::vector<long long> fb_pairs;
 };
 TimingState g_timing;
@@ -50,7 +50,7 @@ int hip_fail(hipError_t e, const char *where) {
 constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
 constexpr int kExactThreads = 256;                // fallback kernel threads
-constexpr size_t kGroupBudget = (size_t)2 << 30;  // per-pair buffers per group (fused)
+constexpr size_t kGroupBudget = (size_t)8 << 30;  // per-pair buffers per group (fused)
 constexpr int kMaxSlabs = 512;    // statistics chunks (= resp/stats blocks per group)
 
 inline int odd_up(int x) { return (x % 2 == 0) ? x + 1 : x; }
@@ -137,8 +137,6 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
   }
   const int SH = (S + LPC - 1) / LPC;
   const int LPP = S * LPC;
-  const int D = vbhem::split_dim_bucket(d);
-  const int NPF = D * (D + 1) / 2;
   const int XCS = (LPC * SH + 1) / 2 * 2 + 2;
   const int XP = S * XCS + 2;
   const int OFF_X = (2 * S * S + 2 * S + 1) / 2 * 2;
@@ -151,14 +149,13 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
     const int off_F = (off_Y + ppb * S + 1) / 2 * 2;
     const int off_R = (off_F + (ppb + 1) / 2 + 1) / 2 * 2;
     const size_t lattice = (size_t)std::max(0, T - 2) * SH * NT;
-    const size_t staging = (size_t)S * D + 2 * (size_t)S * NPF + S;
-    const size_t lds = ((size_t)off_R + std::max(lattice, staging)) * sizeof(double);
+    const size_t lds = ((size_t)off_R + std::max<size_t>(lattice, 2)) * sizeof(double);
     if (lds > kLdsLimit) continue;
     const double util = double(ppb * LPP) / NT;
     if (util > best + 0.02) {
       best = util;
       vbhem::SplitArgs &x = sp.a;
-      x.SB = SB; x.d = d; x.covmode = covmode; x.K = K; x.S = S; x.T = T; x.D = D; x.nwb = nwb;
+      x.SB = SB; x.d = d; x.covmode = covmode; x.K = K; x.S = S; x.T = T; x.nwb = nwb;
       x.lpc = LPC;
       x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R;
       sp.lds = lds;
@@ -211,7 +208,12 @@ struct PairsWs {
   int *flags;  // [0]=count [1]=total [2..] list
   double *scratch;
   double *tnu;
+  double *E, *W, *bias, *shift;  // emission GEMM (split path)
 };
+
+inline size_t emission_kd(int d, int covmode) {
+  return covmode == VBHEM_COV_FULL ? (size_t)d * (d + 1) / 2 + d : (size_t)2 * d;
+}
 
 size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, bool need_tnu,
                    PairsWs &w) {
@@ -220,6 +222,10 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.flags = cv.take<int>(2 + np);
   w.scratch = cv.take<double>(exact_stride(c->S, b->SB, T) * kExactThreads);
   w.tnu = need_tnu ? cv.take<double>(np * c->S * b->SB) : nullptr;
+  w.E = cv.take<double>(np * c->S * b->SB);
+  w.W = cv.take<double>(emission_kd(b->d, b->covmode) * c->K * c->S);
+  w.bias = cv.take<double>((size_t)c->K * c->S);
+  w.shift = cv.take<double>((size_t)b->d);
   return cv.off + 256;
 }
 
@@ -229,12 +235,13 @@ struct FusedWs {
   int slab_len;
   int *flags;
   double *scratch, *nu1, *xi, *tnu, *Z, *slabs;
+  double *E, *W, *bias, *shift;
 };
 
 size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, FusedWs &w) {
   Carver cv(ws);
   const int K = c->K, S = c->S, SB = b->SB;
-  const size_t per_base = (size_t)K * (S + (size_t)S * S + (size_t)S * SB) * sizeof(double);
+  const size_t per_base = (size_t)K * (S + (size_t)S * S + 2 * (size_t)S * SB) * sizeof(double);
   size_t g = std::max<size_t>(1, kGroupBudget / std::max<size_t>(1, per_base));
   g = std::min<size_t>(g, (size_t)std::max(1, b->N));
   w.group = (int)g;
@@ -247,16 +254,28 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.tnu = cv.take<double>(g * K * S * SB);
   w.Z = cv.take<double>(g * K);
   w.slabs = cv.take<double>((size_t)w.nslab * w.slab_len);
+  w.E = cv.take<double>(g * K * S * SB);
+  w.W = cv.take<double>(emission_kd(b->d, b->covmode) * K * S);
+  w.bias = cv.take<double>((size_t)K * S);
+  w.shift = cv.take<double>((size_t)b->d);
   return cv.off + 256;
 }
 
 struct FbCtx {
   FbPlan plan;      // generic element-per-lane kernel
   SplitPlan split;  // column-per-LPC-lanes kernel (preferred when it applies)
+  vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
+  size_t em_lds = 0;
 };
 
 int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T) {
   c.split = plan_split(b->SB, b->d, b->covmode, cl->K, cl->S, T);
+  if (c.split.ok) {
+    vbhem::EmissionArgs &e = c.em;
+    e.SB = b->SB; e.d = b->d; e.covmode = b->covmode; e.K = cl->K; e.S = cl->S;
+    e.centres = b->centres; e.covars = b->covars; e.m = cl->m; e.P = cl->P; e.c = cl->c;
+    if (!vbhem::plan_emission(e, c.em_lds)) c.split.ok = false;
+  }
   const bool have_elems = plan_fb(b->SB, b->d, b->covmode, cl->K, cl->S, T, c.plan);
   if (!c.split.ok && !have_elems)
     return fail(VBHEM_ERR_UNSUPPORTED,
@@ -269,14 +288,23 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
   c.plan.a.K = cl->K; c.plan.a.S = cl->S; c.plan.a.T = T;
   if (c.split.ok) {
     vbhem::SplitArgs &a = c.split.a;
-    a.prior = b->prior; a.A = b->A; a.centres = b->centres; a.covars = b->covars;
-    a.logA = cl->logA; a.logPi = cl->logPi; a.m = cl->m; a.P = cl->P; a.c = cl->c;
+    a.prior = b->prior; a.A = b->A; a.logA = cl->logA; a.logPi = cl->logPi;
   }
   return VBHEM_OK;
 }
 
+// W, bias, shift of the emission GEMM: once per call (depends on the clusters only)
+int run_emission_prep(FbCtx &c, double *W, double *bias, double *shift, hipStream_t st) {
+  if (!c.split.ok) return VBHEM_OK;
+  c.em.W = W; c.em.bias = bias; c.em.shift = shift;
+  hipError_t e = vbhem::launch_emission_prep(c.em, st);
+  if (e != hipSuccess) return hip_fail(e, "emission_prep_kernel");
+  return VBHEM_OK;
+}
+
 int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, double *nu1,
-           double *xi, double *tnu, int *flags, double *scratch, hipStream_t st) {
+           double *xi, double *tnu, double *Ebuf, long long e_ld, int *flags, double *scratch,
+           hipStream_t st) {
   if (i_end <= i_begin) return VBHEM_OK;
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin;
@@ -287,9 +315,18 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   a.flag_list = flags + 2;
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  if (c.split.ok) {
+    vbhem::EmissionArgs ea = c.em;
+    ea.i_begin = i_begin; ea.i_end = i_end; ea.i_buf0 = i_buf0; ea.E = Ebuf; ea.e_ld = e_ld;
+    hipEvent_t em0 = g_timing.on ? timing_event(st) : nullptr;
+    e = vbhem::launch_emission(ea, c.em_lds, st);
+    if (e != hipSuccess) return hip_fail(e, "emission_kernel");
+    if (g_timing.on) g_timing.em.emplace_back(em0, timing_event(st));
+  }
   hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
   if (c.split.ok) {
     vbhem::SplitArgs ca = c.split.a;
+    ca.E = Ebuf; ca.e_ld = e_ld;
     ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
     ca.LL = LL; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
     ca.flag_count = flags; ca.flag_list = flags + 2;
@@ -356,7 +393,10 @@ int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   if (rc != VBHEM_OK) return rc;
   hipError_t e0 = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
   if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
-  rc = run_fb(ctx, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.flags,
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st);
+  if (rc != VBHEM_OK) return rc;
+  rc = run_fb(ctx, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.E,
+              (long long)base->N * base->SB, w.flags,
               w.scratch, st);
   if (rc != VBHEM_OK) return rc;
   vbhem::EmitArgs ea{};
@@ -413,9 +453,12 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T);
   if (rc != VBHEM_OK) return rc;
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st);
+  if (rc != VBHEM_OK) return rc;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);
-    rc = run_fb(ctx, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.flags, w.scratch, st);
+    rc = run_fb(ctx, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.E, (long long)w.group * SB,
+                w.flags, w.scratch, st);
     if (rc != VBHEM_OK) return rc;
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     const int nchunk = std::min(w.nslab, g1 - g0);
@@ -466,6 +509,27 @@ int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs
   if (fb_pairs) *fb_pairs = np;
   if (stats_ms) *stats_ms = s;
   if (stats_launches) *stats_launches = ns;
+  return rc;
+}
+
+int vbhem_timing_read_emission(double *em_ms, long long *em_launches) {
+  double t = 0.0;
+  int rc = VBHEM_OK;
+  const long long n = (long long)g_timing.em.size();
+  for (auto &pr : g_timing.em) {
+    float ms = 0.f;
+    if (pr.first && pr.second) {
+      hipError_t e = hipEventSynchronize(pr.second);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
+      if (e != hipSuccess) rc = hip_fail(e, "vbhem_timing_read_emission");
+      t += ms;
+    }
+    if (pr.first) (void)hipEventDestroy(pr.first);
+    if (pr.second) (void)hipEventDestroy(pr.second);
+  }
+  g_timing.em.clear();
+  if (em_ms) *em_ms = t;
+  if (em_launches) *em_launches = n;
   return rc;
 }
 

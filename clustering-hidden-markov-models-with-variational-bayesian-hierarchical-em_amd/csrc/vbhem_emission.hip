@@ -1,0 +1,286 @@
+// vbhem_emission.hip -- K1, the expected emission log-likelihood of every
+// (base state beta, cluster state sigma) of every (base i, cluster j) pair
+// (mex.c:715-865), as one fp64 GEMM on v_mfma_f64_16x16x4f64:
+//
+//   E[(i,b),(j,s)] = -1/2 ( d log 2pi + c_s + <P_s, Sigma_b> + (mu_b - m_s)' P_s (mu_b - m_s) )
+//                  = -1/2 ( bias_s + sum_e W[e][(j,s)] * U[e][(i,b)] )
+//
+// with every mean shifted by the same vector z (the average cluster mean; the
+// quadratic form is shift-invariant, the shift keeps the expanded terms small):
+//   full: U = [ Sigma_ab + Sigma_ba + 2 mu'_a mu'_b (a<b) | Sigma_aa + mu'_a^2 (a=b) , mu'_a ]
+//         W = [ P_ab (packed upper, symmetrised)                              , -2 (P m')_a ]
+//         bias = d log 2pi + c + m'' P m'
+//   diag: U = [ Sigma_a + mu'_a^2 , mu'_a ],  W = [ P_a , -2 P_a m'_a ],  bias = d log 2pi + c + sum P_a m'_a^2
+// (mu' = mu - z, m' = m - z; KD = d(d+1)/2 + d full, 2d diag).
+//
+// emission_prep_kernel builds W, bias and z once per call (K*S columns);
+// emission_kernel streams the base set: every wavefront walks tiles of 16
+// consecutive columns (i,b), builds its MFMA B operand U directly in registers
+// from the covariances and means, and multiplies by W (LDS-resident when it
+// fits, else read from L2) for all K*S rows.  Output layout E[(j,s)][(i - i_buf0) * Sb + b] (cluster-
+// major rows): the MFMA tile stores 128-B row segments and fb_split_kernel's
+// lanes (consecutive bases x base states) read contiguous 256-B runs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "vbhem_internal.h"
+
+namespace vbhem {
+
+namespace {
+typedef double double4_t __attribute__((ext_vector_type(4)));
+constexpr double kLog2PiE = 1.8378770664093454835606594728112353;
+constexpr int kEmThreads = 256;
+
+__device__ __forceinline__ void packed_ab(int e, int d, int &a, int &b) {
+  a = 0;
+  int k = e;
+  while (k >= d - a) {
+    k -= d - a;
+    ++a;
+  }
+  b = a + k;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// prep: z (mean of all cluster means), bias[K*S], W[KD][K*S]
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kEmThreads) void emission_prep_kernel(EmissionArgs p) {
+  __shared__ double zs[64];
+  const int tid = threadIdx.x, d = p.d, KS = p.K * p.S;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d;
+  // z: fixed-order mean over the K*S cluster means
+  for (int a = tid; a < d; a += kEmThreads) {
+    double s = 0.0;
+    for (int r = 0; r < KS; ++r) s += p.m[(size_t)r * d + a];
+    zs[a] = s / (double)KS;
+    p.shift[a] = zs[a];
+  }
+  __syncthreads();
+  for (int r = tid; r < KS; r += kEmThreads) {
+    const double *mr = p.m + (size_t)r * d;
+    if (full) {
+      const double *P = p.P + (size_t)r * d * d;
+      double q = 0.0;
+      for (int a = 0; a < d; ++a) {
+        double pm = 0.0;  // (P_sym m')_a
+        for (int b = 0; b < d; ++b) {
+          const double ps = 0.5 * (P[a * d + b] + P[b * d + a]);
+          pm = fma(ps, mr[b] - zs[b], pm);
+        }
+        q = fma(mr[a] - zs[a], pm, q);
+        p.W[(size_t)(NPF + a) * KS + r] = -2.0 * pm;
+      }
+      p.bias[r] = d * kLog2PiE + p.c[r] + q;
+      int e = 0;
+      for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b, ++e)
+          p.W[(size_t)e * KS + r] = (a == b) ? P[a * d + a] : 0.5 * (P[a * d + b] + P[b * d + a]);
+    } else {
+      const double *P = p.P + (size_t)r * d;
+      double q = 0.0;
+      for (int a = 0; a < d; ++a) {
+        const double ma = mr[a] - zs[a];
+        q = fma(P[a] * ma, ma, q);
+        p.W[(size_t)a * KS + r] = P[a];
+        p.W[(size_t)(d + a) * KS + r] = -2.0 * P[a] * ma;
+      }
+      p.bias[r] = d * kLog2PiE + p.c[r] + q;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// emission_kernel: every wavefront independently walks tiles of 16 columns
+// (i,b).  The tile's covariances and means are contiguous in memory: the wave
+// loads them with coalesced 16-B loads into its private LDS slot (RAW), then
+// each lane forms, per k-step, the MFMA B operand U[4t + (l>>4)][l & 15] from
+// LDS; operand A (W, <= 50 KB) is read through L1/L2.  Rows are processed in
+// chunks of 8 row tiles (32 fp64 accumulators per lane).
+// ---------------------------------------------------------------------------
+constexpr int kEmRowChunk = 8;
+constexpr int kEmRawSlot = 16 * 64 + 16 * 8;  // doubles per wave: 16 cols x (d*d <= 64, d <= 8)
+
+template <bool RAW>
+__global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int d = p.d, SB = p.SB, KS = p.K * p.S, KD = p.KD;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d;
+  const int dd = full ? d * d : d;
+  const int RT = (KS + 15) / 16, KQ = (KD + 3) / 4;
+  const int ncols = (p.i_end - p.i_begin) * SB;
+  const int nctile = (ncols + 15) / 16;
+  int *tab = reinterpret_cast<int *>(lds);                 // [KD] (a | b << 8 | kind << 16)
+  double *slot = lds + (KD + 1) / 2 + 1 + wave * kEmRawSlot;
+  double *rawc = slot;                                     // [16][dd]
+  double *mus = slot + 16 * dd;                            // [16][d] (unshifted)
+  for (int e = tid; e < KD; e += kEmThreads) {
+    int a, b, kind;
+    if (e < NPF) {
+      a = b = e;
+      if (full) packed_ab(e, d, a, b);
+      kind = full ? (a == b ? 0 : 1) : 2;
+    } else {
+      a = b = e - NPF;
+      kind = 3;
+    }
+    tab[e] = a | (b << 8) | (kind << 16);
+  }
+  __syncthreads();
+  const int kl = lane >> 4, cl = lane & 15;
+  const size_t ldE = (size_t)p.e_ld;
+  const int wstride = gridDim.x * (kEmThreads / 64);
+  int ct = blockIdx.x * (kEmThreads / 64) + wave;
+
+  // register prefetch of a tile's raw covariances (16 cols x dd <= 1024 doubles) and
+  // means (16 x d <= 128): 8 + 1 double2 per lane, fully coalesced
+  constexpr int kPre = 8;
+  double2 pre_c[kPre], pre_m;
+  auto prefetch = [&](int t) {
+    const int c0 = t * 16;
+    const int ccount = min(16, ncols - c0);
+    const size_t g0 = (size_t)p.i_begin * SB + c0;
+    const double2 *src = reinterpret_cast<const double2 *>(p.covars + g0 * dd);
+    const int n2 = ccount * dd / 2;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int x = lane + 64 * k;
+      pre_c[k] = (x < n2) ? src[x] : make_double2(0.0, 0.0);
+    }
+    const double2 *ms = reinterpret_cast<const double2 *>(p.centres + g0 * d);
+    const int nm2 = ccount * d / 2;
+    pre_m = lane < nm2 ? ms[lane] : make_double2(0.0, 0.0);
+  };
+  if (RAW && ct < nctile) prefetch(ct);
+
+  for (; ct < nctile; ct += wstride) {
+    const int c0 = ct * 16;
+    const int ccount = min(16, ncols - c0);
+    const int col = c0 + cl;
+    const bool cv = cl < ccount;
+    const size_t g0 = (size_t)p.i_begin * SB + c0;
+    const double *Cg = p.covars + (g0 + (cv ? cl : 0)) * dd;
+    const double *Mg = p.centres + (g0 + (cv ? cl : 0)) * d;
+    if (RAW) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // previous tile's LDS reads done
+      double2 *r2 = reinterpret_cast<double2 *>(rawc);
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int x = lane + 64 * k;
+        if (x < 8 * dd) r2[x] = pre_c[k];
+      }
+      if (lane < 8 * d) reinterpret_cast<double2 *>(mus)[lane] = pre_m;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ct + wstride < nctile) prefetch(ct + wstride);  // next tile, overlaps the MFMAs
+    }
+    const size_t cbuf = (size_t)(p.i_begin - p.i_buf0) * SB + col;
+    for (int r0 = 0; r0 < RT; r0 += kEmRowChunk) {
+      double4_t acc[kEmRowChunk];
+#pragma unroll
+      for (int q = 0; q < kEmRowChunk; ++q) acc[q] = (double4_t){0.0, 0.0, 0.0, 0.0};
+      // W (operand A) for k-step t, software-pipelined one step ahead
+      double wc[kEmRowChunk], wn[kEmRowChunk];
+      auto loadw = [&](int t, double (&w)[kEmRowChunk]) {
+        const int e = 4 * t + kl;
+        const double *We = p.W + (size_t)(e < KD ? e : 0) * KS;
+#pragma unroll
+        for (int q = 0; q < kEmRowChunk; ++q) {
+          const int row = (r0 + q) * 16 + cl;
+          w[q] = (e < KD && row < KS) ? We[row] : 0.0;
+        }
+      };
+      loadw(0, wc);
+      for (int t = 0; t < KQ; ++t) {
+        if (t + 1 < KQ) loadw(t + 1, wn);
+        const int e = 4 * t + kl;
+        double u = 0.0;
+        if (e < KD) {
+          const int tb = tab[e], a = tb & 0xff, b = (tb >> 8) & 0xff, kind = tb >> 16;
+          double ma, mb, caa;
+          if (RAW) {
+            ma = mus[cl * d + a] - p.shift[a];
+            mb = mus[cl * d + b] - p.shift[b];
+            caa = kind <= 1 ? rawc[cl * dd + a * d + b] : (kind == 2 ? rawc[cl * dd + a] : 0.0);
+            if (kind == 1) caa += rawc[cl * dd + b * d + a];
+          } else {
+            ma = Mg[a] - p.shift[a];
+            mb = Mg[b] - p.shift[b];
+            caa = kind <= 1 ? Cg[a * d + b] : (kind == 2 ? Cg[a] : 0.0);
+            if (kind == 1) caa += Cg[b * d + a];
+          }
+          u = kind == 3 ? ma : (kind == 1 ? fma(2.0 * ma, mb, caa) : fma(ma, ma, caa));
+          u = cv ? u : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kEmRowChunk; ++q)
+          if (r0 + q < RT) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], u, acc[q], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
+      }
+      if (cv) {
+#pragma unroll
+        for (int q = 0; q < kEmRowChunk; ++q) {
+          const int rt = r0 + q;
+          if (rt < RT) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int row = rt * 16 + kl + 4 * v;
+              if (row < KS) p.E[(size_t)row * ldE + cbuf] = -0.5 * (p.bias[row] + acc[q][v]);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+bool plan_emission(EmissionArgs &a, size_t &lds) {
+  const bool full = a.covmode == kCovFull;
+  const int d = a.d;
+  if (d > 64) return false;
+  a.KD = full ? d * (d + 1) / 2 + d : 2 * d;
+  const int dd = full ? d * d : d;
+  a.wfull = (dd <= 64 && d <= 8 && dd % 2 == 0 && d % 2 == 0);  // RAW: tile staged in LDS
+  lds = ((size_t)(a.KD + 1) / 2 + 1) * sizeof(double) +
+        (a.wfull ? (size_t)4 * kEmRawSlot * sizeof(double) : 0);
+  a.CB = 16;
+  return true;
+}
+
+hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st) {
+  hipLaunchKernelGGL(emission_prep_kernel, dim3(1), dim3(kEmThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+template <bool RAW>
+static hipError_t launch_emission_t(const EmissionArgs &a, size_t lds, unsigned grid,
+                                    hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&emission_kernel<RAW>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(emission_kernel<RAW>, dim3(grid), dim3(kEmThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
+  const int ncols = (a.i_end - a.i_begin) * a.SB;
+  if (ncols <= 0) return hipSuccess;
+  const int nctile = (ncols + 15) / 16;
+  const int per_block = kEmThreads / 64;
+  // persistent: ~4 resident blocks per CU, every wave walks 16-column tiles
+  const unsigned grid = (unsigned)std::min((nctile + per_block - 1) / per_block, 256 * 4);
+  return a.wfull ? launch_emission_t<true>(a, lds, grid, st)
+                 : launch_emission_t<false>(a, lds, grid, st);
+}
+
+}  // namespace vbhem

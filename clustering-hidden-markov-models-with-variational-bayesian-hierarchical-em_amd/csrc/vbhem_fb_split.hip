@@ -35,7 +35,6 @@ namespace vbhem {
 
 namespace {
 
-constexpr double kLog2PiS = 1.8378770664093454835606594728112353;
 constexpr double kZMinS = 1e-200;
 
 // ---- DPP lane exchange inside aligned lane quads -------------------------------
@@ -197,18 +196,17 @@ __device__ __forceinline__ void load_row(double (&dst)[SH], const double *row, i
 
 }  // namespace
 
-template <int S, int LPC, int D>
+template <int S, int LPC>
 __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using LY = SplitLayout<S, LPC>;
   constexpr int SH = LY::SH;
-  constexpr int NPF = D * (D + 1) / 2;
   constexpr int LPP = S * LPC;  // lanes per pair
   constexpr bool kWaveLocal = (LPP & (LPP - 1)) == 0;  // pairs never straddle a wave
   const int tid = threadIdx.x;
   const int NT = p.nwb * 64;
   const int PPB = NT / LPP;
-  const int SB = p.SB, T = p.T, d = p.d, K = p.K;
+  const int SB = p.SB, T = p.T, K = p.K;
   const int j = blockIdx.x % K;
   const int i0 = p.i_begin + (blockIdx.x / K) * PPB;
   const int q = tid / LPP;
@@ -221,7 +219,6 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   const int ic = active ? i : p.i_begin;
   const bool bvalid = b < SB;
   const int bc = bvalid ? b : SB - 1;
-  const bool full = p.covmode == kCovFull;
   __builtin_assume(h >= 0 && h < LPC);
   const int r0 = h * SH;  // first row owned by this lane
 
@@ -231,132 +228,19 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   double *lpi = amax + S;        // [S]
   double *X = lds + LY::OFF_X + (valid ? q : 0) * LY::XP;   // slab [col][XCS]
   double *Y = lds + p.off_Y + (valid ? q : 0) * S;
-  double *R = lds + p.off_R;     // K1 staging | lattice [(T-2)][SH][NT]
+  double *R = lds + p.off_R;     // lattice [(T-2)][SH][NT]
   int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
 
-  // ---------------- stage the cluster constants ------------------------------------
-  {
-    const double *la = p.logA + (size_t)j * S * S;
-    if (tid < S) {
-      double mx = la[tid * S];
-      for (int s = 1; s < S; ++s) mx = fmax(mx, la[tid * S + s]);
-      amax[tid] = mx;
-      lpi[tid] = p.logPi[(size_t)j * S + tid];
-    }
-    double *km = R;              // [S][D]
-    double *kP = km + S * D;     // [S][NPF]
-    double *kPT = kP + S * NPF;  // [NPF][S]
-    double *kc = kPT + S * NPF;  // [S]
-    for (int x = tid; x < S * D; x += NT) {
-      const int s = x / D, qd = x - s * D;
-      const double v = p.m[((size_t)j * S + s) * d + (qd < d ? qd : d - 1)];
-      km[x] = qd < d ? v : 0.0;
-    }
-    if (full) {
-      for (int x = tid; x < S * NPF; x += NT) {
-        const int s = x / NPF;
-        int k = x - s * NPF, a = 0;
-        while (k >= D - a) {
-          k -= D - a;
-          ++a;
-        }
-        const int c2 = a + k;
-        const int aa = a < d ? a : d - 1, cc = c2 < d ? c2 : d - 1;
-        const double v = p.P[(((size_t)j * S + s) * d + aa) * d + cc];
-        const double val = (a < d && c2 < d) ? v : 0.0;
-        kP[x] = val;
-        kPT[(x - s * NPF) * S + s] = val;
-      }
-    } else {
-      for (int x = tid; x < S * D; x += NT) {
-        const int s = x / D, qd = x - s * D;
-        const double v = p.P[((size_t)j * S + s) * d + (qd < d ? qd : d - 1)];
-        kP[x] = qd < d ? v : 0.0;
-      }
-    }
-    if (tid < S) kc[tid] = p.c[(size_t)j * S + tid];
-    for (int x = tid; x < PPB; x += NT) F[x] = 0;
-  }
-  __syncthreads();
-  for (int x = tid; x < S * S; x += NT) {
-    const int r = x / S, s = x - r * S;
-    const double a = exp_nonpos(p.logA[(size_t)j * S * S + x] - amax[r]);
-    At[x] = a;
-    AtT[s * S + r] = a;
-  }
-
-  // ---------------- K1: E[k] for rows sigma = r0 + k ---------------------------------------
+  // ---------------- per-pair inputs: E (K1, precomputed), Ab row/column, prior -------------
+  const size_t lp = (size_t)(ic - p.i_buf0) * K + j;
   double E[SH];
   {
-    const double *km = R;
-    const double *kP = km + S * D;
-    const double *kPT = kP + S * NPF;
-    const double *kc = kPT + S * NPF;
-    double mu[D];
-    const double *mub = p.centres + ((size_t)ic * SB + bc) * d;
-#pragma unroll
-    for (int qd = 0; qd < D; ++qd) {
-      const double v = mub[qd < d ? qd : d - 1];
-      mu[qd] = (qd < d && bvalid) ? v : 0.0;
-    }
-    double acc[SH];
-#pragma unroll
-    for (int k = 0; k < SH; ++k) acc[k] = 0.0;
-    if (full) {
-      const double *C = p.covars + ((size_t)ic * SB + bc) * d * d;
-      int kk = 0;
-#pragma unroll
-      for (int a = 0; a < D; ++a) {
-#pragma unroll
-        for (int c2 = a; c2 < D; ++c2, ++kk) {
-          const int aa = a < d ? a : d - 1, cc = c2 < d ? c2 : d - 1;
-          const double v1 = C[aa * d + cc], v2 = C[cc * d + aa];
-          const double cs = (a < d && c2 < d && bvalid) ? (a == c2 ? v1 : v1 + v2) : 0.0;
-          const double *pk = kPT + kk * S;
-#pragma unroll
-          for (int k = 0; k < SH; ++k) {
-            const int r = r0 + k < S ? r0 + k : S - 1;
-            acc[k] = fma(pk[r], cs, acc[k]);
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < SH; ++k) {
-        const int r = r0 + k < S ? r0 + k : S - 1;
-        double x[D];
-#pragma unroll
-        for (int qd = 0; qd < D; ++qd) x[qd] = mu[qd] - km[r * D + qd];
-        const double *ps = kP + r * NPF;
-        double t = 0.0;
-        int k2 = 0;
-#pragma unroll
-        for (int a = 0; a < D; ++a) {
-#pragma unroll
-          for (int c2 = a; c2 < D; ++c2, ++k2) {
-            const double wv = (a == c2) ? x[a] * x[a] : 2.0 * x[a] * x[c2];
-            t = fma(ps[k2], wv, t);
-          }
-        }
-        acc[k] += t;
-      }
-    } else {
-      const double *C = p.covars + ((size_t)ic * SB + bc) * d;
-#pragma unroll
-      for (int qd = 0; qd < D; ++qd) {
-        const double v = C[qd < d ? qd : d - 1];
-        const double cq = (qd < d && bvalid) ? v : 0.0;
-#pragma unroll
-        for (int k = 0; k < SH; ++k) {
-          const int r = r0 + k < S ? r0 + k : S - 1;
-          const double x = mu[qd] - km[r * D + qd];
-          acc[k] = fma(kP[r * D + qd], fma(x, x, cq), acc[k]);
-        }
-      }
-    }
+    const double *Ep = p.E + (size_t)j * S * p.e_ld + (size_t)(ic - p.i_buf0) * SB + bc;
 #pragma unroll
     for (int k = 0; k < SH; ++k) {
-      const int r = r0 + k < S ? r0 + k : S - 1;
-      E[k] = (r0 + k < S) ? -0.5 * (d * kLog2PiS + kc[r] + acc[k]) : -INFINITY;
+      const bool rv = r0 + k < S;
+      const double v = Ep[(size_t)(rv ? r0 + k : S - 1) * p.e_ld];
+      E[k] = rv ? v : -INFINITY;
     }
   }
   double arow[S], acol[S];
@@ -373,7 +257,26 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   }
   const double pb0 = p.prior[(size_t)ic * SB + bc];
   const double pb = bvalid ? pb0 : 0.0;
-  __syncthreads();  // K1 staging is dead from here on
+
+  // ---------------- cluster constants: A' = exp(logA - rowmax), rowmax, logPi --------------
+  {
+    const double *la = p.logA + (size_t)j * S * S;
+    if (tid < S) {
+      double mx = la[tid * S];
+      for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[tid * S + s2]);
+      amax[tid] = mx;
+      lpi[tid] = p.logPi[(size_t)j * S + tid];
+    }
+    for (int x = tid; x < PPB; x += NT) F[x] = 0;
+  }
+  __syncthreads();
+  for (int x = tid; x < S * S; x += NT) {
+    const int r = x / S, s2 = x - r * S;
+    const double a = exp_nonpos(p.logA[(size_t)j * S * S + x] - amax[r]);
+    At[x] = a;
+    AtT[s2 * S + r] = a;
+  }
+  __syncthreads();
 
   // ---------------- K2: backward recursion -------------------------------------------------
   double am[SH];  // amax of my rows (LDS -> registers once)
@@ -412,7 +315,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
 #pragma unroll
     for (int k = 0; k < SH; ++k) {
       const bool rv = r0 + k < S;
-      bad |= rv && !(Z[k] >= kZMinS);
+      bad |= bvalid && rv && !(Z[k] >= kZMinS);
       zz[k] = rv ? Z[k] : 1.0;
     }
     log_pos_n<SH>(lz, zz);
@@ -469,7 +372,6 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   }
   pair_sync<kWaveLocal>();
   const size_t pair = (size_t)i * K + j;
-  const size_t lp = (size_t)(i - p.i_buf0) * K + j;
   if (active) {
     if (w == 0) {
       double ll = 0.0;
@@ -605,25 +507,14 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-template <int S, int LPC, int D>
-static hipError_t launch_split_sld(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
-  auto *fn = &fb_split_kernel<S, LPC, D>;
+template <int S, int LPC>
+static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  auto *fn = &fb_split_kernel<S, LPC>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((fb_split_kernel<S, LPC, D>), dim3(grid), dim3(a.nwb * 64), lds, st, a);
+  hipLaunchKernelGGL((fb_split_kernel<S, LPC>), dim3(grid), dim3(a.nwb * 64), lds, st, a);
   return hipGetLastError();
-}
-
-template <int S, int LPC>
-static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
-  switch (a.D) {
-    case 2: return launch_split_sld<S, LPC, 2>(a, grid, lds, st);
-    case 4: return launch_split_sld<S, LPC, 4>(a, grid, lds, st);
-    case 8: return launch_split_sld<S, LPC, 8>(a, grid, lds, st);
-    case 16: return launch_split_sld<S, LPC, 16>(a, grid, lds, st);
-    default: return hipErrorInvalidValue;
-  }
 }
 
 template <int S>
@@ -658,10 +549,8 @@ hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream
 }
 
 bool split_supported(int S, int SB, int d) {
-  return S >= 1 && S <= kSplitMaxS && SB >= 1 && SB <= S && d >= 1 && d <= 16;
+  return S >= 1 && S <= kSplitMaxS && SB >= 1 && SB <= S && d >= 1 && d <= 64;
 }
-
-int split_dim_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
 int split_lpc(int S) { return S <= 4 ? 1 : S <= 8 ? 2 : 4; }
 

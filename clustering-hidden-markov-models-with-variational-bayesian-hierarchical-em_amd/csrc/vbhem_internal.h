@@ -59,17 +59,32 @@ struct SplitLayout {
   static constexpr int HEAD = 2 * S * S + 2 * S;            // At, AtT, amax, lpi
   static constexpr int OFF_X = (HEAD + 1) / 2 * 2;
 };
+// K1 emission GEMM (vbhem_emission.hip)
+struct EmissionArgs {
+  int SB, d, covmode, K, S, KD, CB;
+  bool wfull;  // column tiles staged in LDS (d <= 8); else read through L1/L2
+  int i_begin, i_end, i_buf0;
+  long long e_ld;  // row stride of E = (bases in the buffer) * SB
+  const double *centres, *covars, *m, *P, *c;
+  double *W, *bias, *shift;  // [KD][K*S], [K*S], [d] (emission_prep_kernel)
+  double *E;                 // [K*S][(i - i_buf0) * SB + b]  (row stride e_ld)
+};
+bool plan_emission(EmissionArgs &a, size_t &lds);
+hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st);
+hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st);
+
 struct SplitArgs {
-  int SB, d, covmode, K, S, T, D, nwb, lpc;
+  int SB, d, covmode, K, S, T, nwb, lpc;
   int i_begin, i_end, i_buf0;
   int off_Y, off_F, off_R;  // LDS layout (doubles), depends on pairs per block
-  const double *prior, *A, *centres, *covars;
-  const double *logA, *logPi, *m, *P, *c;
+  const double *prior, *A;
+  const double *logA, *logPi;
+  const double *E;  // emission_kernel output, [K*S][(i - i_buf0) * SB + b], row stride e_ld
+  long long e_ld;
   double *LL, *nu1, *xi, *tnu;
   int *flag_count, *flag_list;
 };
 bool split_supported(int S, int SB, int d);
-int split_dim_bucket(int d);
 int split_lpc(int S);  // default lanes per column (VBHEM_SPLIT_LPC=4 overrides for S = 5..8)
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
 

@@ -124,6 +124,9 @@ int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
 int vbhem_timing_enable(int on);
 int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs,
                       double *stats_ms, long long *stats_launches);
+/* Summed time and launch count of the K1 emission GEMM (emission_kernel) since
+ * the last call; same event mechanism as vbhem_timing_read. */
+int vbhem_timing_read_emission(double *em_ms, long long *em_launches);
 
 const char *vbhem_last_error(void);
 const char *vbhem_version(void);
