@@ -245,7 +245,9 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   size_t g = std::max<size_t>(1, kGroupBudget / std::max<size_t>(1, per_base));
   g = std::min<size_t>(g, (size_t)std::max(1, b->N));
   w.group = (int)g;
-  w.nslab = std::min<int>(w.group, kMaxSlabs);
+  int maxslab = kMaxSlabs;
+  if (const char *ev = std::getenv("VBHEM_NSLAB")) maxslab = std::max(1, std::min(8192, std::atoi(ev)));
+  w.nslab = std::min<int>(w.group, maxslab);
   w.slab_len = (int)vbhem_stats_len(K, S, b->d, b->covmode);
   w.flags = cv.take<int>(2 + g * K);
   w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);

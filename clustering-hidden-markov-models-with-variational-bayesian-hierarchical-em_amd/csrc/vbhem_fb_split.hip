@@ -67,73 +67,46 @@ __device__ __forceinline__ double allsum(double v) {
   return v;
 }
 
-// Reduce-scatter: in[LPC*SH] holds this lane's partial sums for every owner's
-// rows (owner o, index k at o*SH+k); out[SH] = sum over the group for rows
-// owned by lane h.  Butterfly: mask 2 then mask 1.
+// Owner-relative ordering: a lane keeps per-owner blocks of SH values indexed by
+// o' = o ^ h (o the owning lane's h), so its own block is always first and the
+// butterfly exchanges below need no selects.  Absolute row of relative index x:
+//   rel_row<SH>(x, h) = ((x / SH) ^ h) * SH + x % SH.
+template <int SH>
+__device__ __forceinline__ int rel_row(int x, int h) {
+  return ((x / SH) ^ h) * SH + x % SH;
+}
+
+// Reduce-scatter: in[LPC*SH] = this lane's partial sums for every owner block
+// (owner-relative order); out[SH] = the group's sums for this lane's rows.
 template <int LPC, int SH>
-__device__ __forceinline__ void reduce_scatter(const double (&in)[LPC * SH], double (&out)[SH], int h) {
+__device__ __forceinline__ void reduce_scatter(const double (&in)[LPC * SH], double (&out)[SH]) {
   if constexpr (LPC == 1) {
 #pragma unroll
     for (int k = 0; k < SH; ++k) out[k] = in[k];
   } else if constexpr (LPC == 2) {
-    const bool hi = h & 1;
 #pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const double mine = hi ? in[SH + k] : in[k];
-      const double send = hi ? in[k] : in[SH + k];
-      out[k] = mine + xchg<1>(send);
-    }
+    for (int k = 0; k < SH; ++k) out[k] = in[k] + xchg<1>(in[SH + k]);
   } else {
-    // round 1 (mask 2): keep owners with bit1 == mine (o = (h&2) + {0,1})
-    const bool b1 = h & 2, b0 = h & 1;
-    double t[2 * SH];
+    double t[2 * SH];  // relative owners 0, 1 (o = h, h ^ 1) summed over lanes h, h ^ 2
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2 * SH; ++q) t[q] = in[q] + xchg<2>(in[2 * SH + q]);
 #pragma unroll
-      for (int k = 0; k < SH; ++k) {
-        const double keep = b1 ? in[(2 + q) * SH + k] : in[q * SH + k];
-        const double send = b1 ? in[q * SH + k] : in[(2 + q) * SH + k];
-        t[q * SH + k] = keep + xchg<2>(send);
-      }
-    // round 2 (mask 1): keep owner o = h
-#pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const double keep = b0 ? t[SH + k] : t[k];
-      const double send = b0 ? t[k] : t[SH + k];
-      out[k] = keep + xchg<1>(send);
-    }
+    for (int k = 0; k < SH; ++k) out[k] = t[k] + xchg<1>(t[SH + k]);
   }
 }
 
-// All-gather: in[SH] (rows of lane h) -> out[LPC*SH] (all rows, owner-major).
+// All-gather: in[SH] (this lane's rows) -> out[LPC*SH] (all rows, owner-relative).
 template <int LPC, int SH>
-__device__ __forceinline__ void all_gather(const double (&in)[SH], double (&out)[LPC * SH], int h) {
-  if constexpr (LPC == 1) {
+__device__ __forceinline__ void all_gather(const double (&in)[SH], double (&out)[LPC * SH]) {
 #pragma unroll
-    for (int k = 0; k < SH; ++k) out[k] = in[k];
-  } else if constexpr (LPC == 2) {
-    const bool hi = h & 1;
+  for (int k = 0; k < SH; ++k) out[k] = in[k];
+  if constexpr (LPC >= 2) {
 #pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const double other = xchg<1>(in[k]);
-      out[k] = hi ? other : in[k];
-      out[SH + k] = hi ? in[k] : other;
-    }
-  } else {
-    const bool b0 = h & 1, b1 = h & 2;
-    double t[2 * SH];  // rows of owners (h & 2) + {0, 1}
+    for (int k = 0; k < SH; ++k) out[SH + k] = xchg<1>(in[k]);
+  }
+  if constexpr (LPC == 4) {
 #pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const double other = xchg<1>(in[k]);
-      t[k] = b0 ? other : in[k];
-      t[SH + k] = b0 ? in[k] : other;
-    }
-#pragma unroll
-    for (int q = 0; q < 2 * SH; ++q) {
-      const double other = xchg<2>(t[q]);
-      out[q] = b1 ? other : t[q];
-      out[2 * SH + q] = b1 ? t[q] : other;
-    }
+    for (int q = 0; q < 2 * SH; ++q) out[2 * SH + q] = xchg<2>(out[q]);
   }
 }
 
@@ -301,7 +274,8 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     double Pz[LPC * SH];
 #pragma unroll
     for (int r = 0; r < LPC * SH; ++r) {
-      const int rr = r < S ? r : S - 1;
+      const int ra = rel_row<SH>(r, h);
+      const int rr = ra < S ? ra : S - 1;
       double ar[SH];
       load_row<S, SH, LPC>(ar, At + rr * S, r0);
       double z = 0.0;
@@ -310,7 +284,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
       Pz[r] = z;
     }
     double Z[SH];
-    reduce_scatter<LPC, SH>(Pz, Z, h);
+    reduce_scatter<LPC, SH>(Pz, Z);
     double sv[SH], zz[SH], lz[SH];
 #pragma unroll
     for (int k = 0; k < SH; ++k) {
@@ -425,7 +399,8 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     double Pz[LPC * SH];
 #pragma unroll
     for (int r = 0; r < LPC * SH; ++r) {
-      const int rr = r < S ? r : S - 1;
+      const int ra = rel_row<SH>(r, h);
+      const int rr = ra < S ? ra : S - 1;
       double ar[SH];
       load_row<S, SH, LPC>(ar, At + rr * S, r0);
       double z = 0.0;
@@ -434,7 +409,7 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
       Pz[r] = z;
     }
     double Z[SH], g[SH];
-    reduce_scatter<LPC, SH>(Pz, Z, h);
+    reduce_scatter<LPC, SH>(Pz, Z);
     {
       double zr[SH], rz[SH];
 #pragma unroll
@@ -447,7 +422,8 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     double Pn[LPC * SH];
 #pragma unroll
     for (int s = 0; s < LPC * SH; ++s) {
-      const int ss = s < S ? s : S - 1;
+      const int sa = rel_row<SH>(s, h);
+      const int ss = sa < S ? sa : S - 1;
       double ac[SH];
       load_row<S, SH, LPC>(ac, AtT + ss * S, r0);
       double a = 0.0;
@@ -456,14 +432,14 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
       Pn[s] = a;
     }
     double Q[SH];
-    reduce_scatter<LPC, SH>(Pn, Q, h);
+    reduce_scatter<LPC, SH>(Pn, Q);
 #pragma unroll
     for (int k = 0; k < SH; ++k) {
       nu[k] = G[k] * Q[k];
       tn[k] += nu[k];
     }
     double Ga[LPC * SH];
-    all_gather<LPC, SH>(G, Ga, h);
+    all_gather<LPC, SH>(G, Ga);
 #pragma unroll
     for (int k = 0; k < SH; ++k)
 #pragma unroll
@@ -482,17 +458,13 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
 #pragma unroll
   for (int r = 0; r < S; ++r) {
     pair_sync<kWaveLocal>();
-    if (valid && h == r / SH) {
-      double hr[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s) hr[s] = H[r % SH][s];
-      lds_st<S>(X + b * LY::XCS, hr);
-    }
+    if (valid && h == r / SH) lds_st<LPC * SH>(X + b * LY::XCS, H[r % SH]);  // owner-relative
     pair_sync<kWaveLocal>();
     if (active && w < S) {
+      const int wr = rel_row<SH>(w, r / SH);  // w's position in row r's owner-relative order
       double acc = 0.0;
 #pragma unroll
-      for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + w];
+      for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + wr];
       p.xi[(lp * S + r) * S + w] = At[r * S + w] * acc;
     }
   }

@@ -5,10 +5,11 @@
 //                      and the per-chunk partial sums Nj = sum_i Z (:282),
 //                      Lt1 = sum Z .* L_elbo, Lt7 = sum hat_Z .* log(hat_Z)
 //                      (vbhemh3m_lb.m:90, 107).
-//   stats_kernel<..>   streaming split-K reduction over this chunk's bases
+//   nm_kernel          streaming weighted sums over this chunk's bases
 //                      (vbhem_compute_Statistics.m:33-55, gate Z > 1e-8):
 //                        N1[j][s]    += g Z(i,j) sum_nu_1(i,j,s)
 //                        M[j][s][r]  += g Z(i,j) sum_xi(i,j,s,r)
+//   stats_kernel<..>   split-K reduction
 //                        U[(j,s)][c] += sum_b (g Z(i,j) sum_t_nu(i,j,s,b)) u(i,b,c)
 //                      with u = [1, mu, packed Sigma + mu mu'] -- the emission
 //                      moments of mex.c:1348-1469 contracted over the base states
@@ -62,41 +63,59 @@ __device__ __forceinline__ void chunk_range(int nb, int i_begin, int chunk, int 
 // ---------------------------------------------------------------------------
 constexpr int kRespThreads = 256;
 
+__device__ __forceinline__ double group_max(double v, int G) {
+  for (int off = G >> 1; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ double group_sum(double v, int G) {
+  for (int off = G >> 1; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// G = lanes per base (power of two >= K, <= 64): 64/G bases per wavefront step.
 __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = kRespThreads / 64;
   const int K = p.K;
-  double *accNj = lds;                 // [NW][K]
-  double *accLt = accNj + NW * K;      // [NW][2]
-  for (int x = tid; x < NW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
+  int G = 1;
+  while (G < K && G < 64) G <<= 1;
+  const int BPW = 64 / G;            // bases per wave step
+  const int sub = lane / G, gl = lane - sub * G;
+  double *accNj = lds;               // [NW*BPW][K]
+  double *accLt = accNj + NW * BPW * K;  // [NW][2]
+  for (int x = tid; x < NW * BPW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
   __syncthreads();
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
   double l1 = 0.0, l7 = 0.0;
-  for (int i = b0 + wave; i < b1; i += NW) {
+  for (int i = b0 + wave * BPW + sub; i - sub < b1; i += NW * BPW) {
     // log_Z = tilde_N .* (logOmega + L_elbo) is rounded before the shift, as in
     // step_fc.m:275-276 (an fma-contracted shift would let the winning entry
     // exceed 1 by ~ulp(log_Z)).
 #pragma clang fp contract(off)
-    const double tn = p.tildeN[i];
-    const double *LL = p.LL + (size_t)i * K;
+    const bool iv = i < b1;
+    const int ii = iv ? i : b0;
+    const double tn = p.tildeN[ii];
+    const double *LL = p.LL + (size_t)ii * K;
     double mx = -INFINITY;
-    for (int j = lane; j < K; j += 64) mx = fmax(mx, tn * (p.logOmega[j] + LL[j]));
-    mx = wave_max(mx);
+    for (int j = gl; j < K; j += G) mx = fmax(mx, tn * (p.logOmega[j] + LL[j]));
+    mx = group_max(mx, G);
     double sm = 0.0;
-    for (int j = lane; j < K; j += 64) sm += exp(tn * (p.logOmega[j] + LL[j]) - mx);
-    sm = wave_sum(sm);
+    for (int j = gl; j < K; j += G) sm += exp(tn * (p.logOmega[j] + LL[j]) - mx);
+    sm = group_sum(sm, G);
     const double lse = mx + log(sm);
-    for (int j = lane; j < K; j += 64) {
-      const double ll = LL[j];
-      const double hz = exp(tn * (p.logOmega[j] + ll) - lse) + 1e-50;
-      const double Z = hz * tn;
-      p.hatZ[(size_t)i * K + j] = hz;
-      p.Z[(size_t)(i - p.i_buf0) * K + j] = Z;
-      accNj[wave * K + j] += Z;
-      l1 += Z * ll;
-      l7 += hz * log(hz);
+    if (iv) {
+      for (int j = gl; j < K; j += G) {
+        const double ll = LL[j];
+        const double hz = exp(tn * (p.logOmega[j] + ll) - lse) + 1e-50;
+        const double Z = hz * tn;
+        p.hatZ[(size_t)i * K + j] = hz;
+        p.Z[(size_t)(i - p.i_buf0) * K + j] = Z;
+        accNj[(wave * BPW + sub) * K + j] += Z;
+        l1 += Z * ll;
+        l7 += hz * log(hz);
+      }
     }
   }
   l1 = wave_sum(l1);
@@ -109,7 +128,7 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   double *slab = p.slabs + (size_t)blockIdx.x * p.slab_len;
   for (int j = tid; j < K; j += kRespThreads) {
     double s = 0.0;
-    for (int w = 0; w < NW; ++w) s += accNj[w * K + j];
+    for (int w = 0; w < NW * BPW; ++w) s += accNj[w * K + j];
     slab[j] += s;
   }
   if (tid < 2) {
@@ -120,13 +139,18 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// stats_kernel<TPW, MAXM>: TPW = max MFMA tiles per wave, MAXM = max M entries
-// per thread (registers).
+// stats_kernel<TPW>: the emission-moment GEMM U (TPW = max MFMA tiles per
+// wave).  Software-pipelined over batches of NBB (<= 4) bases: while batch b
+// is contracted on the MFMA, the loads of batch b+1 (sum_t_nu, Z, covariances,
+// means) are in flight into registers.  N1 / M are summed by nm_kernel.
 // ---------------------------------------------------------------------------
 constexpr int kStatsThreads = 512;
 constexpr int kStatsWaves = kStatsThreads / 64;
+constexpr int kStatsMaxNBB = 4;
+constexpr int kStatsMaxA = 8;   // sum_t_nu values per thread per batch
+constexpr int kStatsMaxR = 8;   // raw covariance / mean values per thread per batch
 
-template <int TPW, int MAXM>
+template <int TPW>
 __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -136,10 +160,15 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
   const int RG = JGc * S, SS = S * S;
   const int MT = (RG + 15) / 16, NTL = (NU + 15) / 16, ntiles = MT * NTL;
   const bool full = p.covmode == kCovFull;
+  const int dd = full ? d * d : d;
+  const int NA = NBB * RG * SB;          // A elements per batch
+  const int NRC = NBB * SB * dd;         // raw covariance values per batch
+  const int NR = NRC + NBB * SB * d;     // + means
 
   double *As = lds;                                   // [RG][AST]   g Z sum_t_nu
   double *Us = As + (size_t)RG * AST;                 // [NBB*SBp][UST] base moments
-  double *gzs = Us + (size_t)NBB * SBp * UST;         // [NBB][JGc]
+  double *raw = Us + (size_t)NBB * SBp * UST;         // [NBB*SB][dd] | [NBB*SB][d]
+  double *gzs = raw + (size_t)NR;                     // [NBB][JGc]
   int *tab = reinterpret_cast<int *>(gzs + (size_t)NBB * JGc);  // [NU] packed (a,b)
 
   for (int x = tid; x < RG * AST + NBB * SBp * UST; x += kStatsThreads) As[x] = 0.0;
@@ -161,86 +190,90 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
   }
 
   const float invNU = 1.0f / (float)NU, invSB = 1.0f / (float)SB, invS = 1.0f / (float)S;
-  const float invSS = 1.0f / (float)SS, invJG = 1.0f / (float)JGc;
+  const float invJG = 1.0f / (float)JGc;
   const float invRSB = 1.0f / (float)(RG * SB);
 
   double4_t acc[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = (double4_t){0.0, 0.0, 0.0, 0.0};
-  double accM[MAXM];
-  int jM[MAXM];
-#pragma unroll
-  for (int e = 0; e < MAXM; ++e) {
-    accM[e] = 0.0;
-    jM[e] = qdiv(tid + e * kStatsThreads, invSS);
-  }
-  double accN1 = 0.0;
-  const int jN1 = qdiv(tid, invS);
 
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
   const double *__restrict__ tnu = p.tnu;
-  const double *__restrict__ xi = p.xi;
-  const double *__restrict__ nu1 = p.nu1;
-  const double *__restrict__ cen = p.centres;
-  const double *__restrict__ cov = p.covars;
-  const size_t dC = full ? (size_t)d * d : (size_t)d;
+
+  // ---- register prefetch buffers ----
+  double pa[kStatsMaxA], pr[kStatsMaxR], pz = 0.0;
+  auto prefetch = [&](int ib) {
+    const int nq = min(NBB, b1 - ib);
+#pragma unroll
+    for (int e = 0; e < kStatsMaxA; ++e) {
+      const int x = tid + e * kStatsThreads;
+      const int q = qdiv(x, invRSB), rem = x - q * RG * SB;
+      pa[e] = (x < NA && q < nq) ? tnu[((size_t)(ib + q - p.i_buf0) * K * S + (size_t)j0 * S) * SB + rem]
+                                 : 0.0;
+    }
+    const size_t gs = (size_t)ib * SB;
+#pragma unroll
+    for (int e = 0; e < kStatsMaxR; ++e) {
+      const int x = tid + e * kStatsThreads;
+      double v = 0.0;
+      if (x < NRC) {
+        if (x < nq * SB * dd) v = p.covars[gs * dd + x];
+      } else if (x < NR) {
+        const int y = x - NRC;
+        if (y < nq * SB * d) v = p.centres[gs * d + y];
+      }
+      pr[e] = v;
+    }
+    if (tid < NBB * JGc) {
+      const int q = qdiv(tid, invJG), jj = tid - q * JGc;
+      pz = q < nq ? p.Z[(size_t)(ib + q - p.i_buf0) * K + j0 + jj] : 0.0;
+    }
+  };
   __syncthreads();
+  if (b0 < b1) prefetch(b0);
 
   for (int ib = b0; ib < b1; ib += NBB) {
     const int nq = min(NBB, b1 - ib);
-    // -- gated Z of the batch, and the base moments u (independent of Z) -------
-    for (int x = tid; x < NBB * JGc; x += kStatsThreads) {
-      const int q = qdiv(x, invJG), jj = x - q * JGc;
-      double z = 0.0;
-      if (q < nq) z = p.Z[(size_t)(ib + q - p.i_buf0) * K + j0 + jj];
-      gzs[x] = (z > 1e-8) ? z : 0.0;
+    // -- commit: gated Z and the raw base data of this batch -> LDS ------------------
+    if (tid < NBB * JGc) gzs[tid] = (pz > 1e-8) ? pz : 0.0;
+#pragma unroll
+    for (int e = 0; e < kStatsMaxR; ++e) {
+      const int x = tid + e * kStatsThreads;
+      if (x < NR) raw[x] = pr[e];
+    }
+    __syncthreads();
+    // -- A = g Z sum_t_nu and the base moments U -------------------------------------
+#pragma unroll
+    for (int e = 0; e < kStatsMaxA; ++e) {
+      const int x = tid + e * kStatsThreads;
+      if (x < NA) {
+        const int q = qdiv(x, invRSB), rem = x - q * RG * SB;
+        const int r = qdiv(rem, invSB), be = rem - r * SB;
+        As[r * AST + q * SBp + be] = (q < nq) ? gzs[q * JGc + qdiv(r, invS)] * pa[e] : 0.0;
+      }
     }
     for (int x = tid; x < NBB * SB * NU; x += kStatsThreads) {
       const int row = qdiv(x, invNU), c = x - row * NU;
       const int q = qdiv(row, invSB), be = row - q * SB;
       double u = 0.0;
       if (q < nq) {
-        const int i = ib + q;
         const int t = tab[c], a = (t & 0xffff) - 1, b = (t >> 16) - 1;
-        const double *mu = cen + ((size_t)i * SB + be) * d;
+        const double *mu = raw + NRC + (size_t)row * d;
         if (a < 0) {
           u = 1.0;
         } else if (b < 0) {
           u = mu[a];
         } else {
-          const double *C = cov + ((size_t)i * SB + be) * dC;
+          const double *C = raw + (size_t)row * dd;
           u = (full ? C[a * d + b] : C[a]) + mu[a] * mu[b];
         }
       }
       Us[(q * SBp + be) * UST + c] = u;
     }
     __syncthreads();
-    // -- A = g Z sum_t_nu (rows r = (j - j0)*S + s, cols q*SBp + beta) ---------
-#pragma unroll 4
-    for (int x = tid; x < NBB * RG * SB; x += kStatsThreads) {
-      const int q = qdiv(x, invRSB), rem = x - q * RG * SB;
-      const int r = qdiv(rem, invSB), be = rem - r * SB;
-      double v = 0.0;
-      if (q < nq) {
-        const size_t pr = (size_t)(ib + q - p.i_buf0) * K * S + (size_t)j0 * S + r;
-        v = gzs[q * JGc + qdiv(r, invS)] * tnu[pr * SB + be];
-      }
-      As[r * AST + q * SBp + be] = v;
-    }
-    // -- N1 / M partial sums (registers) ---------------------------------------
-    for (int q = 0; q < nq; ++q) {
-      const size_t ib_rel = (size_t)(ib + q - p.i_buf0);
-      if (tid < RG) accN1 += gzs[q * JGc + jN1] * nu1[ib_rel * K * S + (size_t)j0 * S + tid];
-      const double *xq = xi + ib_rel * K * SS + (size_t)j0 * SS;
-#pragma unroll
-      for (int e = 0; e < MAXM; ++e) {
-        const int x = tid + e * kStatsThreads;
-        if (x < JGc * SS) accM[e] += gzs[q * JGc + jM[e]] * xq[x];
-      }
-    }
-    __syncthreads();
-    // -- MFMA: acc[tile] += A[16 rows, 4 k] x U[4 k, 16 cols] -------------------
+    // -- next batch's loads fly while this batch is contracted --------------------------
+    if (ib + NBB < b1) prefetch(ib + NBB);
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       const int tile = wave + t * kStatsWaves;
@@ -263,13 +296,6 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
 
   // -- slab (this chunk) += partials ------------------------------------------
   double *slab = p.slabs + (size_t)blockIdx.x * p.slab_len;
-  if (tid < RG) slab[K + (size_t)j0 * S + tid] += accN1;
-  double *slabM = slab + K + (size_t)K * S + (size_t)j0 * SS;
-#pragma unroll
-  for (int e = 0; e < MAXM; ++e) {
-    const int x = tid + e * kStatsThreads;
-    if (x < JGc * SS) slabM[x] += accM[e];
-  }
   double *slabU = slab + K + (size_t)K * S + (size_t)K * SS + 2;
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
@@ -284,7 +310,56 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
       }
     }
   }
-  (void)invS;
+}
+
+// ---------------------------------------------------------------------------
+// nm_kernel: N1[j][s] += g Z(i,j) sum_nu_1(i,j,s) and M[j][s][r] += g Z(i,j)
+// sum_xi(i,j,s,r) over this chunk's bases -- plain streaming weighted sums
+// (each thread owns fixed outputs; 4 bases in flight per step).
+// ---------------------------------------------------------------------------
+constexpr int kNmThreads = 256;
+
+// PER outputs per thread (K*S + K*S*S <= PER * 256), UNR bases per step in flight.
+template <int PER, int UNR>
+__global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
+  const int tid = threadIdx.x;
+  const int K = p.K, S = p.S, KS = K * S, KSS = KS * S, NO = KS + KSS;
+  int b0, b1;
+  chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
+  double acc[PER];
+  int jo[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    acc[e] = 0.0;
+    const int x = tid + e * kNmThreads;
+    jo[e] = x < KS ? x / S : (x < NO ? (x - KS) / (S * S) : 0);
+  }
+  for (int i = b0; i < b1; i += UNR) {
+    double v[UNR][PER], z[UNR][PER];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool iv = i + u < b1;
+      const size_t ir = (size_t)((iv ? i + u : i) - p.i_buf0);
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int x = tid + e * kNmThreads;
+        const int xc = x < NO ? x : 0;
+        v[u][e] = xc < KS ? p.nu1[ir * KS + xc] : p.xi[ir * KSS + (xc - KS)];
+        const double zz = p.Z[ir * K + jo[e]];
+        z[u][e] = (iv && x < NO && zz > 1e-8) ? zz : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int e = 0; e < PER; ++e) acc[e] = fma(z[u][e], v[u][e], acc[e]);
+  }
+  double *slab = p.slabs + (size_t)blockIdx.x * p.slab_len + K;  // [N1 | M]
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int x = tid + e * kNmThreads;
+    if (x < NO) slab[x] += acc[e];
+  }
 }
 
 // 256 threads = 32 columns x 8 slab partitions: partition p sums slabs
@@ -313,11 +388,13 @@ __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, i
 // planning + launch
 // ---------------------------------------------------------------------------
 namespace {
-constexpr size_t kStatsLdsTarget = 64 * 1024;  // two 512-thread blocks per CU
-constexpr int kMaxTPW = 16, kMaxM = 16;
+constexpr size_t kStatsLdsTarget = 78 * 1024;  // two 512-thread blocks per CU
+constexpr int kMaxTPW = 16;
 
-size_t stats_lds_bytes(int RG, int AST, int NBB, int SBp, int UST, int JG, int NU) {
-  return ((size_t)RG * AST + (size_t)NBB * SBp * UST + (size_t)NBB * JG) * sizeof(double) +
+size_t stats_lds_bytes(int RG, int AST, int NBB, int SBp, int UST, int JG, int NU, int SB, int d,
+                       int dd) {
+  return ((size_t)RG * AST + (size_t)NBB * SBp * UST + (size_t)NBB * SB * (dd + d) +
+          (size_t)NBB * JG) * sizeof(double) +
          (size_t)NU * sizeof(int);
 }
 }  // namespace
@@ -335,37 +412,42 @@ bool plan_stats(StatsArgs &a, size_t &lds, int &ngroups) {
   const int RG = jg * S;
   const int ntiles = ((RG + 15) / 16) * NTL;
   if ((ntiles + kStatsWaves - 1) / kStatsWaves > kMaxTPW) return false;
-  if ((jg * S * S + kStatsThreads - 1) / kStatsThreads > kMaxM) return false;
+  if (K * S + K * S * S > 24 * kNmThreads) return false;
   if (RG > kStatsThreads) return false;
-  int nbb = 8;
+  const int dd = a.covmode == kCovFull ? a.d * a.d : a.d;
+  int nbb = kStatsMaxNBB;
   for (; nbb >= 1; --nbb) {
+    const bool regs_ok = (nbb * RG * a.SB + kStatsThreads - 1) / kStatsThreads <= kStatsMaxA &&
+                         (nbb * a.SB * (dd + a.d) + kStatsThreads - 1) / kStatsThreads <= kStatsMaxR;
     a.NBB = nbb;
     a.AST = nbb * a.SBp + 1;
-    lds = stats_lds_bytes(RG, a.AST, nbb, a.SBp, a.UST, jg, a.NU);
-    if (lds <= kStatsLdsTarget) break;
+    lds = stats_lds_bytes(RG, a.AST, nbb, a.SBp, a.UST, jg, a.NU, a.SB, a.d, dd);
+    if (regs_ok && lds <= kStatsLdsTarget) break;
   }
-  if (nbb < 1) {
-    a.NBB = 1;
-    a.AST = a.SBp + 1;
-    lds = stats_lds_bytes(RG, a.AST, 1, a.SBp, a.UST, jg, a.NU);
-    if (lds > 160 * 1024) return false;
-  }
+  if (nbb < 1) return false;
   return true;
 }
 
-template <int TPW, int MAXM>
+template <int TPW>
 static hipError_t launch_stats_t(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
                                  hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_kernel<TPW, MAXM>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_kernel<TPW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((stats_kernel<TPW, MAXM>), dim3(nchunk, ngroups), dim3(kStatsThreads), lds, st,
-                     a);
+  hipLaunchKernelGGL((stats_kernel<TPW>), dim3(nchunk, ngroups), dim3(kStatsThreads), lds, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int no = a.K * a.S + a.K * a.S * a.S;
+  if (no <= 6 * kNmThreads)
+    hipLaunchKernelGGL((nm_kernel<6, 4>), dim3(nchunk), dim3(kNmThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL((nm_kernel<24, 1>), dim3(nchunk), dim3(kNmThreads), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
-  const size_t lds = ((size_t)(kRespThreads / 64) * (a.K + 2)) * sizeof(double);
+  int G = 1;
+  while (G < a.K && G < 64) G <<= 1;
+  const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2)) * sizeof(double);
   hipLaunchKernelGGL(resp_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
   return hipGetLastError();
 }
@@ -374,11 +456,9 @@ hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
   const int RG = a.JG * a.S;
   const int ntiles = ((RG + 15) / 16) * ((a.NU + 15) / 16);
   const int tpw = (ntiles + kStatsWaves - 1) / kStatsWaves;
-  const int m = (a.JG * a.S * a.S + kStatsThreads - 1) / kStatsThreads;
-  if (tpw <= 4 && m <= 4) return launch_stats_t<4, 4>(a, nchunk, ngroups, lds, st);
-  if (tpw <= 8 && m <= 4) return launch_stats_t<8, 4>(a, nchunk, ngroups, lds, st);
-  if (tpw <= 8) return launch_stats_t<8, 16>(a, nchunk, ngroups, lds, st);
-  return launch_stats_t<16, 16>(a, nchunk, ngroups, lds, st);
+  if (tpw <= 4) return launch_stats_t<4>(a, nchunk, ngroups, lds, st);
+  if (tpw <= 8) return launch_stats_t<8>(a, nchunk, ngroups, lds, st);
+  return launch_stats_t<16>(a, nchunk, ngroups, lds, st);
 }
 
 hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
