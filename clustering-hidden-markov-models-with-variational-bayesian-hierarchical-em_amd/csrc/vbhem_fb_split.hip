@@ -41,8 +41,9 @@ constexpr double kZMinS = 1e-200;
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
   const int lo = __double2loint(v), hi = __double2hiint(v);
-  const int lo2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false);
-  const int hi2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false);
+  // bound_ctrl: no 'old' operand to initialise (quad_perm never reads out of bounds)
+  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, true);
+  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi2, lo2);
 }
 constexpr int kXor1 = 0xB1;  // quad_perm [1,0,3,2]
@@ -252,6 +253,17 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
   __syncthreads();
 
   // ---------------- K2: backward recursion -------------------------------------------------
+  // A'(rows of every owner block, my columns r0..r0+SH): register-resident for both sweeps
+  // (occupancy is bounded by LDS, not registers)
+  constexpr bool kAtReg = LPC * SH * SH <= 48;  // <= 96 VGPRs
+  double atr[kAtReg ? LPC * SH : 1][SH];
+  if constexpr (kAtReg) {
+#pragma unroll
+    for (int r = 0; r < LPC * SH; ++r) {
+      const int ra = rel_row<SH>(r, h);
+      load_row<S, SH, LPC>(atr[r], At + (ra < S ? ra : S - 1) * S, r0);
+    }
+  }
   double am[SH];  // amax of my rows (LDS -> registers once)
 #pragma unroll
   for (int k = 0; k < SH; ++k) am[k] = amax[r0 + k < S ? r0 + k : S - 1];
@@ -274,10 +286,14 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     double Pz[LPC * SH];
 #pragma unroll
     for (int r = 0; r < LPC * SH; ++r) {
-      const int ra = rel_row<SH>(r, h);
-      const int rr = ra < S ? ra : S - 1;
       double ar[SH];
-      load_row<S, SH, LPC>(ar, At + rr * S, r0);
+      if constexpr (kAtReg) {
+#pragma unroll
+        for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
+      } else {
+        const int ra = rel_row<SH>(r, h);
+        load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
+      }
       double z = 0.0;
 #pragma unroll
       for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
@@ -399,10 +415,14 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     double Pz[LPC * SH];
 #pragma unroll
     for (int r = 0; r < LPC * SH; ++r) {
-      const int ra = rel_row<SH>(r, h);
-      const int rr = ra < S ? ra : S - 1;
       double ar[SH];
-      load_row<S, SH, LPC>(ar, At + rr * S, r0);
+      if constexpr (kAtReg) {
+#pragma unroll
+        for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
+      } else {
+        const int ra = rel_row<SH>(r, h);
+        load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
+      }
       double z = 0.0;
 #pragma unroll
       for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
