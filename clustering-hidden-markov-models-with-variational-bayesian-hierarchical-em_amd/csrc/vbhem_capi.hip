@@ -149,7 +149,8 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
     const int off_F = (off_Y + ppb * S + 1) / 2 * 2;
     const int off_R = (off_F + (ppb + 1) / 2 + 1) / 2 * 2;
     const size_t lattice = (size_t)std::max(0, T - 2) * SH * NT;
-    const size_t lds = ((size_t)off_R + std::max<size_t>(lattice, 2)) * sizeof(double);
+    const size_t xi_park = S > 8 ? (size_t)ppb * S * S * LPC * SH : 0;  // parked H blocks (sum_xi)
+    const size_t lds = ((size_t)off_R + std::max<size_t>(std::max(lattice, xi_park), 2)) * sizeof(double);
     if (lds > kLdsLimit) continue;
     const double util = double(ppb * LPP) / NT;
     if (util > best + 0.02) {

@@ -474,18 +474,43 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
     for (int k = 0; k < SH; ++k)
       if (r0 + k < S) p.tnu[(lp * S + r0 + k) * SB + b] = tn[k];
   }
-  // sum_xi(r, s) = A'(r, s) * sum_b H_b(r, s): one pair-wide reduction per row r
+  // sum_xi(r, s) = A'(r, s) * sum_b H_b(r, s).
+  //  S > 8 : every lane parks its H block in the (now dead) lattice region, one
+  //          barrier, then each lane of the pair reduces S*S/LPP outputs;
+  //  S <= 8: one wave-local round per row r through the pair's slab.
+  if constexpr (S > 8) {
+    constexpr int HW = LPC * SH;                      // values per H row (owner-relative)
+    __syncthreads();                                  // all lattice reads of the block done
+    double *Hq = R + (size_t)(valid ? q : 0) * S * S * HW;   // [b][r][HW]
+    if (valid && b < S) {
 #pragma unroll
-  for (int r = 0; r < S; ++r) {
-    pair_sync<kWaveLocal>();
-    if (valid && h == r / SH) lds_st<LPC * SH>(X + b * LY::XCS, H[r % SH]);  // owner-relative
-    pair_sync<kWaveLocal>();
-    if (active && w < S) {
-      const int wr = rel_row<SH>(w, r / SH);  // w's position in row r's owner-relative order
-      double acc = 0.0;
+      for (int k = 0; k < SH; ++k)
+        if (r0 + k < S) lds_st<HW>(Hq + ((size_t)b * S + r0 + k) * HW, H[k]);
+    }
+    __syncthreads();
+    if (active) {
+      for (int o = w; o < S * S; o += LPP) {
+        const int r = o / S, s2 = o - r * S;
+        const int sr = rel_row<SH>(s2, r / SH);       // s2 in row r's owner-relative order
+        double acc = 0.0;
 #pragma unroll
-      for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + wr];
-      p.xi[(lp * S + r) * S + w] = At[r * S + w] * acc;
+        for (int be = 0; be < S; ++be) acc += Hq[((size_t)be * S + r) * HW + sr];
+        p.xi[lp * S * S + o] = At[o] * acc;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+      pair_sync<kWaveLocal>();
+      if (valid && h == r / SH) lds_st<LPC * SH>(X + b * LY::XCS, H[r % SH]);  // owner-relative
+      pair_sync<kWaveLocal>();
+      if (active && w < S) {
+        const int wr = rel_row<SH>(w, r / SH);  // w's position in row r's owner-relative order
+        double acc = 0.0;
+#pragma unroll
+        for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + wr];
+        p.xi[(lp * S + r) * S + w] = At[r * S + w] * acc;
+      }
     }
   }
   // fallback flags (one per pair)
