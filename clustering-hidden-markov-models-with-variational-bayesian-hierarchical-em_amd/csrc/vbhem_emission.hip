@@ -149,13 +149,15 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
     const double2 *src = reinterpret_cast<const double2 *>(p.covars + g0 * dd);
     const int n2 = ccount * dd / 2;
 #pragma unroll
-    for (int k = 0; k < kPre; ++k) {
+    for (int k = 0; k < kPre; ++k) {  // clamped, unconditional loads (no branch + wait)
       const int x = lane + 64 * k;
-      pre_c[k] = (x < n2) ? src[x] : make_double2(0.0, 0.0);
+      const double2 v = src[x < n2 ? x : 0];
+      pre_c[k] = (x < n2) ? v : make_double2(0.0, 0.0);
     }
     const double2 *ms = reinterpret_cast<const double2 *>(p.centres + g0 * d);
     const int nm2 = ccount * d / 2;
-    pre_m = lane < nm2 ? ms[lane] : make_double2(0.0, 0.0);
+    const double2 vm = ms[lane < nm2 ? lane : 0];
+    pre_m = lane < nm2 ? vm : make_double2(0.0, 0.0);
   };
   if (RAW && ct < nctile) prefetch(ct);
 

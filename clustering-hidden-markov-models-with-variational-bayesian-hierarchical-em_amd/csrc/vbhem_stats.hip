@@ -336,6 +336,8 @@ __global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
   }
   for (int i = b0; i < b1; i += UNR) {
     double v[UNR][PER], z[UNR][PER];
+    // branch-free: clamped addresses and unconditional loads (a conditional load
+    // becomes a branch with its own vmcnt(0) wait and serialises the stream)
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const bool iv = i + u < b1;
@@ -344,8 +346,18 @@ __global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
       for (int e = 0; e < PER; ++e) {
         const int x = tid + e * kNmThreads;
         const int xc = x < NO ? x : 0;
-        v[u][e] = xc < KS ? p.nu1[ir * KS + xc] : p.xi[ir * KSS + (xc - KS)];
-        const double zz = p.Z[ir * K + jo[e]];
+        const double *src = xc < KS ? p.nu1 + ir * KS + xc : p.xi + ir * KSS + (xc - KS);
+        v[u][e] = *src;
+        z[u][e] = p.Z[ir * K + jo[e]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool iv = i + u < b1;
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int x = tid + e * kNmThreads;
+        const double zz = z[u][e];
         z[u][e] = (iv && x < NO && zz > 1e-8) ? zz : 0.0;
       }
     }
