@@ -330,9 +330,11 @@ def synth_workload(name: str, seed: Optional[int] = None, device="cpu", N: Optio
                           ragged=ragged, n_total=n, i_offset=lo)
     opt = default_options(cfg["K"], cfg["S"], cfg["d"], tau=cfg["tau"], Nv=cfg["Nv"],
                           covmode=cfg["covmode"], **cfg["opt"])
-    if lo == 0 and (hi - lo) >= min(n, 4096):
+    if shard is None and n <= 4096:
         init = base
     else:
+        # every shard (and the unsharded large case) draws the initial clusters from the
+        # same standalone first-4096-bases set, so all ranks hold identical posteriors
         init = synth_base_set(min(n, 4096), *args, seed, device=device, exprmt1=ex, ragged=ragged,
                               n_total=n)
     rb, rg, om = baseem_draws(init, cfg["K"], cfg["S"], seed)

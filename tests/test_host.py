@@ -191,13 +191,21 @@ def test_shard_range_partitions(vb):
             assert max(sizes) - min(sizes) <= 1
 
 
-def test_synth_workload_shards_consistent(vb):
+@pytest.mark.parametrize("N", [300, 6000])
+def test_synth_workload_shards_consistent(vb, N):
     """A shard generated alone equals the same rows of the whole set only in
-    shape/semantics (per-shard seeding); the cluster posterior is identical."""
-    b0, P0, _ = vb.synth_workload("C3", N=300, shard=(0, 150))
-    b1, P1, _ = vb.synth_workload("C3", N=300, shard=(150, 300))
-    assert b0.N == 150 and b1.N == 150
+    shape/semantics (per-shard seeding); the cluster posterior is identical on
+    every shard -- and, above 4096 bases, identical to the unsharded run -- so
+    all ranks of a multi-GPU run start from the same h3m_r."""
+    h = N // 2
+    b0, P0, _ = vb.synth_workload("C3", N=N, shard=(0, h))
+    b1, P1, _ = vb.synth_workload("C3", N=N, shard=(h, N))
+    assert b0.N == h and b1.N == N - h
     for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
         np.testing.assert_array_equal(getattr(P0, k), getattr(P1, k))
-    np.testing.assert_allclose(b0.omega.sum() + b1.omega.sum(), 1.0, rtol=1e-14)
+    if N > 4096:
+        _, Pu, _ = vb.synth_workload("C3", N=N)
+        for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+            np.testing.assert_array_equal(getattr(P0, k), getattr(Pu, k))
+    np.testing.assert_allclose((b0.omega.sum() + b1.omega.sum()).item(), 1.0, rtol=1e-13)
     assert torch.equal(b0.omega, b1.omega)
