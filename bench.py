@@ -127,6 +127,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4")
     ap.add_argument("--N", type=int, default=None, help="override the number of base HMMs")
+    ap.add_argument("--tau", type=int, default=None, help="override tau (experiments only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -152,6 +153,8 @@ def main():
     cfg = vb.CONFIGS[args.config]
     N = args.N or cfg["N"]
     K, S, Sb, d, T, cov = cfg["K"], cfg["S"], cfg["Sb"], cfg["d"], cfg["tau"], cfg["covmode"]
+    if args.tau is not None:
+        T = args.tau
     lo, hi = shard_range(N, rank, world)
     base, post, opt = vb.synth_workload(args.config, device=dev, N=N, shard=(lo, hi))
     eng = EStepEngine(base, K, S, T, device=dev)
