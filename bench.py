@@ -42,9 +42,17 @@ def flops_per_pair(S, Sb, d, T, covmode):
 def fb_flops_per_pair(S, Sb, T):
     """The part fb_split_kernel executes: K2 backward + K3 termination + K4
     forward (K1 runs in emission_kernel, K5 in stats_kernel)."""
-    k2 = (T - 1) * S * (2 * S * Sb + 2 * Sb * Sb + S * Sb)
-    k4 = (T - 1) * (2 * S * Sb * Sb + 3 * S * S * Sb)
-    return k2 + k4 + 2 * S * Sb
+    return bwd_flops_per_pair(S, Sb, T) + fwd_flops_per_pair(S, Sb, T)
+
+
+def bwd_flops_per_pair(S, Sb, T):
+    """K2 backward + K3 termination (the gated schedule's first pass, every pair)."""
+    return (T - 1) * S * (2 * S * Sb + 2 * Sb * Sb + S * Sb) + 2 * S * Sb
+
+
+def fwd_flops_per_pair(S, Sb, T):
+    """K4 forward (the gated schedule's second pass, gated pairs only)."""
+    return (T - 1) * (2 * S * Sb * Sb + 3 * S * S * Sb)
 
 
 def emission_flops_per_pair(S, Sb, d, covmode):
@@ -58,18 +66,19 @@ def transcendentals_per_pair(S, Sb, T):
     return T * S * S * Sb, T * S * Sb
 
 
-def fb_bytes_per_pair(S, Sb, d, covmode, K, split=True):
+def fb_bytes_per_pair(S, Sb, d, covmode, K, split=True, backward_only=False):
     """Algorithmic HBM bytes of one fb-kernel pair.  Split path: its 1/K share
     of the base transitions/prior + its E tile (emission_kernel output) + its
-    outputs (LL, nu_1, sum_xi, sum_t_nu).  Generic path: base emissions instead of E."""
-    out = (1 + S + S * S + S * Sb) * 8
+    outputs (LL, nu_1, sum_xi, sum_t_nu; LL alone for the backward pass).
+    Generic path: base emissions instead of E."""
+    out = 8 if backward_only else (1 + S + S * S + S * Sb) * 8
     if split:
         return (Sb + Sb * Sb) * 8 / K + S * Sb * 8 + out
     dC = d * d if covmode == 1 else d
     return (Sb + Sb * Sb + Sb * d + Sb * dC) * 8 / K + out
 
 
-def committed_traffic(config, N, world, split):
+def committed_traffic(config, N, world, want):
     """HBM bytes per launch of the E-step kernel from the newest committed PMC
     summary for this config (profiles/rNN_<config>.json, made by
     scripts/profile.sh + scripts/prof_summary.py; FETCH_SIZE x2 + WRITE_SIZE per
@@ -77,7 +86,6 @@ def committed_traffic(config, N, world, split):
     run, so the value is read back here; None when no summary matches."""
     import glob
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config.lower()}.json")))
-    want = "vbhem::fb_split_kernel" if split else "vbhem::fb_pairs_kernel"
     for path in reversed(cands):
         try:
             with open(path) as f:
@@ -87,7 +95,7 @@ def committed_traffic(config, N, world, split):
         if summ.get("N") not in (None, N) or summ.get("n_gpus", 1) != world:
             continue
         for name, k in summ.get("kernels", {}).items():
-            if name.startswith(want) and "hbm_bytes_per_launch" in k:
+            if name == want and "hbm_bytes_per_launch" in k:
                 return k["hbm_bytes_per_launch"]["traffic"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -191,6 +199,31 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
     tk = _capi.timing_read()
+    # fraction of pairs the gate Z > 1e-8 keeps (the gated schedule's second pass)
+    zk = (eng.hatZ * tN.view(-1, 1)) > 1e-8
+    n_gated = int(zk.sum().item())
+    if world > 1:
+        ng = torch.tensor([n_gated], dtype=torch.float64, device=dev)
+        dist.all_reduce(ng)
+        n_gated = int(ng.item())
+
+    # the dense schedule (both sweeps for every pair, same outputs) on the same
+    # inputs, for reference: a few steps, reported beside `value`
+    dense_steps = max(1, min(args.steps, 5))
+    prev_mode = _capi.set_fused_mode(_capi.FUSED_DENSE)
+    step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    td0 = time.perf_counter()
+    for _ in range(dense_steps):
+        dstats = step()
+    torch.cuda.synchronize()
+    dtd = torch.tensor([time.perf_counter() - td0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dtd, op=dist.ReduceOp.MAX)
+    _capi.set_fused_mode(prev_mode)
+    dense_rel = float((dstats - stats).abs().max() / stats.abs().max().clamp_min(1e-300))
 
     # host M-step + ELBO cost of one full EM iteration (reported, not in value)
     th0 = time.perf_counter()
@@ -206,15 +239,22 @@ def main():
             dist.destroy_process_group()
         return
 
-    n_local_pairs = (hi - lo) * K
     fb_launch_ms = tk["fb_ms"] / max(1, tk["fb_launches"])
     pairs_per_launch = tk["fb_pairs"] / max(1, tk["fb_launches"])
     split = S <= 16 and Sb <= S and d <= 64
-    fpp = fb_flops_per_pair(S, Sb, T) if split else flops_per_pair(S, Sb, d, T, cov)
+    gated = split and tk["gated_fwd_launches"] > 0
+    if gated:
+        fpp = bwd_flops_per_pair(S, Sb, T)
+    else:
+        fpp = fb_flops_per_pair(S, Sb, T) if split else flops_per_pair(S, Sb, d, T, cov)
     achieved = fpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e12
-    bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split)
+    bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split, backward_only=gated)
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
-    traffic, traffic_src = committed_traffic(args.config, N, world, split)
+    lpc = 1 if S <= 4 else 2 if S <= 8 else 4
+    kname = (f"vbhem::fb_split_kernel<{S}, {lpc}, {1 if gated else 0}>" if split
+             else "vbhem::fb_pairs_kernel")
+    traffic, traffic_src = committed_traffic(args.config, N, world, kname)
+    gf_ms = tk["gated_fwd_ms"] / max(1, tk["gated_fwd_launches"])
     res = {
         "metric": METRIC,
         "value": args.steps / dt,
@@ -242,22 +282,32 @@ def main():
             "frac": achieved / PEAK_FP64_TFLOPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "fb_split_kernel" if split else "fb_pairs_kernel",
+            "kernel": kname,
             "kernel_ms": fb_launch_ms,
             "flops_per_pair": fpp,
             "pairs_per_launch": pairs_per_launch,
             "note": ("fp64 compute-bound (VALU + software exp/log); peak = MI355X FP64 dense "
                      "78.6 TF/s (vector = matrix rate); flops counted on the reference "
-                     "recurrences this kernel runs (K2-K4), excluding exp/log"),
+                     "recurrences this kernel runs (" + ("K2 backward + K3 termination, every "
+                     "pair" if gated else "K2-K4") + "), excluding exp/log"),
             "hbm": {"algorithmic_bytes_per_launch": bpp * pairs_per_launch,
                     "achieved_GBs": bpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e9,
                     "peak_GBs": PEAK_HBM_GBS,
                     "frac": bpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
             "exp_log_per_pair_reference": [n_exp, n_log],
         },
+        "schedule": "gated" if gated else "dense",
+        "gated_pairs_frac": n_gated / float(N * K),
+        "gated_forward": ({"kernel": f"vbhem::fb_split_kernel<{S}, {lpc}, 2>", "kernel_ms": gf_ms,
+                           "pairs_per_launch": n_gated / world,
+                           "flops_per_pair": fb_flops_per_pair(S, Sb, T),
+                           "achieved_TFLOPs": fb_flops_per_pair(S, Sb, T) * n_gated / world
+                           / max(gf_ms * 1e-3, 1e-12) / 1e12} if gated else None),
+        "dense_schedule": {"value": dense_steps / float(dtd.item()), "unit": "E-steps/s",
+                           "steps": dense_steps, "max_rel_diff_vs_gated": dense_rel},
         "emission_kernel_ms": tk["em_ms"] / max(1, tk["em_launches"]),
-        "stats_kernel_ms": tk["stats_ms"] / max(1, tk["stats_launches"]),
-        "algorithmic_tflops_per_s_whole_estep": flops_per_pair(S, Sb, d, T, cov) * N * K * args.steps / dt / 1e12,
+        "stats_kernels_ms_per_step": tk["stats_ms"] / args.steps,
+        "reference_equivalent_tflops_per_s": flops_per_pair(S, Sb, d, T, cov) * N * K * args.steps / dt / 1e12,
         "host_mstep_ms": host_ms,
         "elbo": L,
     }

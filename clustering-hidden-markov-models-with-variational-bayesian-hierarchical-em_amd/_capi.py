@@ -49,6 +49,9 @@ EXPORTS = {
                                    ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_timing_read_emission": (_c_int, [ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_longlong)]),
+    "vbhem_timing_read_gated": (_c_int, [ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_longlong)]),
+    "vbhem_set_fused_mode": (_c_int, [_c_int]),
     "vbhem_last_error": (ctypes.c_char_p, []),
     "vbhem_version": (ctypes.c_char_p, []),
 }
@@ -100,5 +103,17 @@ def timing_read() -> dict:
     em, ne = ctypes.c_double(), ctypes.c_longlong()
     check(lib().vbhem_timing_read_emission(ctypes.byref(em), ctypes.byref(ne)),
           "vbhem_timing_read_emission")
+    gf, ng = ctypes.c_double(), ctypes.c_longlong()
+    check(lib().vbhem_timing_read_gated(ctypes.byref(gf), ctypes.byref(ng)),
+          "vbhem_timing_read_gated")
     return dict(fb_ms=fb.value, fb_launches=nf.value, fb_pairs=npairs.value,
-                stats_ms=st.value, stats_launches=ns.value, em_ms=em.value, em_launches=ne.value)
+                stats_ms=st.value, stats_launches=ns.value, em_ms=em.value, em_launches=ne.value,
+                gated_fwd_ms=gf.value, gated_fwd_launches=ng.value)
+
+
+FUSED_GATED, FUSED_DENSE = 0, 1
+
+
+def set_fused_mode(mode: int) -> int:
+    """Fused E-step schedule (FUSED_GATED default, FUSED_DENSE); returns the previous one."""
+    return int(lib().vbhem_set_fused_mode(int(mode)))

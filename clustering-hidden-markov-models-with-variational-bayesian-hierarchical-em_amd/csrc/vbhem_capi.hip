@@ -26,10 +26,16 @@ thread_local std::string g_err;
 // synchronised) only by vbhem_timing_read.  Off by default (graph capture).
 struct TimingState {
   bool on = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em, gf;
   std::vector<long long> fb_pairs;
 };
 TimingState g_timing;
+
+// fused schedule (vbhem_set_fused_mode; VBHEM_FUSED_DENSE=1 in the environment)
+int g_fused_mode = [] {
+  const char *ev = std::getenv("VBHEM_FUSED_DENSE");
+  return (ev && std::atoi(ev) != 0) ? VBHEM_FUSED_DENSE : VBHEM_FUSED_GATED;
+}();
 
 hipEvent_t timing_event(hipStream_t st) {
   hipEvent_t ev = nullptr;
@@ -122,7 +128,9 @@ bool plan_fb(int SB, int d, int covmode, int K, int S, int T, FbPlan &out) {
 struct SplitPlan {
   bool ok = false;
   vbhem::SplitArgs a{};
-  size_t lds = 0;
+  size_t lds = 0;       // kFbDense
+  size_t lds_bwd = 0;   // kFbBackward (no lattice)
+  size_t lds_list = 0;  // kFbList (lattice + work-item prefix)
   int ppb = 0;
 };
 
@@ -130,11 +138,7 @@ struct SplitPlan {
 SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
   SplitPlan sp;
   if (!vbhem::split_supported(S, SB, d)) return sp;
-  int LPC = vbhem::split_lpc(S);
-  if (const char *ev = std::getenv("VBHEM_SPLIT_LPC")) {
-    const int v = std::atoi(ev);
-    if (v == 4 && S >= 5 && S <= 8) LPC = 4;
-  }
+  const int LPC = vbhem::split_lpc(S);
   const int SH = (S + LPC - 1) / LPC;
   const int LPP = S * LPC;
   const int XCS = (LPC * SH + 1) / 2 * 2 + 2;
@@ -150,16 +154,22 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
     const int off_R = (off_F + (ppb + 1) / 2 + 1) / 2 * 2;
     const size_t lattice = (size_t)std::max(0, T - 2) * SH * NT;
     const size_t xi_park = S > 8 ? (size_t)ppb * S * S * LPC * SH : 0;  // parked H blocks (sum_xi)
-    const size_t lds = ((size_t)off_R + std::max<size_t>(std::max(lattice, xi_park), 2)) * sizeof(double);
-    if (lds > kLdsLimit) continue;
+    const size_t region = std::max<size_t>(std::max(lattice, xi_park), 2);
+    const size_t lds = ((size_t)off_R + region) * sizeof(double);
+    const int off_L = (int)(off_R + region);
+    const size_t lds_list = ((size_t)off_L + ((size_t)K + 2) / 2) * sizeof(double);
+    if (lds_list > kLdsLimit) continue;
     const double util = double(ppb * LPP) / NT;
     if (util > best + 0.02) {
       best = util;
       vbhem::SplitArgs &x = sp.a;
       x.SB = SB; x.d = d; x.covmode = covmode; x.K = K; x.S = S; x.T = T; x.nwb = nwb;
       x.lpc = LPC;
-      x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R;
+      x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R; x.off_L = off_L;
+      x.mode = vbhem::kFbDense;
       sp.lds = lds;
+      sp.lds_bwd = ((size_t)off_R + 2) * sizeof(double);
+      sp.lds_list = lds_list;
       sp.ppb = ppb;
       sp.ok = true;
     }
@@ -235,6 +245,7 @@ struct FusedWs {
   int nslab;
   int slab_len;
   int *flags;
+  int *gate_cnt, *list, *list_tot;  // gated schedule: [nslab][K], [K][group], [K]
   double *scratch, *nu1, *xi, *tnu, *Z, *slabs;
   double *E, *W, *bias, *shift;
 };
@@ -261,6 +272,9 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.W = cv.take<double>(emission_kd(b->d, b->covmode) * K * S);
   w.bias = cv.take<double>((size_t)K * S);
   w.shift = cv.take<double>((size_t)b->d);
+  w.gate_cnt = cv.take<int>((size_t)w.nslab * K);
+  w.list = cv.take<int>(g * K);
+  w.list_tot = cv.take<int>((size_t)K);
   return cv.off + 256;
 }
 
@@ -305,9 +319,54 @@ int run_emission_prep(FbCtx &c, double *W, double *bias, double *shift, hipStrea
   return VBHEM_OK;
 }
 
+// Persistent grid of the list-mode pass: every resident block of the device.
+unsigned list_grid(const vbhem::SplitArgs &a, size_t lds) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+  }
+  const int per_cu = std::max(1, vbhem::split_resident_blocks(a, lds));
+  return (unsigned)(cus * per_cu);
+}
+
+// Gated schedule, second pass: both sweeps for the pairs of the gate lists.
+int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1, double *xi,
+                double *tnu, const double *Ebuf, long long e_ld, const int *list,
+                const int *list_tot, int list_cap, int *flags, double *scratch, double *LL,
+                hipStream_t st) {
+  if (i_end <= i_begin) return VBHEM_OK;
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  vbhem::SplitArgs ca = c.split.a;
+  ca.mode = vbhem::kFbList;
+  ca.E = Ebuf; ca.e_ld = e_ld;
+  ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
+  ca.LL = nullptr; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
+  ca.flag_count = flags; ca.flag_list = flags + 2;
+  ca.list = list; ca.list_tot = list_tot; ca.list_cap = list_cap;
+  hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
+  e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_list), c.split.lds_list, st);
+  if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
+  if (g_timing.on) g_timing.gf.emplace_back(ev0, timing_event(st));
+  vbhem::FbArgs a = c.plan.a;
+  a.i_begin = i_begin; a.i_end = i_end; a.i_buf0 = i_buf0;
+  a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
+  a.flag_count = flags; a.flag_list = flags + 2;
+  e = vbhem::launch_fb_exact(a, scratch, exact_stride(a.S, a.SB, a.T), kExactThreads, st);
+  if (e != hipSuccess) return hip_fail(e, "fb_exact_kernel");
+  return VBHEM_OK;
+}
+
+// K1 + K2-K4 over bases [i_begin, i_end) x all clusters.  mode kFbBackward
+// (split kernel only) computes K2 + K3 (LL) alone; flagged pairs still get every
+// output from the exact kernel.
 int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, double *nu1,
            double *xi, double *tnu, double *Ebuf, long long e_ld, int *flags, double *scratch,
-           hipStream_t st) {
+           hipStream_t st, int mode = vbhem::kFbDense) {
   if (i_end <= i_begin) return VBHEM_OK;
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin;
@@ -329,13 +388,14 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
   if (c.split.ok) {
     vbhem::SplitArgs ca = c.split.a;
+    ca.mode = mode;
     ca.E = Ebuf; ca.e_ld = e_ld;
     ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
     ca.LL = LL; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
     ca.flag_count = flags; ca.flag_list = flags + 2;
     const unsigned grid =
         (unsigned)((i_end - i_begin + c.split.ppb - 1) / c.split.ppb) * (unsigned)ca.K;
-    e = vbhem::launch_split(ca, grid, c.split.lds, st);
+    e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? c.split.lds_bwd : c.split.lds, st);
     if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
   } else {
     const int nib = (i_end - i_begin + a.BI - 1) / a.BI;
@@ -456,25 +516,50 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T);
   if (rc != VBHEM_OK) return rc;
+  // gated schedule: split kernel + list statistics tile must apply
+  size_t sl_lds = 0;
+  const bool gated = g_fused_mode == VBHEM_FUSED_GATED && ctx.split.ok &&
+                     vbhem::plan_stats_list(sa, sl_lds);
+  sa.gate_cnt = gated ? w.gate_cnt : nullptr;
+  sa.list = w.list; sa.list_tot = w.list_tot; sa.list_cap = w.group;
   rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st);
   if (rc != VBHEM_OK) return rc;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);
-    rc = run_fb(ctx, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.E, (long long)w.group * SB,
-                w.flags, w.scratch, st);
+    const long long e_ld = (long long)w.group * SB;
+    rc = run_fb(ctx, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.E, e_ld, w.flags, w.scratch,
+                st, gated ? vbhem::kFbBackward : vbhem::kFbDense);
     if (rc != VBHEM_OK) return rc;
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     const int nchunk = std::min(w.nslab, g1 - g0);
     hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
     e = vbhem::launch_resp(sa, nchunk, st);
     if (e != hipSuccess) return hip_fail(e, "resp_kernel");
-    e = vbhem::launch_stats(sa, nchunk, ngroups, slds, st);
-    if (e != hipSuccess) return hip_fail(e, "stats_kernel");
+    if (gated) {
+      e = vbhem::launch_gate_list(sa, nchunk, st);
+      if (e != hipSuccess) return hip_fail(e, "gate_list_kernel");
+      if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
+      rc = run_fb_list(ctx, g0, g1, g0, w.nu1, w.xi, w.tnu, w.E, e_ld, w.list, w.list_tot,
+                       w.group, w.flags, w.scratch, LL_elbo_dev, st);
+      if (rc != VBHEM_OK) return rc;
+      ev0 = g_timing.on ? timing_event(st) : nullptr;
+      e = vbhem::launch_stats_list(sa, nchunk, sl_lds, st);
+      if (e != hipSuccess) return hip_fail(e, "stats_list_kernel");
+    } else {
+      e = vbhem::launch_stats(sa, nchunk, ngroups, slds, st);
+      if (e != hipSuccess) return hip_fail(e, "stats_kernel");
+    }
     if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
   e = vbhem::launch_stats_final(w.slabs, w.nslab, w.slab_len, stats_dev, st);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
   return VBHEM_OK;
+}
+
+int vbhem_set_fused_mode(int mode) {
+  const int prev = g_fused_mode;
+  if (mode == VBHEM_FUSED_GATED || mode == VBHEM_FUSED_DENSE) g_fused_mode = mode;
+  return prev;
 }
 
 int vbhem_timing_enable(int on) {
@@ -513,6 +598,32 @@ int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs
   if (stats_ms) *stats_ms = s;
   if (stats_launches) *stats_launches = ns;
   return rc;
+}
+
+static int drain_events(std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, double *ms_out,
+                        long long *n_out, const char *where) {
+  double t = 0.0;
+  int rc = VBHEM_OK;
+  const long long n = (long long)v.size();
+  for (auto &pr : v) {
+    float ms = 0.f;
+    if (pr.first && pr.second) {
+      hipError_t e = hipEventSynchronize(pr.second);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
+      if (e != hipSuccess) rc = hip_fail(e, where);
+      t += ms;
+    }
+    if (pr.first) (void)hipEventDestroy(pr.first);
+    if (pr.second) (void)hipEventDestroy(pr.second);
+  }
+  v.clear();
+  if (ms_out) *ms_out = t;
+  if (n_out) *n_out = n;
+  return rc;
+}
+
+int vbhem_timing_read_gated(double *fwd_ms, long long *fwd_launches) {
+  return drain_events(g_timing.gf, fwd_ms, fwd_launches, "vbhem_timing_read_gated");
 }
 
 int vbhem_timing_read_emission(double *em_ms, long long *em_launches) {

@@ -170,70 +170,33 @@ __device__ __forceinline__ void load_row(double (&dst)[SH], const double *row, i
 
 }  // namespace
 
-template <int S, int LPC>
-__global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
+// One workgroup = NWB wavefronts = PPB pairs of ONE cluster.  Dense / backward
+// modes: block (tile, j) = bases [i_begin + tile*PPB, +PPB) x cluster blockIdx % K.
+// List mode: the gated pairs of every cluster cut into PPB-pair work items,
+// contiguous item ranges per block (cluster constants restaged when j changes).
+template <int S, int LPC, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kFbBackward ? 3 : 2)))
+void fb_split_kernel(const SplitArgs p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using LY = SplitLayout<S, LPC>;
   constexpr int SH = LY::SH;
   constexpr int LPP = S * LPC;  // lanes per pair
   constexpr bool kWaveLocal = (LPP & (LPP - 1)) == 0;  // pairs never straddle a wave
+  constexpr bool kFwd = MODE != kFbBackward;
   const int tid = threadIdx.x;
   const int NT = p.nwb * 64;
   const int PPB = NT / LPP;
   const int SB = p.SB, T = p.T, K = p.K;
-  const int j = blockIdx.x % K;
-  const int i0 = p.i_begin + (blockIdx.x / K) * PPB;
-  const int q = tid / LPP;
-  const int w = tid - q * LPP;
-  const int b = w / LPC;
-  const int h = w - b * LPC;
-  const bool valid = q < PPB;
-  const int i = i0 + q;
-  const bool active = valid && i < p.i_end;
-  const int ic = active ? i : p.i_begin;
-  const bool bvalid = b < SB;
-  const int bc = bvalid ? b : SB - 1;
-  __builtin_assume(h >= 0 && h < LPC);
-  const int r0 = h * SH;  // first row owned by this lane
 
   double *At = lds;              // [S][S]
   double *AtT = At + S * S;      // [S][S]
   double *amax = AtT + S * S;    // [S]
   double *lpi = amax + S;        // [S]
-  double *X = lds + LY::OFF_X + (valid ? q : 0) * LY::XP;   // slab [col][XCS]
-  double *Y = lds + p.off_Y + (valid ? q : 0) * S;
   double *R = lds + p.off_R;     // lattice [(T-2)][SH][NT]
   int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
 
-  // ---------------- per-pair inputs: E (K1, precomputed), Ab row/column, prior -------------
-  const size_t lp = (size_t)(ic - p.i_buf0) * K + j;
-  double E[SH];
-  {
-    const double *Ep = p.E + (size_t)j * S * p.e_ld + (size_t)(ic - p.i_buf0) * SB + bc;
-#pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const bool rv = r0 + k < S;
-      const double v = Ep[(size_t)(rv ? r0 + k : S - 1) * p.e_ld];
-      E[k] = rv ? v : -INFINITY;
-    }
-  }
-  double arow[S], acol[S];
-  {
-    const double *Ai = p.A + (size_t)ic * SB * SB;
-#pragma unroll
-    for (int be = 0; be < S; ++be) {
-      const int bb = be < SB ? be : SB - 1;
-      const double r1 = Ai[bc * SB + bb], c1 = Ai[bb * SB + bc];
-      const bool ok = bvalid && be < SB;
-      arow[be] = ok ? r1 : 0.0;
-      acol[be] = ok ? c1 : 0.0;
-    }
-  }
-  const double pb0 = p.prior[(size_t)ic * SB + bc];
-  const double pb = bvalid ? pb0 : 0.0;
-
   // ---------------- cluster constants: A' = exp(logA - rowmax), rowmax, logPi --------------
-  {
+  auto stage_cluster = [&](int j) {
     const double *la = p.logA + (size_t)j * S * S;
     if (tid < S) {
       double mx = la[tid * S];
@@ -241,304 +204,439 @@ __global__ __launch_bounds__(256) void fb_split_kernel(const SplitArgs p) {
       amax[tid] = mx;
       lpi[tid] = p.logPi[(size_t)j * S + tid];
     }
-    for (int x = tid; x < PPB; x += NT) F[x] = 0;
-  }
-  __syncthreads();
-  for (int x = tid; x < S * S; x += NT) {
-    const int r = x / S, s2 = x - r * S;
-    const double a = exp_nonpos(p.logA[(size_t)j * S * S + x] - amax[r]);
-    At[x] = a;
-    AtT[s2 * S + r] = a;
-  }
-  __syncthreads();
-
-  // ---------------- K2: backward recursion -------------------------------------------------
-  // A'(rows of every owner block, my columns r0..r0+SH): register-resident for both sweeps
-  // (occupancy is bounded by LDS, not registers)
-  constexpr bool kAtReg = LPC * SH * SH <= 48;  // <= 96 VGPRs
-  double atr[kAtReg ? LPC * SH : 1][SH];
-  if constexpr (kAtReg) {
-#pragma unroll
-    for (int r = 0; r < LPC * SH; ++r) {
-      const int ra = rel_row<SH>(r, h);
-      load_row<S, SH, LPC>(atr[r], At + (ra < S ? ra : S - 1) * S, r0);
-    }
-  }
-  double am[SH];  // amax of my rows (LDS -> registers once)
-#pragma unroll
-  for (int k = 0; k < SH; ++k) am[k] = amax[r0 + k < S ? r0 + k : S - 1];
-  double L[SH];
-#pragma unroll
-  for (int k = 0; k < SH; ++k) L[k] = 0.0;
-  bool bad = false;
-  for (int t = T - 1; t >= 1; --t) {
-    double G[SH], M = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < SH; ++k) M = fmax(M, E[k] + L[k]);
-    M = allmax<LPC>(M);
-    {
-      double ex[SH];
-#pragma unroll
-      for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
-      exp_nonpos_n<SH>(G, ex);
-    }
-    // partial Z for every owner's rows, then reduce-scatter
-    double Pz[LPC * SH];
-#pragma unroll
-    for (int r = 0; r < LPC * SH; ++r) {
-      double ar[SH];
-      if constexpr (kAtReg) {
-#pragma unroll
-        for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
-      } else {
-        const int ra = rel_row<SH>(r, h);
-        load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
-      }
-      double z = 0.0;
-#pragma unroll
-      for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
-      Pz[r] = z;
-    }
-    double Z[SH];
-    reduce_scatter<LPC, SH>(Pz, Z);
-    double sv[SH], zz[SH], lz[SH];
-#pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const bool rv = r0 + k < S;
-      bad |= bvalid && rv && !(Z[k] >= kZMinS);
-      zz[k] = rv ? Z[k] : 1.0;
-    }
-    log_pos_n<SH>(lz, zz);
-#pragma unroll
-    for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];
-    if (t <= T - 2) {
-      double *slot = R + (size_t)(t - 1) * SH * NT + tid;
-#pragma unroll
-      for (int k = 0; k < SH; ++k) slot[k * NT] = G[k];
-    }
-    if (valid) lds_st<SH>(X + b * LY::XCS + r0, sv);
-    pair_sync<kWaveLocal>();
-#pragma unroll
-    for (int k = 0; k < SH; ++k) L[k] = 0.0;
-#pragma unroll
-    for (int be = 0; be < S; ++be) {
-      double xs[SH];
-      lds_ld<SH>(xs, X + be * LY::XCS + r0);
-#pragma unroll
-      for (int k = 0; k < SH; ++k) L[k] = fma(arow[be], xs[k], L[k]);
-    }
-    pair_sync<kWaveLocal>();
-  }
-
-  // ---------------- K3: termination ----------------------------------------------------------
-  double nu[SH];
-  {
-    double v1[SH], M1 = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const int r = r0 + k < S ? r0 + k : S - 1;
-      v1[k] = lpi[r] + E[k] + L[k];
-      M1 = fmax(M1, v1[k]);
-    }
-    M1 = allmax<LPC>(M1);
-    double ex[SH], ev[SH];
-#pragma unroll
-    for (int k = 0; k < SH; ++k) ex[k] = v1[k] - M1;
-    exp_nonpos_n<SH>(ev, ex);
-    double zs = 0.0;
-#pragma unroll
-    for (int k = 0; k < SH; ++k) zs += ev[k];
-    zs = allsum<LPC>(zs);
-    const double s1 = M1 + log_pos(zs);
-#pragma unroll
-    for (int k = 0; k < SH; ++k) ex[k] = v1[k] - s1;
-    exp_nonpos_n<SH>(ev, ex);
-#pragma unroll
-    for (int k = 0; k < SH; ++k) nu[k] = pb * ev[k];
-    if (valid) {
-      if (h == 0) Y[b] = pb * s1;
-      lds_st<SH>(X + b * LY::XCS + r0, nu);
-    }
-  }
-  pair_sync<kWaveLocal>();
-  const size_t pair = (size_t)i * K + j;
-  if (active) {
-    if (w == 0) {
-      double ll = 0.0;
-      for (int be = 0; be < SB; ++be) ll += Y[be];
-      p.LL[pair] = ll;
-    }
-    if (w < S) {
-      double n1 = 0.0;
-#pragma unroll
-      for (int be = 0; be < S; ++be) n1 += X[be * LY::XCS + w];
-      p.nu1[lp * S + w] = n1;
-    }
-  }
-
-  // ---------------- K4: forward recursion ----------------------------------------------------
-  double tn[SH], H[SH][LPC * SH];
-#pragma unroll
-  for (int k = 0; k < SH; ++k) {
-    tn[k] = nu[k];
-#pragma unroll
-    for (int s = 0; s < LPC * SH; ++s) H[k][s] = 0.0;
-  }
-  for (int t = 1; t < T; ++t) {
-    double G[SH];
-    if (t == T - 1) {
-      double M = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < SH; ++k) M = fmax(M, E[k]);
-      M = allmax<LPC>(M);
-      double ex[SH];
-#pragma unroll
-      for (int k = 0; k < SH; ++k) ex[k] = E[k] - M;
-      exp_nonpos_n<SH>(G, ex);
-    } else {
-      const double *slot = R + (size_t)(t - 1) * SH * NT + tid;
-#pragma unroll
-      for (int k = 0; k < SH; ++k) G[k] = slot[k * NT];
-    }
-    pair_sync<kWaveLocal>();  // X holds nu
-    double f[SH];
-#pragma unroll
-    for (int k = 0; k < SH; ++k) f[k] = 0.0;
-#pragma unroll
-    for (int be = 0; be < S; ++be) {
-      double xs[SH];
-      lds_ld<SH>(xs, X + be * LY::XCS + r0);
-#pragma unroll
-      for (int k = 0; k < SH; ++k) f[k] = fma(xs[k], acol[be], f[k]);
-    }
-    // Z recomputed exactly as in the backward pass
-    double Pz[LPC * SH];
-#pragma unroll
-    for (int r = 0; r < LPC * SH; ++r) {
-      double ar[SH];
-      if constexpr (kAtReg) {
-#pragma unroll
-        for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
-      } else {
-        const int ra = rel_row<SH>(r, h);
-        load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
-      }
-      double z = 0.0;
-#pragma unroll
-      for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
-      Pz[r] = z;
-    }
-    double Z[SH], g[SH];
-    reduce_scatter<LPC, SH>(Pz, Z);
-    {
-      double zr[SH], rz[SH];
-#pragma unroll
-      for (int k = 0; k < SH; ++k) zr[k] = (r0 + k < S) ? Z[k] : 1.0;
-      rcp_pos_n<SH>(rz, zr);
-#pragma unroll
-      for (int k = 0; k < SH; ++k) g[k] = (r0 + k < S) ? f[k] * rz[k] : 0.0;
-    }
-    // nu'(s) = G(s) * sum_r A'(r, s) g(r): partial over my rows r for every s
-    double Pn[LPC * SH];
-#pragma unroll
-    for (int s = 0; s < LPC * SH; ++s) {
-      const int sa = rel_row<SH>(s, h);
-      const int ss = sa < S ? sa : S - 1;
-      double ac[SH];
-      load_row<S, SH, LPC>(ac, AtT + ss * S, r0);
-      double a = 0.0;
-#pragma unroll
-      for (int k = 0; k < SH; ++k) a = fma(ac[k], g[k], a);
-      Pn[s] = a;
-    }
-    double Q[SH];
-    reduce_scatter<LPC, SH>(Pn, Q);
-#pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      nu[k] = G[k] * Q[k];
-      tn[k] += nu[k];
-    }
-    double Ga[LPC * SH];
-    all_gather<LPC, SH>(G, Ga);
-#pragma unroll
-    for (int k = 0; k < SH; ++k)
-#pragma unroll
-      for (int s = 0; s < LPC * SH; ++s) H[k][s] = fma(g[k], Ga[s], H[k][s]);
-    pair_sync<kWaveLocal>();  // all reads of X done
-    if (valid) lds_st<SH>(X + b * LY::XCS + r0, nu);
-  }
-
-  // ---------------- outputs -------------------------------------------------------------------
-  if (active && bvalid) {
-#pragma unroll
-    for (int k = 0; k < SH; ++k)
-      if (r0 + k < S) p.tnu[(lp * S + r0 + k) * SB + b] = tn[k];
-  }
-  // sum_xi(r, s) = A'(r, s) * sum_b H_b(r, s).
-  //  S > 8 : every lane parks its H block in the (now dead) lattice region, one
-  //          barrier, then each lane of the pair reduces S*S/LPP outputs;
-  //  S <= 8: one wave-local round per row r through the pair's slab.
-  if constexpr (S > 8) {
-    constexpr int HW = LPC * SH;                      // values per H row (owner-relative)
-    __syncthreads();                                  // all lattice reads of the block done
-    double *Hq = R + (size_t)(valid ? q : 0) * S * S * HW;   // [b][r][HW]
-    if (valid && b < S) {
-#pragma unroll
-      for (int k = 0; k < SH; ++k)
-        if (r0 + k < S) lds_st<HW>(Hq + ((size_t)b * S + r0 + k) * HW, H[k]);
+    __syncthreads();
+    for (int x = tid; x < S * S; x += NT) {
+      const int r = x / S, s2 = x - r * S;
+      const double a = exp_nonpos(la[x] - amax[r]);
+      At[x] = a;
+      AtT[s2 * S + r] = a;
     }
     __syncthreads();
+  };
+
+  // ---------------- one pair per LPP lanes: (ic, j) --------------------------------------------
+  // pair n0 + q of the item: base i = lst ? lst[n0 + q] : n0 + q, active while n0 + q < lim
+  auto run_pair = [&](int j, int n0, int lim, const int *lst) {
+    // lane geometry recomputed from an opaque copy of the thread id: in the list
+    // mode's item loop this keeps LICM from hoisting every lane-invariant address
+    // out of the loop (which costs ~90 VGPRs of live ranges)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    // the arguments re-read through a laundered kernarg-segment pointer, for the same
+    // reason (SGPR live ranges); p is the kernel's only argument, at offset 0
+    const SplitArgs *pap = (const SplitArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(pap));
+    const SplitArgs &pa = *pap;
+    const int q = tid / LPP;
+    const int w = tid - q * LPP;
+    const int b = w / LPC;
+    const int h = w - b * LPC;
+    const bool valid = q < PPB;
+    const bool bvalid = b < SB;
+    const int bc = bvalid ? b : SB - 1;
+    __builtin_assume(h >= 0 && h < LPC);
+    const int r0 = h * SH;  // first row owned by this lane
+    double *X = lds + LY::OFF_X + (valid ? q : 0) * LY::XP;   // slab [col][XCS]
+    double *Y = lds + pa.off_Y + (valid ? q : 0) * S;
+    const bool active = valid && n0 + q < lim;
+    const int i = active ? (lst ? lst[n0 + q] : n0 + q) : pa.i_begin;
+    const int ic = i;
+    const size_t lp = (size_t)(ic - pa.i_buf0) * K + j;
+    if (valid && w == 0) F[q] = 0;  // read back only after this pair's later syncs
+    // per-pair inputs: E (K1, precomputed), Ab row/column, prior
+    double E[SH];
+    {
+      const double *Ep = pa.E + (size_t)j * S * pa.e_ld + (size_t)(ic - pa.i_buf0) * SB + bc;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        const bool rv = r0 + k < S;
+        const double v = Ep[(size_t)(rv ? r0 + k : S - 1) * pa.e_ld];
+        E[k] = rv ? v : -INFINITY;
+      }
+    }
+    double arow[S], acol[kFwd ? S : 1];
+    {
+      const double *Ai = pa.A + (size_t)ic * SB * SB;
+#pragma unroll
+      for (int be = 0; be < S; ++be) {
+        const int bb = be < SB ? be : SB - 1;
+        const bool ok = bvalid && be < SB;
+        const double r1 = Ai[bc * SB + bb];
+        arow[be] = ok ? r1 : 0.0;
+        if constexpr (kFwd) {
+          const double c1 = Ai[bb * SB + bc];
+          acol[be] = ok ? c1 : 0.0;
+        }
+      }
+    }
+    const double pb0 = pa.prior[(size_t)ic * SB + bc];
+    const double pb = bvalid ? pb0 : 0.0;
+
+    // ---------------- K2: backward recursion -----------------------------------------------
+    // A'(rows of every owner block, my columns r0..r0+SH): register-resident for both sweeps
+    // (occupancy is bounded by LDS, not registers)
+    constexpr bool kAtReg = LPC * SH * SH <= 48;  // <= 96 VGPRs
+    double atr[kAtReg ? LPC * SH : 1][SH];
+    if constexpr (kAtReg) {
+#pragma unroll
+      for (int r = 0; r < LPC * SH; ++r) {
+        const int ra = rel_row<SH>(r, h);
+        load_row<S, SH, LPC>(atr[r], At + (ra < S ? ra : S - 1) * S, r0);
+      }
+    }
+    double am[SH];  // amax of my rows (LDS -> registers once)
+#pragma unroll
+    for (int k = 0; k < SH; ++k) am[k] = amax[r0 + k < S ? r0 + k : S - 1];
+    double L[SH];
+#pragma unroll
+    for (int k = 0; k < SH; ++k) L[k] = 0.0;
+    bool bad = false;
+    for (int t = T - 1; t >= 1; --t) {
+      double G[SH], M = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) M = fmax(M, E[k] + L[k]);
+      M = allmax<LPC>(M);
+      {
+        double ex[SH];
+#pragma unroll
+        for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
+        exp_nonpos_n<SH>(G, ex);
+      }
+      // partial Z for every owner's rows, then reduce-scatter
+      double Pz[LPC * SH];
+#pragma unroll
+      for (int r = 0; r < LPC * SH; ++r) {
+        double ar[SH];
+        if constexpr (kAtReg) {
+#pragma unroll
+          for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
+        } else {
+          const int ra = rel_row<SH>(r, h);
+          load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
+        }
+        double z = 0.0;
+#pragma unroll
+        for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
+        Pz[r] = z;
+      }
+      double Z[SH];
+      reduce_scatter<LPC, SH>(Pz, Z);
+      double sv[SH], zz[SH], lz[SH];
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        const bool rv = r0 + k < S;
+        bad |= bvalid && rv && !(Z[k] >= kZMinS);
+        zz[k] = rv ? Z[k] : 1.0;
+      }
+      log_pos_n<SH>(lz, zz);
+#pragma unroll
+      for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];
+      if (kFwd && t <= T - 2) {
+        double *slot = R + (size_t)(t - 1) * SH * NT + tid;
+#pragma unroll
+        for (int k = 0; k < SH; ++k) slot[k * NT] = G[k];
+      }
+      if (valid) lds_st<SH>(X + b * LY::XCS + r0, sv);
+      pair_sync<kWaveLocal>();
+#pragma unroll
+      for (int k = 0; k < SH; ++k) L[k] = 0.0;
+#pragma unroll
+      for (int be = 0; be < S; ++be) {
+        double xs[SH];
+        lds_ld<SH>(xs, X + be * LY::XCS + r0);
+#pragma unroll
+        for (int k = 0; k < SH; ++k) L[k] = fma(arow[be], xs[k], L[k]);
+      }
+      pair_sync<kWaveLocal>();
+    }
+
+    // ---------------- K3: termination --------------------------------------------------------
+    double nu[SH];
+    {
+      double v1[SH], M1 = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        const int r = r0 + k < S ? r0 + k : S - 1;
+        v1[k] = lpi[r] + E[k] + L[k];
+        M1 = fmax(M1, v1[k]);
+      }
+      M1 = allmax<LPC>(M1);
+      double ex[SH], ev[SH];
+#pragma unroll
+      for (int k = 0; k < SH; ++k) ex[k] = v1[k] - M1;
+      exp_nonpos_n<SH>(ev, ex);
+      double zs = 0.0;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) zs += ev[k];
+      zs = allsum<LPC>(zs);
+      const double s1 = M1 + log_pos(zs);
+      if constexpr (kFwd) {
+#pragma unroll
+        for (int k = 0; k < SH; ++k) ex[k] = v1[k] - s1;
+        exp_nonpos_n<SH>(ev, ex);
+#pragma unroll
+        for (int k = 0; k < SH; ++k) nu[k] = pb * ev[k];
+      }
+      if (valid) {
+        if (MODE != kFbList && h == 0) Y[b] = pb * s1;
+        if constexpr (kFwd) lds_st<SH>(X + b * LY::XCS + r0, nu);
+      }
+    }
+    pair_sync<kWaveLocal>();
+    const size_t pair = (size_t)ic * K + j;
     if (active) {
-      for (int o = w; o < S * S; o += LPP) {
-        const int r = o / S, s2 = o - r * S;
-        const int sr = rel_row<SH>(s2, r / SH);       // s2 in row r's owner-relative order
-        double acc = 0.0;
+      if (MODE != kFbList && w == 0) {
+        double ll = 0.0;
+        for (int be = 0; be < SB; ++be) ll += Y[be];
+        pa.LL[pair] = ll;
+      }
+      if (kFwd && w < S) {
+        double n1 = 0.0;
 #pragma unroll
-        for (int be = 0; be < S; ++be) acc += Hq[((size_t)be * S + r) * HW + sr];
-        p.xi[lp * S * S + o] = At[o] * acc;
+        for (int be = 0; be < S; ++be) n1 += X[be * LY::XCS + w];
+        pa.nu1[lp * S + w] = n1;
       }
     }
+
+    if constexpr (kFwd) {
+      // ---------------- K4: forward recursion ------------------------------------------------
+      double tn[SH], H[SH][LPC * SH];
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        tn[k] = nu[k];
+#pragma unroll
+        for (int s = 0; s < LPC * SH; ++s) H[k][s] = 0.0;
+      }
+      for (int t = 1; t < T; ++t) {
+        double G[SH];
+        if (t == T - 1) {
+          double M = -INFINITY;
+#pragma unroll
+          for (int k = 0; k < SH; ++k) M = fmax(M, E[k]);
+          M = allmax<LPC>(M);
+          double ex[SH];
+#pragma unroll
+          for (int k = 0; k < SH; ++k) ex[k] = E[k] - M;
+          exp_nonpos_n<SH>(G, ex);
+        } else {
+          const double *slot = R + (size_t)(t - 1) * SH * NT + tid;
+#pragma unroll
+          for (int k = 0; k < SH; ++k) G[k] = slot[k * NT];
+        }
+        pair_sync<kWaveLocal>();  // X holds nu
+        double f[SH];
+#pragma unroll
+        for (int k = 0; k < SH; ++k) f[k] = 0.0;
+#pragma unroll
+        for (int be = 0; be < S; ++be) {
+          double xs[SH];
+          lds_ld<SH>(xs, X + be * LY::XCS + r0);
+#pragma unroll
+          for (int k = 0; k < SH; ++k) f[k] = fma(xs[k], acol[be], f[k]);
+        }
+        // Z recomputed exactly as in the backward pass
+        double Pz[LPC * SH];
+#pragma unroll
+        for (int r = 0; r < LPC * SH; ++r) {
+          double ar[SH];
+          if constexpr (kAtReg) {
+#pragma unroll
+            for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
+          } else {
+            const int ra = rel_row<SH>(r, h);
+            load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
+          }
+          double z = 0.0;
+#pragma unroll
+          for (int k = 0; k < SH; ++k) z = fma(ar[k], G[k], z);
+          Pz[r] = z;
+        }
+        double Z[SH], g[SH];
+        reduce_scatter<LPC, SH>(Pz, Z);
+        {
+          double zr[SH], rz[SH];
+#pragma unroll
+          for (int k = 0; k < SH; ++k) zr[k] = (r0 + k < S) ? Z[k] : 1.0;
+          rcp_pos_n<SH>(rz, zr);
+#pragma unroll
+          for (int k = 0; k < SH; ++k) g[k] = (r0 + k < S) ? f[k] * rz[k] : 0.0;
+        }
+        // nu'(s) = G(s) * sum_r A'(r, s) g(r): partial over my rows r for every s
+        double Pn[LPC * SH];
+#pragma unroll
+        for (int s = 0; s < LPC * SH; ++s) {
+          const int sa = rel_row<SH>(s, h);
+          const int ss = sa < S ? sa : S - 1;
+          double ac[SH];
+          load_row<S, SH, LPC>(ac, AtT + ss * S, r0);
+          double a = 0.0;
+#pragma unroll
+          for (int k = 0; k < SH; ++k) a = fma(ac[k], g[k], a);
+          Pn[s] = a;
+        }
+        double Q[SH];
+        reduce_scatter<LPC, SH>(Pn, Q);
+#pragma unroll
+        for (int k = 0; k < SH; ++k) {
+          nu[k] = G[k] * Q[k];
+          tn[k] += nu[k];
+        }
+        double Ga[LPC * SH];
+        all_gather<LPC, SH>(G, Ga);
+#pragma unroll
+        for (int k = 0; k < SH; ++k)
+#pragma unroll
+          for (int s = 0; s < LPC * SH; ++s) H[k][s] = fma(g[k], Ga[s], H[k][s]);
+        pair_sync<kWaveLocal>();  // all reads of X done
+        if (valid) lds_st<SH>(X + b * LY::XCS + r0, nu);
+      }
+
+      // ---------------- outputs ---------------------------------------------------------------
+      if (active && bvalid) {
+#pragma unroll
+        for (int k = 0; k < SH; ++k)
+          if (r0 + k < S) pa.tnu[(lp * S + r0 + k) * SB + b] = tn[k];
+      }
+      // sum_xi(r, s) = A'(r, s) * sum_b H_b(r, s).
+      //  S > 8 : every lane parks its H block in the (now dead) lattice region, one
+      //          barrier, then each lane of the pair reduces S*S/LPP outputs;
+      //  S <= 8: one wave-local round per row r through the pair's slab.
+      if constexpr (S > 8) {
+        constexpr int HW = LPC * SH;                      // values per H row (owner-relative)
+        __syncthreads();                                  // all lattice reads of the block done
+        double *Hq = R + (size_t)(valid ? q : 0) * S * S * HW;   // [b][r][HW]
+        if (valid && b < S) {
+#pragma unroll
+          for (int k = 0; k < SH; ++k)
+            if (r0 + k < S) lds_st<HW>(Hq + ((size_t)b * S + r0 + k) * HW, H[k]);
+        }
+        __syncthreads();
+        if (active) {
+          for (int o = w; o < S * S; o += LPP) {
+            const int r = o / S, s2 = o - r * S;
+            const int sr = rel_row<SH>(s2, r / SH);       // s2 in row r's owner-relative order
+            double acc = 0.0;
+#pragma unroll
+            for (int be = 0; be < S; ++be) acc += Hq[((size_t)be * S + r) * HW + sr];
+            pa.xi[lp * S * S + o] = At[o] * acc;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+          pair_sync<kWaveLocal>();
+          if (valid && h == r / SH) lds_st<LPC * SH>(X + b * LY::XCS, H[r % SH]);  // owner-relative
+          pair_sync<kWaveLocal>();
+          if (active && w < S) {
+            const int wr = rel_row<SH>(w, r / SH);  // w's position in row r's owner-relative order
+            double acc = 0.0;
+#pragma unroll
+            for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + wr];
+            pa.xi[(lp * S + r) * S + w] = At[r * S + w] * acc;
+          }
+        }
+      }
+    }
+    // fallback flags (one per pair)
+    if (bad && active) F[q] = 1;
+    pair_sync<kWaveLocal>();
+    if (active && w == 0 && F[q]) {
+      const int slot = atomicAdd(pa.flag_count, 1);
+      atomicAdd(pa.flag_count + 1, 1);
+      pa.flag_list[slot] = (int)pair;
+    }
+  };
+
+  if constexpr (MODE != kFbList) {
+    const int j = blockIdx.x % K;
+    stage_cluster(j);
+    run_pair(j, p.i_begin + (int)(blockIdx.x / K) * PPB, p.i_end, nullptr);
   } else {
-#pragma unroll
-    for (int r = 0; r < S; ++r) {
-      pair_sync<kWaveLocal>();
-      if (valid && h == r / SH) lds_st<LPC * SH>(X + b * LY::XCS, H[r % SH]);  // owner-relative
-      pair_sync<kWaveLocal>();
-      if (active && w < S) {
-        const int wr = rel_row<SH>(w, r / SH);  // w's position in row r's owner-relative order
-        double acc = 0.0;
-#pragma unroll
-        for (int be = 0; be < S; ++be) acc += X[be * LY::XCS + wr];
-        p.xi[(lp * S + r) * S + w] = At[r * S + w] * acc;
+    // work items: cluster j owns ceil(list_tot[j] / PPB) consecutive items
+    int *pre = reinterpret_cast<int *>(lds + p.off_L);  // [K + 1]
+    if (tid == 0) {
+      int s = 0;
+      for (int jj = 0; jj < K; ++jj) {
+        pre[jj] = s;
+        s += (p.list_tot[jj] + PPB - 1) / PPB;
       }
+      pre[K] = s;
     }
-  }
-  // fallback flags (one per pair)
-  if (bad && active) F[q] = 1;
-  pair_sync<kWaveLocal>();
-  if (active && w == 0 && F[q]) {
-    const int slot = atomicAdd(p.flag_count, 1);
-    atomicAdd(p.flag_count + 1, 1);
-    p.flag_list[slot] = (int)pair;
+    __syncthreads();
+    const int nitem = __builtin_amdgcn_readfirstlane(pre[K]);  // block-uniform: keep in SGPRs
+    const int per = (nitem + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int w0 = (int)blockIdx.x * per, w1 = min(nitem, w0 + per);
+    int jcur = -1;
+    for (int wi = w0; wi < w1; ++wi) {
+      int jj = jcur < 0 ? 0 : jcur;
+      while (pre[jj + 1] <= wi) ++jj;
+      jj = __builtin_amdgcn_readfirstlane(jj);
+      __syncthreads();  // previous item's LDS traffic (slabs, lattice, parked H) done
+      if (jj != jcur) {
+        stage_cluster(jj);
+        jcur = jj;
+      }
+      const int tot = __builtin_amdgcn_readfirstlane(p.list_tot[jj]);
+      run_pair(jj, (wi - pre[jj]) * PPB, tot, p.list + (size_t)jj * p.list_cap);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-template <int S, int LPC>
-static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
-  auto *fn = &fb_split_kernel<S, LPC>;
+template <int S, int LPC, int MODE>
+static hipError_t launch_split_slm(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  auto *fn = &fb_split_kernel<S, LPC, MODE>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((fb_split_kernel<S, LPC>), dim3(grid), dim3(a.nwb * 64), lds, st, a);
+  hipLaunchKernelGGL((fb_split_kernel<S, LPC, MODE>), dim3(grid), dim3(a.nwb * 64), lds, st, a);
   return hipGetLastError();
+}
+
+template <int S, int LPC>
+static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  switch (a.mode) {
+    case kFbDense: return launch_split_slm<S, LPC, kFbDense>(a, grid, lds, st);
+    case kFbBackward: return launch_split_slm<S, LPC, kFbBackward>(a, grid, lds, st);
+    case kFbList: return launch_split_slm<S, LPC, kFbList>(a, grid, lds, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int S, int LPC, int MODE>
+static int resident_slm(const SplitArgs &a, size_t lds) {
+  int n = 0;
+  if (hipFuncSetAttribute(reinterpret_cast<const void *>(&fb_split_kernel<S, LPC, MODE>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_split_kernel<S, LPC, MODE>, a.nwb * 64,
+                                                   lds) != hipSuccess)
+    return 1;
+  return n;
+}
+
+template <int S>
+static int resident_s(const SplitArgs &a, size_t lds) {
+  constexpr int LPC = SplitLPC<S>::value;
+  switch (a.mode) {
+    case kFbDense: return resident_slm<S, LPC, kFbDense>(a, lds);
+    case kFbBackward: return resident_slm<S, LPC, kFbBackward>(a, lds);
+    default: return resident_slm<S, LPC, kFbList>(a, lds);
+  }
+}
+
+int split_resident_blocks(const SplitArgs &a, size_t lds) {
+  switch (a.S) {
+#define VBHEM_RS(s) case s: return resident_s<s>(a, lds);
+    VBHEM_RS(1) VBHEM_RS(2) VBHEM_RS(3) VBHEM_RS(4) VBHEM_RS(5) VBHEM_RS(6) VBHEM_RS(7)
+    VBHEM_RS(8) VBHEM_RS(9) VBHEM_RS(10) VBHEM_RS(11) VBHEM_RS(12) VBHEM_RS(13) VBHEM_RS(14)
+    VBHEM_RS(15) VBHEM_RS(16)
+#undef VBHEM_RS
+    default: return 1;
+  }
 }
 
 template <int S>
 static hipError_t launch_split_s(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
-  if constexpr (S >= 5 && S <= 8) {
-    if (a.lpc == 4) return launch_split_sl<S, 4>(a, grid, lds, st);
-  }
   if (a.lpc != SplitLPC<S>::value) return hipErrorInvalidValue;
   return launch_split_sl<S, SplitLPC<S>::value>(a, grid, lds, st);
 }

@@ -43,6 +43,12 @@ struct StatsArgs {
   const double *centres, *covars, *LL, *nu1, *xi, *tnu, *tildeN, *logOmega;
   double *Z;  // [group][K] hat_Z * tilde_N (resp_kernel -> stats_kernel)
   double *hatZ, *slabs;
+  // gated-pair lists (sparse path): per-chunk gate counts, per-cluster bases, totals
+  int *gate_cnt;   // [nchunk][K]  (resp_kernel)
+  int *list;       // [K][list_cap] bases i with Z(i, j) > 1e-8, ascending i
+  int *list_tot;   // [K]
+  int list_cap;
+  int PB;          // pairs per batch of stats_list_kernel
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).
@@ -73,20 +79,32 @@ bool plan_emission(EmissionArgs &a, size_t &lds);
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st);
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st);
 
+// fb_split_kernel modes:
+//   kFbDense    every pair of [i_begin, i_end) x K: all outputs (K2-K4)
+//   kFbBackward every pair: K2 + K3 log-likelihood only (no lattice, no forward sweep)
+//   kFbList     the gated pairs list[j * list_cap + n], n < list_tot[j]: K2-K4 outputs
+//               except LL (already written by the backward pass)
+enum FbMode : int { kFbDense = 0, kFbBackward = 1, kFbList = 2 };
+
 struct SplitArgs {
   int SB, d, covmode, K, S, T, nwb, lpc;
+  int mode;  // FbMode
   int i_begin, i_end, i_buf0;
   int off_Y, off_F, off_R;  // LDS layout (doubles), depends on pairs per block
+  int off_L;                // kFbList: [K + 1] ints of work-item prefix (after the lattice)
   const double *prior, *A;
   const double *logA, *logPi;
   const double *E;  // emission_kernel output, [K*S][(i - i_buf0) * SB + b], row stride e_ld
   long long e_ld;
   double *LL, *nu1, *xi, *tnu;
   int *flag_count, *flag_list;
+  const int *list, *list_tot;  // kFbList: gated bases per cluster (gate_list_kernel)
+  int list_cap;
 };
 bool split_supported(int S, int SB, int d);
-int split_lpc(int S);  // default lanes per column (VBHEM_SPLIT_LPC=4 overrides for S = 5..8)
+int split_lpc(int S);  // lanes per column
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
+int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mode
 
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
@@ -95,6 +113,9 @@ hipError_t launch_emit(const EmitArgs &a, hipStream_t st);
 bool plan_stats(StatsArgs &a, size_t &lds, int &ngroups);
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st);
 hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds, hipStream_t st);
+bool plan_stats_list(StatsArgs &a, size_t &lds);
+hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st);
+hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st);
 hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
                               hipStream_t st);
 

@@ -58,6 +58,8 @@ __device__ __forceinline__ void chunk_range(int nb, int i_begin, int chunk, int 
 
 }  // namespace
 
+constexpr double kGateZ = 1e-8;  // vbhem_compute_Statistics.m:35  (Z_Ni(i) > 1e-8)
+
 // ---------------------------------------------------------------------------
 // resp_kernel: one wavefront per base (lanes over clusters j).
 // ---------------------------------------------------------------------------
@@ -84,7 +86,9 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   const int sub = lane / G, gl = lane - sub * G;
   double *accNj = lds;               // [NW*BPW][K]
   double *accLt = accNj + NW * BPW * K;  // [NW][2]
+  int *gcnt = reinterpret_cast<int *>(accLt + 2 * NW);  // [K] gated pairs of this chunk
   for (int x = tid; x < NW * BPW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
+  for (int x = tid; x < K; x += kRespThreads) gcnt[x] = 0;
   __syncthreads();
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
@@ -113,6 +117,7 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
         p.hatZ[(size_t)i * K + j] = hz;
         p.Z[(size_t)(i - p.i_buf0) * K + j] = Z;
         accNj[(wave * BPW + sub) * K + j] += Z;
+        if (Z > kGateZ) atomicAdd(&gcnt[j], 1);
         l1 += Z * ll;
         l7 += hz * log(hz);
       }
@@ -135,6 +140,168 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
     double s = 0.0;
     for (int w = 0; w < NW; ++w) s += accLt[2 * w + tid];
     slab[(size_t)K + (size_t)K * p.S + (size_t)K * p.S * p.S + tid] += s;
+  }
+  if (p.gate_cnt)
+    for (int j = tid; j < K; j += kRespThreads) p.gate_cnt[(size_t)blockIdx.x * K + j] = gcnt[j];
+}
+
+// ---------------------------------------------------------------------------
+// gate_list_kernel: the gated pairs as per-cluster lists of bases, ascending i
+// (list[j][n], n < list_tot[j]).  Block = the resp_kernel chunk: its offset in
+// cluster j's list is the gate count of the chunks before it; inside the chunk
+// the bases are ranked by a block-wide ballot scan, one cluster at a time.
+// Deterministic (no global atomics): the same list every call.
+// ---------------------------------------------------------------------------
+constexpr int kListThreads = 256;
+
+__global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs p) {
+  extern __shared__ int ish[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kListThreads / 64;
+  const int K = p.K, nchunk = gridDim.x, me = blockIdx.x;
+  int *before = ish;          // [K] this chunk's offset in every cluster's list
+  int *total = ish + K;       // [K]
+  int *wcnt = ish + 2 * K;    // [NW]
+  for (int x = tid; x < 2 * K; x += kListThreads) ish[x] = 0;
+  __syncthreads();
+  for (int x = tid; x < nchunk * K; x += kListThreads) {
+    const int c = x / K, j = x - c * K;
+    const int v = p.gate_cnt[x];
+    atomicAdd(&total[j], v);
+    if (c < me) atomicAdd(&before[j], v);
+  }
+  __syncthreads();
+  if (me == 0)
+    for (int j = tid; j < K; j += kListThreads) p.list_tot[j] = total[j];
+  int b0, b1;
+  chunk_range(p.i_end - p.i_begin, p.i_begin, me, nchunk, b0, b1);
+  for (int i0 = b0; i0 < b1; i0 += kListThreads) {
+    const int i = i0 + tid;
+    const bool iv = i < b1;
+    const double *Zi = p.Z + (size_t)((iv ? i : b0) - p.i_buf0) * K;
+    for (int j = 0; j < K; ++j) {
+      const bool g = iv && Zi[j] > kGateZ;
+      const unsigned long long m = __ballot(g);
+      if (lane == 0) wcnt[wave] = __popcll(m);
+      __syncthreads();
+      int off = before[j];
+      for (int w = 0; w < wave; ++w) off += wcnt[w];
+      if (g) p.list[(size_t)j * p.list_cap + off + __popcll(m & ((1ull << lane) - 1ull))] = i;
+      __syncthreads();
+      if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < NW; ++w) t += wcnt[w];
+        before[j] += t;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// stats_list_kernel<PER>: the gated sums over the gated-pair lists only.
+// Block (c, j) = part c of cluster j's list (fixed split, ascending bases) ->
+// slab c's cluster-j entries; PB pairs per batch staged in LDS as
+//   [ Z sum_t_nu (S x SB) | Z sum_nu_1 (S) | Z sum_xi (S x S) | u (SB x NU) ],
+// each thread owning PER outputs of  N1 (S) | M (S x S) | U (S x NU).
+// ---------------------------------------------------------------------------
+constexpr int kSlThreads = 256;
+
+template <int PER>
+__global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x;
+  const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU, PB = p.PB;
+  const int j = blockIdx.y, c = blockIdx.x, nch = gridDim.x;
+  const bool full = p.covmode == kCovFull;
+  const int dd = full ? d * d : d;
+  const int OT = S * SB, OM = OT + S, OU = OM + S * S;  // record: tnu | nu1 | xi | u
+  const int RS = (OU + SB * NU + 1) / 2 * 2;  // record stride (doubles), = sl_record()
+  const int NO = S + S * S + S * NU;
+  double *rec = lds;                                            // [PB][RS]
+  int *tab = reinterpret_cast<int *>(rec + (size_t)PB * RS);    // [NU] packed (a, b)
+  for (int cc = tid; cc < NU; cc += kSlThreads) {
+    int a = -1, b = -1;
+    if (cc >= 1 && cc <= d) {
+      a = cc - 1;
+    } else if (cc > d) {
+      if (full) {
+        int k = cc - 1 - d;
+        a = 0;
+        while (k >= d - a) { k -= d - a; ++a; }
+        b = a + k;
+      } else {
+        a = b = cc - 1 - d;
+      }
+    }
+    tab[cc] = (a + 1) | ((b + 1) << 16);
+  }
+  const int tot = p.list_tot[j];
+  const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
+  const int *lst = p.list + (size_t)j * p.list_cap;
+  const float invNU = 1.0f / (float)NU;
+  double *slab = p.slabs + (size_t)c * p.slab_len;
+  for (int o0 = 0; o0 < NO; o0 += PER * kSlThreads) {
+    double acc[PER];
+#pragma unroll
+    for (int e = 0; e < PER; ++e) acc[e] = 0.0;
+    for (int n = n0; n < n1; n += PB) {
+      const int np = min(PB, n1 - n);
+      __syncthreads();  // tab ready / previous batch consumed
+      for (int pq = 0; pq < np; ++pq) {
+        const int i = lst[n + pq];
+        const size_t lp = (size_t)(i - p.i_buf0) * K + j;
+        const double z = p.Z[lp];
+        double *r = rec + (size_t)pq * RS;
+        for (int e = tid; e < OU; e += kSlThreads) {
+          double v;
+          if (e < OT) v = p.tnu[lp * OT + e];
+          else if (e < OM) v = p.nu1[lp * S + (e - OT)];
+          else v = p.xi[lp * S * S + (e - OM)];
+          r[e] = z * v;
+        }
+        const double *mu0 = p.centres + (size_t)i * SB * d;
+        const double *C0 = p.covars + (size_t)i * SB * dd;
+        for (int e = tid; e < SB * NU; e += kSlThreads) {
+          const int bb = qdiv(e, invNU), cc = e - bb * NU;
+          const int t = tab[cc], a = (t & 0xffff) - 1, b2 = (t >> 16) - 1;
+          const double *mu = mu0 + (size_t)bb * d;
+          double u;
+          if (a < 0) u = 1.0;
+          else if (b2 < 0) u = mu[a];
+          else u = (full ? C0[(size_t)bb * dd + a * d + b2] : C0[(size_t)bb * dd + a]) + mu[a] * mu[b2];
+          r[OU + e] = u;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int o = o0 + tid + e * kSlThreads;
+        if (o < S) {
+          for (int pq = 0; pq < np; ++pq) acc[e] += rec[(size_t)pq * RS + OT + o];
+        } else if (o < S + S * S) {
+          for (int pq = 0; pq < np; ++pq) acc[e] += rec[(size_t)pq * RS + OM + (o - S)];
+        } else if (o < NO) {
+          const int oo = o - S - S * S;
+          const int sg = qdiv(oo, invNU), cc = oo - sg * NU;
+          for (int pq = 0; pq < np; ++pq) {
+            const double *r = rec + (size_t)pq * RS;
+            for (int bb = 0; bb < SB; ++bb) acc[e] = fma(r[sg * SB + bb], r[OU + bb * NU + cc], acc[e]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int o = o0 + tid + e * kSlThreads;
+      if (o < S) {
+        slab[K + (size_t)j * S + o] += acc[e];
+      } else if (o < S + S * S) {
+        slab[K + (size_t)K * S + (size_t)j * S * S + (o - S)] += acc[e];
+      } else if (o < NO) {
+        const int oo = o - S - S * S;
+        slab[K + (size_t)K * S + (size_t)K * S * S + 2 + (size_t)j * S * NU + oo] += acc[e];
+      }
+    }
   }
 }
 
@@ -236,7 +403,7 @@ __global__ __launch_bounds__(kStatsThreads) void stats_kernel(const StatsArgs p)
   for (int ib = b0; ib < b1; ib += NBB) {
     const int nq = min(NBB, b1 - ib);
     // -- commit: gated Z and the raw base data of this batch -> LDS ------------------
-    if (tid < NBB * JGc) gzs[tid] = (pz > 1e-8) ? pz : 0.0;
+    if (tid < NBB * JGc) gzs[tid] = (pz > kGateZ) ? pz : 0.0;
 #pragma unroll
     for (int e = 0; e < kStatsMaxR; ++e) {
       const int x = tid + e * kStatsThreads;
@@ -358,7 +525,7 @@ __global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
       for (int e = 0; e < PER; ++e) {
         const int x = tid + e * kNmThreads;
         const double zz = z[u][e];
-        z[u][e] = (iv && x < NO && zz > 1e-8) ? zz : 0.0;
+        z[u][e] = (iv && x < NO && zz > kGateZ) ? zz : 0.0;
       }
     }
 #pragma unroll
@@ -459,7 +626,8 @@ static hipError_t launch_stats_t(const StatsArgs &a, int nchunk, int ngroups, si
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
   int G = 1;
   while (G < a.K && G < 64) G <<= 1;
-  const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2)) * sizeof(double);
+  const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2)) * sizeof(double) +
+                     (size_t)a.K * sizeof(int);
   hipLaunchKernelGGL(resp_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
   return hipGetLastError();
 }
@@ -471,6 +639,43 @@ hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
   if (tpw <= 4) return launch_stats_t<4>(a, nchunk, ngroups, lds, st);
   if (tpw <= 8) return launch_stats_t<8>(a, nchunk, ngroups, lds, st);
   return launch_stats_t<16>(a, nchunk, ngroups, lds, st);
+}
+
+hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st) {
+  const size_t lds = ((size_t)2 * a.K + kListThreads / 64) * sizeof(int);
+  hipLaunchKernelGGL(gate_list_kernel, dim3(nchunk), dim3(kListThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+namespace {
+constexpr size_t kSlLdsBudget = 48 * 1024;
+int sl_record(const StatsArgs &a) {
+  const int OU = a.S * a.SB + a.S + a.S * a.S;
+  return (OU + a.SB * a.NU + 1) / 2 * 2;
+}
+}  // namespace
+
+bool plan_stats_list(StatsArgs &a, size_t &lds) {
+  const size_t rs = (size_t)sl_record(a) * sizeof(double);
+  const size_t tab = (size_t)a.NU * sizeof(int);
+  if (rs + tab > kSlLdsBudget) return false;
+  a.PB = (int)std::min<size_t>(16, (kSlLdsBudget - tab) / rs);
+  lds = (size_t)a.PB * rs + tab;
+  return a.PB >= 1;
+}
+
+hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st) {
+  const int NO = a.S + a.S * a.S + a.S * a.NU;
+  const dim3 grid(nchunk, a.K);
+  if (NO <= 4 * kSlThreads) {
+    hipLaunchKernelGGL((stats_list_kernel<4>), grid, dim3(kSlThreads), lds, st, a);
+  } else {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_list_kernel<8>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((stats_list_kernel<8>), grid, dim3(kSlThreads), lds, st, a);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,

@@ -111,6 +111,18 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
                       double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
                       void *workspace_dev, size_t workspace_bytes, void *stream);
 
+/* Fused E-step schedule (process-wide; default VBHEM_FUSED_GATED, or set the
+ * environment variable VBHEM_FUSED_DENSE=1).  Both give the same outputs:
+ *   VBHEM_FUSED_GATED  backward sweep + log-likelihood for every pair, then the
+ *                      forward sweep and statistics only for the pairs the gate
+ *                      Z > 1e-8 of vbhem_compute_Statistics.m:35 keeps (the
+ *                      reference computes the others and discards them);
+ *   VBHEM_FUSED_DENSE  both sweeps for every pair (mex.c order of work).
+ * Returns the previous mode. */
+#define VBHEM_FUSED_GATED 0
+#define VBHEM_FUSED_DENSE 1
+int vbhem_set_fused_mode(int mode);
+
 /* Number of pairs the last call on this thread had to recompute with the
  * exact (reference-order, Theta-storing) fallback because the factorised
  * log-sum-exp fell below its safe range.  Synchronises `stream`. */
@@ -127,6 +139,9 @@ int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs
 /* Summed time and launch count of the K1 emission GEMM (emission_kernel) since
  * the last call; same event mechanism as vbhem_timing_read. */
 int vbhem_timing_read_emission(double *em_ms, long long *em_launches);
+/* Summed time and launch count of the gated forward pass (fb_split_kernel in
+ * list mode; VBHEM_FUSED_GATED only) since the last call. */
+int vbhem_timing_read_gated(double *fwd_ms, long long *fwd_launches);
 
 const char *vbhem_last_error(void);
 const char *vbhem_version(void);

@@ -51,13 +51,27 @@ def test_pairs_match_oracle(vb, vo, shape):
         assert e < RTOL_PAIRS, (name, k, e)
 
 
+@pytest.fixture(params=["gated", "dense"])
+def fused_mode(request):
+    """Run a fused test under both schedules (VBHEM_FUSED_GATED / _DENSE)."""
+    from vbhem_amd import _capi
+    prev = _capi.set_fused_mode(_capi.FUSED_GATED if request.param == "gated" else _capi.FUSED_DENSE)
+    yield request.param
+    _capi.set_fused_mode(prev)
+
+
 @pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
-def test_fused_matches_oracle(vb, vo, shape):
+@pytest.mark.parametrize("tscale", [100.0, 1e-9], ids=["Nv100", "allgated"])
+def test_fused_matches_oracle(vb, vo, shape, fused_mode, tscale):
+    """tscale = Nv: 100 (the configs' virtual samples: Z mostly one-hot, the gate
+    drops most pairs) and 1e-9 (every Z < 1e-8: no pair passes the gate)."""
     name, N, K, S, Sb, d, cov, T, ragged = shape
+    if tscale != 100.0 and fused_mode == "dense":
+        pytest.skip("gate-edge case targets the gated schedule")
     cs = make_case(N, K, S, Sb, d, cov, seed=seed_of(name) + 1, ragged=ragged, tau=T)
     base, consts = cs["base"], cs["consts"]
     pairs = vo.c_estep_pairs(base, consts, T, nthreads=4)
-    tN = 100.0 * N * base["omega"]
+    tN = tscale * N * base["omega"]
     logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
     st = vo.c_statistics(Z, pairs, cov)
     eng = engine(vb, base, consts, T)
@@ -102,7 +116,7 @@ def test_exact_fallback_pairs(vb, vo, cov):
         assert rel_err(got[k].cpu().numpy(), ref[k]) < RTOL_PAIRS, k
 
 
-def test_exact_fallback_fused(vb, vo):
+def test_exact_fallback_fused(vb, vo, fused_mode):
     cs, consts = adversarial_case(1)
     base, T = cs["base"], cs["T"]
     N, K = base["prior"].shape[0], consts["logPi"].shape[0]
@@ -198,6 +212,23 @@ def test_c4_deterministic(c4_full):
     assert torch.equal(a, b)
     assert torch.equal(hz_a, eng.hatZ)
     assert eng.fallback_count() == 0
+
+
+def test_c4_gated_matches_dense(c4_full):
+    """Both fused schedules at full size: same statistics (sums in a different
+    order: ~1e-15 relative), identical hat_Z and L_elbo (same backward code)."""
+    from vbhem_amd import _capi
+    eng, tN = c4_full["eng"], c4_full["tN"]
+    prev = _capi.set_fused_mode(_capi.FUSED_GATED)
+    try:
+        g = eng.fused(tN).clone()
+        hz, LL = eng.hatZ.clone(), eng.LL.clone()
+        _capi.set_fused_mode(_capi.FUSED_DENSE)
+        d = eng.fused(tN).clone()
+    finally:
+        _capi.set_fused_mode(prev)
+    assert rel_err(g.cpu().numpy(), d.cpu().numpy()) < 1e-11
+    assert torch.equal(hz, eng.hatZ) and torch.equal(LL, eng.LL)
 
 
 def test_c4_shard_additivity(vb, c4_full):
