@@ -6,7 +6,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
 LIBDIR   := $(PKG)/lib
 SRCS     := $(PKG)/csrc/vbhem_kernels.hip $(PKG)/csrc/vbhem_fb_split.hip $(PKG)/csrc/vbhem_emission.hip $(PKG)/csrc/vbhem_stats.hip $(PKG)/csrc/vbhem_capi.hip
-HDRS     := include/vbhem_estep.h $(PKG)/csrc/vbhem_internal.h $(PKG)/csrc/vbhem_math.h
+HDRS     := include/vbhem_estep.h $(PKG)/csrc/vbhem_internal.h $(PKG)/csrc/vbhem_math.h $(PKG)/csrc/vbhem_log_table.h
 OBJS     := $(patsubst $(PKG)/csrc/%.hip,$(LIBDIR)/%.o,$(SRCS))
 
 all: lib oracle mex mathcheck
@@ -35,7 +35,7 @@ $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so: integration/vbhem_hmm_bwd_fwd_mex.c include/
 # test-only: the restricted-domain exp/log/rcp of vbhem_math.h, host and device
 mathcheck: tests/mathcheck/libmathcheck.so
 
-tests/mathcheck/libmathcheck.so: tests/mathcheck/mathcheck.hip $(PKG)/csrc/vbhem_math.h
+tests/mathcheck/libmathcheck.so: tests/mathcheck/mathcheck.hip $(PKG)/csrc/vbhem_math.h $(PKG)/csrc/vbhem_log_table.h
 	$(HIPCC) $(HIPFLAGS) -I$(PKG)/csrc -shared -o $@ $<
 
 clean:

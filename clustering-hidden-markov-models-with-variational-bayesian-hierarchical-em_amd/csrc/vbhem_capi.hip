@@ -16,6 +16,7 @@
 
 #include "vbhem_estep.h"
 #include "vbhem_internal.h"
+#include "vbhem_math.h"
 
 namespace {
 
@@ -135,10 +136,9 @@ struct SplitPlan {
 };
 
 // Geometry of fb_split_kernel; must match SplitLayout<S, LPC> (vbhem_internal.h).
-SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
+SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T, int LPC) {
   SplitPlan sp;
   if (!vbhem::split_supported(S, SB, d)) return sp;
-  const int LPC = vbhem::split_lpc(S);
   const int SH = (S + LPC - 1) / LPC;
   const int LPP = S * LPC;
   const int XCS = (LPC * SH + 1) / 2 * 2 + 2;
@@ -160,7 +160,7 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
     const size_t lds_list = ((size_t)off_L + ((size_t)K + 2) / 2) * sizeof(double);
     if (lds_list > kLdsLimit) continue;
     const double util = double(ppb * LPP) / NT;
-    if (util > best + 0.02) {
+    if (util > best + 0.02 || (LPC != vbhem::split_lpc(S) && util >= best)) {
       best = util;
       vbhem::SplitArgs &x = sp.a;
       x.SB = SB; x.d = d; x.covmode = covmode; x.K = K; x.S = S; x.T = T; x.nwb = nwb;
@@ -168,7 +168,8 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T) {
       x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R; x.off_L = off_L;
       x.mode = vbhem::kFbDense;
       sp.lds = lds;
-      sp.lds_bwd = ((size_t)off_R + 2) * sizeof(double);
+      x.off_T = off_R + 2;
+      sp.lds_bwd = ((size_t)x.off_T + vbhem::kLogTabDoubles) * sizeof(double);
       sp.lds_list = lds_list;
       sp.ppb = ppb;
       sp.ok = true;
@@ -281,12 +282,16 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
 struct FbCtx {
   FbPlan plan;      // generic element-per-lane kernel
   SplitPlan split;  // column-per-LPC-lanes kernel (preferred when it applies)
+  SplitPlan bwd;    // its backward-only mode (gated schedule), possibly another LPC
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
 };
 
 int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T) {
-  c.split = plan_split(b->SB, b->d, b->covmode, cl->K, cl->S, T);
+  c.split = plan_split(b->SB, b->d, b->covmode, cl->K, cl->S, T, vbhem::split_lpc(cl->S));
+  // backward-only pass: half the lanes per column (no forward-sweep registers to
+  // hold), more rows per lane: no DPP for S <= 8, more independent exp/log chains
+  c.bwd = plan_split(b->SB, b->d, b->covmode, cl->K, cl->S, T, vbhem::split_lpc_bwd(cl->S));
   if (c.split.ok) {
     vbhem::EmissionArgs &e = c.em;
     e.SB = b->SB; e.d = b->d; e.covmode = b->covmode; e.K = cl->K; e.S = cl->S;
@@ -306,6 +311,8 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
   if (c.split.ok) {
     vbhem::SplitArgs &a = c.split.a;
     a.prior = b->prior; a.A = b->A; a.logA = cl->logA; a.logPi = cl->logPi;
+    vbhem::SplitArgs &ab = c.bwd.a;
+    ab.prior = b->prior; ab.A = b->A; ab.logA = cl->logA; ab.logPi = cl->logPi;
   }
   return VBHEM_OK;
 }
@@ -387,15 +394,19 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   }
   hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
   if (c.split.ok) {
-    vbhem::SplitArgs ca = c.split.a;
+    const SplitPlan &sp = mode == vbhem::kFbBackward ? c.bwd : c.split;
+    vbhem::SplitArgs ca = sp.a;
     ca.mode = mode;
     ca.E = Ebuf; ca.e_ld = e_ld;
     ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
     ca.LL = LL; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
     ca.flag_count = flags; ca.flag_list = flags + 2;
-    const unsigned grid =
-        (unsigned)((i_end - i_begin + c.split.ppb - 1) / c.split.ppb) * (unsigned)ca.K;
-    e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? c.split.lds_bwd : c.split.lds, st);
+    const unsigned ntile = (unsigned)((i_end - i_begin + sp.ppb - 1) / sp.ppb);
+    unsigned grid = ntile * (unsigned)ca.K;
+    if (mode == vbhem::kFbBackward)  // persistent: whole tiles-per-cluster strides
+      grid = (unsigned)ca.K *
+             std::max(1u, std::min(ntile, list_grid(ca, sp.lds_bwd) / (unsigned)ca.K));
+    e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? sp.lds_bwd : sp.lds, st);
     if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
   } else {
     const int nib = (i_end - i_begin + a.BI - 1) / a.BI;

@@ -29,6 +29,7 @@
 #include <cmath>
 
 #include "vbhem_internal.h"
+#include "vbhem_log_table.h"
 #include "vbhem_math.h"
 
 namespace vbhem {
@@ -36,6 +37,9 @@ namespace vbhem {
 namespace {
 
 constexpr double kZMinS = 1e-200;
+
+// log_tab_n's table (backward mode stages it in LDS once per persistent block)
+__device__ const double kLogTab[kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
 
 // ---- DPP lane exchange inside aligned lane quads -------------------------------
 template <int CTRL>
@@ -183,6 +187,7 @@ void fb_split_kernel(const SplitArgs p) {
   constexpr int LPP = S * LPC;  // lanes per pair
   constexpr bool kWaveLocal = (LPP & (LPP - 1)) == 0;  // pairs never straddle a wave
   constexpr bool kFwd = MODE != kFbBackward;
+  constexpr bool kTab = MODE == kFbBackward;  // table-driven log (LDS table)
   const int tid = threadIdx.x;
   const int NT = p.nwb * 64;
   const int PPB = NT / LPP;
@@ -194,6 +199,7 @@ void fb_split_kernel(const SplitArgs p) {
   double *lpi = amax + S;        // [S]
   double *R = lds + p.off_R;     // lattice [(T-2)][SH][NT]
   int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
+  double *ltab = lds + p.off_T;  // [kLogTabDoubles] (kTab)
 
   // ---------------- cluster constants: A' = exp(logA - rowmax), rowmax, logPi --------------
   auto stage_cluster = [&](int j) {
@@ -328,7 +334,8 @@ void fb_split_kernel(const SplitArgs p) {
         bad |= bvalid && rv && !(Z[k] >= kZMinS);
         zz[k] = rv ? Z[k] : 1.0;
       }
-      log_pos_n<SH>(lz, zz);
+      if constexpr (kTab) log_tab_n<SH>(lz, zz, ltab);
+      else log_pos_n<SH>(lz, zz);
 #pragma unroll
       for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];
       if (kFwd && t <= T - 2) {
@@ -547,10 +554,19 @@ void fb_split_kernel(const SplitArgs p) {
     }
   };
 
-  if constexpr (MODE != kFbList) {
+  if constexpr (MODE == kFbDense) {
     const int j = blockIdx.x % K;
     stage_cluster(j);
     run_pair(j, p.i_begin + (int)(blockIdx.x / K) * PPB, p.i_end, nullptr);
+  } else if constexpr (MODE == kFbBackward) {
+    // persistent: block b keeps cluster b % K and strides over the tiles
+    for (int x = tid; x < kLogTabDoubles; x += NT) ltab[x] = kLogTab[x];
+    const int j = blockIdx.x % K;
+    stage_cluster(j);  // (its barriers also publish the table)
+    const int ntile = (p.i_end - p.i_begin + PPB - 1) / PPB;
+    const int stride = (int)gridDim.x / K;
+    for (int tile = (int)blockIdx.x / K; tile < ntile; tile += stride)
+      run_pair(j, p.i_begin + tile * PPB, p.i_end, nullptr);
   } else {
     // work items: cluster j owns ceil(list_tot[j] / PPB) consecutive items
     int *pre = reinterpret_cast<int *>(lds + p.off_L);  // [K + 1]
@@ -597,7 +613,6 @@ template <int S, int LPC>
 static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
   switch (a.mode) {
     case kFbDense: return launch_split_slm<S, LPC, kFbDense>(a, grid, lds, st);
-    case kFbBackward: return launch_split_slm<S, LPC, kFbBackward>(a, grid, lds, st);
     case kFbList: return launch_split_slm<S, LPC, kFbList>(a, grid, lds, st);
     default: return hipErrorInvalidValue;
   }
@@ -616,10 +631,10 @@ static int resident_slm(const SplitArgs &a, size_t lds) {
 
 template <int S>
 static int resident_s(const SplitArgs &a, size_t lds) {
-  constexpr int LPC = SplitLPC<S>::value;
+  constexpr int LPC = SplitLPC<S>::value, LB = BwdLPC<S>::value;
   switch (a.mode) {
     case kFbDense: return resident_slm<S, LPC, kFbDense>(a, lds);
-    case kFbBackward: return resident_slm<S, LPC, kFbBackward>(a, lds);
+    case kFbBackward: return resident_slm<S, LB, kFbBackward>(a, lds);
     default: return resident_slm<S, LPC, kFbList>(a, lds);
   }
 }
@@ -637,6 +652,11 @@ int split_resident_blocks(const SplitArgs &a, size_t lds) {
 
 template <int S>
 static hipError_t launch_split_s(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  constexpr int LB = BwdLPC<S>::value;
+  if (a.mode == kFbBackward) {
+    if (a.lpc != LB) return hipErrorInvalidValue;
+    return launch_split_slm<S, LB, kFbBackward>(a, grid, lds, st);
+  }
   if (a.lpc != SplitLPC<S>::value) return hipErrorInvalidValue;
   return launch_split_sl<S, SplitLPC<S>::value>(a, grid, lds, st);
 }
@@ -668,5 +688,6 @@ bool split_supported(int S, int SB, int d) {
 }
 
 int split_lpc(int S) { return S <= 4 ? 1 : S <= 8 ? 2 : 4; }
+int split_lpc_bwd(int S) { return S <= 8 ? 1 : 2; }
 
 }  // namespace vbhem

@@ -57,6 +57,11 @@ template <int S>
 struct SplitLPC {
   static constexpr int value = S <= 4 ? 1 : S <= 8 ? 2 : 4;
 };
+// the backward-only mode's alternative (no H / sum_t_nu registers: wider columns fit)
+template <int S>
+struct BwdLPC {
+  static constexpr int value = S <= 8 ? 1 : 2;
+};
 template <int S, int LPC>
 struct SplitLayout {
   static constexpr int SH = (S + LPC - 1) / LPC;           // rows per lane
@@ -92,6 +97,7 @@ struct SplitArgs {
   int i_begin, i_end, i_buf0;
   int off_Y, off_F, off_R;  // LDS layout (doubles), depends on pairs per block
   int off_L;                // kFbList: [K + 1] ints of work-item prefix (after the lattice)
+  int off_T;                // kFbBackward: log_tab_n table (kLogTabDoubles, after off_R + 2)
   const double *prior, *A;
   const double *logA, *logPi;
   const double *E;  // emission_kernel output, [K*S][(i - i_buf0) * SB + b], row stride e_ld
@@ -102,7 +108,8 @@ struct SplitArgs {
   int list_cap;
 };
 bool split_supported(int S, int SB, int d);
-int split_lpc(int S);  // lanes per column
+int split_lpc(int S);      // lanes per column
+int split_lpc_bwd(int S);  // lanes per column, alternative for kFbBackward (BwdLPC)
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
 int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mode
 

@@ -168,4 +168,68 @@ __host__ __device__ __forceinline__ void log_pos_n(double (&y)[N], const double 
   }
 }
 
+// ---- table-driven log for the backward sweep (fewer VALU ops than log_pos_n) ----
+// z = 2^k * zz, zz in [0.6875, 1.375) by integer ops on hi(z); zz in interval i
+// of the 128-entry table (vbhem_log_table.h, 4 doubles per entry) with
+// invc ~ 1/c_i: log z = k ln2 + logc_i + log1p(r), r = zz*invc - 1 (one fma,
+// |r| <= 1/128), log1p by its Taylor series through r^8.  The two intervals
+// next to 1 carry invc = 1, logc = 0 (r = zz - 1 exact: full relative accuracy
+// near z = 1).  ~23 VALU ops + 2 LDS reads instead of ~35.  `tab` points at the
+// table in LDS (device) or memory (host).
+constexpr int kLogTabEntries = 128;
+constexpr int kLogTabDoubles = 4 * kLogTabEntries;
+
+template <int N>
+__host__ __device__ __forceinline__ void log_tab_n(double (&y)[N], const double (&z)[N],
+                                                   const double *tab) {
+  constexpr double kLn2Hi = 0x1.62e42fefa3800p-1, kLn2Lo = 0x1.ef35793c76730p-45;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned hi = (unsigned)__double2hiint(z[i]);
+    const int lo = __double2loint(z[i]);
+#else
+    unsigned long long bits;
+    __builtin_memcpy(&bits, &z[i], 8);
+    const unsigned hi = (unsigned)(bits >> 32);
+    const unsigned lo = (unsigned)bits;
+#endif
+    const unsigned t = hi - 0x3fe60000u;
+    const int idx = (int)((t >> 13) & 127u);
+    const int k = (int)t >> 20;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double zz = __hiloint2double((int)(hi - (t & 0xfff00000u)), lo);
+    const double2 e01 = *reinterpret_cast<const double2 *>(__builtin_assume_aligned(tab + 4 * idx, 16));
+    const double invc = e01.x, lch = e01.y;
+#else
+    const unsigned long long zb = ((unsigned long long)(hi - (t & 0xfff00000u)) << 32) | lo;
+    double zz;
+    __builtin_memcpy(&zz, &zb, 8);
+    const double invc = tab[4 * idx], lch = tab[4 * idx + 1];
+#endif
+    const double lcl = tab[4 * idx + 2];
+    const double r = fma(zz, invc, -1.0);
+    const double kd = (double)k;
+    const double w = fma(kd, kLn2Hi, lch);
+    const double yy = w + r;
+    const double lo1 = (w - yy) + r;
+    const double lo2 = fma(kd, kLn2Lo, lcl);
+    const double r2 = r * r;
+    double q = fma(r, -1.0 / 8.0, 1.0 / 7.0);
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -1.0 / 4.0);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    y[i] = yy + fma(q, r2, lo1 + lo2);
+  }
+}
+
+__host__ __device__ __forceinline__ double log_tab(double z, const double *tab) {
+  double y[1];
+  const double zin[1] = {z};
+  log_tab_n<1>(y, zin, tab);
+  return y[0];
+}
+
 }  // namespace vbhem

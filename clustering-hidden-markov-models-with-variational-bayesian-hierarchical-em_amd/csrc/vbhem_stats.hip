@@ -219,6 +219,8 @@ __global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs 
   const int NO = S + S * S + S * NU;
   double *rec = lds;                                            // [PB][RS]
   int *tab = reinterpret_cast<int *>(rec + (size_t)PB * RS);    // [NU] packed (a, b)
+  double *sz = reinterpret_cast<double *>(tab + (NU + 1) / 2 * 2);  // [PB] Z of the batch
+  int *sidx = reinterpret_cast<int *>(sz + PB);                   // [PB] bases of the batch
   for (int cc = tid; cc < NU; cc += kSlThreads) {
     int a = -1, b = -1;
     if (cc >= 1 && cc <= d) {
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs 
   const int tot = p.list_tot[j];
   const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
   const int *lst = p.list + (size_t)j * p.list_cap;
-  const float invNU = 1.0f / (float)NU;
+  const float invNU = 1.0f / (float)NU, invOU = 1.0f / (float)OU, invUN = 1.0f / (float)(SB * NU);
   double *slab = p.slabs + (size_t)c * p.slab_len;
   for (int o0 = 0; o0 < NO; o0 += PER * kSlThreads) {
     double acc[PER];
@@ -247,30 +249,35 @@ __global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs 
     for (int n = n0; n < n1; n += PB) {
       const int np = min(PB, n1 - n);
       __syncthreads();  // tab ready / previous batch consumed
-      for (int pq = 0; pq < np; ++pq) {
-        const int i = lst[n + pq];
+      // batch-wide staging: every element of every pair in flight at once
+      if (tid < np) {
+        const int i = lst[n + tid];
         const size_t lp = (size_t)(i - p.i_buf0) * K + j;
-        const double z = p.Z[lp];
-        double *r = rec + (size_t)pq * RS;
-        for (int e = tid; e < OU; e += kSlThreads) {
-          double v;
-          if (e < OT) v = p.tnu[lp * OT + e];
-          else if (e < OM) v = p.nu1[lp * S + (e - OT)];
-          else v = p.xi[lp * S * S + (e - OM)];
-          r[e] = z * v;
-        }
-        const double *mu0 = p.centres + (size_t)i * SB * d;
-        const double *C0 = p.covars + (size_t)i * SB * dd;
-        for (int e = tid; e < SB * NU; e += kSlThreads) {
-          const int bb = qdiv(e, invNU), cc = e - bb * NU;
-          const int t = tab[cc], a = (t & 0xffff) - 1, b2 = (t >> 16) - 1;
-          const double *mu = mu0 + (size_t)bb * d;
-          double u;
-          if (a < 0) u = 1.0;
-          else if (b2 < 0) u = mu[a];
-          else u = (full ? C0[(size_t)bb * dd + a * d + b2] : C0[(size_t)bb * dd + a]) + mu[a] * mu[b2];
-          r[OU + e] = u;
-        }
+        sidx[tid] = i;
+        sz[tid] = p.Z[lp];
+      }
+      __syncthreads();
+      for (int x = tid; x < np * OU; x += kSlThreads) {
+        const int pq = qdiv(x, invOU), e = x - pq * OU;
+        const size_t lp = (size_t)(sidx[pq] - p.i_buf0) * K + j;
+        double v;
+        if (e < OT) v = p.tnu[lp * OT + e];
+        else if (e < OM) v = p.nu1[lp * S + (e - OT)];
+        else v = p.xi[lp * S * S + (e - OM)];
+        rec[(size_t)pq * RS + e] = sz[pq] * v;
+      }
+      for (int x = tid; x < np * SB * NU; x += kSlThreads) {
+        const int pq = qdiv(x, invUN), e = x - pq * SB * NU;
+        const int bb = qdiv(e, invNU), cc = e - bb * NU;
+        const int i = sidx[pq];
+        const int t = tab[cc], a = (t & 0xffff) - 1, b2 = (t >> 16) - 1;
+        const double *mu = p.centres + ((size_t)i * SB + bb) * d;
+        const double *C = p.covars + ((size_t)i * SB + bb) * dd;
+        double u;
+        if (a < 0) u = 1.0;
+        else if (b2 < 0) u = mu[a];
+        else u = (full ? C[a * d + b2] : C[a]) + mu[a] * mu[b2];
+        rec[(size_t)pq * RS + OU + e] = u;
       }
       __syncthreads();
 #pragma unroll
@@ -657,10 +664,10 @@ int sl_record(const StatsArgs &a) {
 
 bool plan_stats_list(StatsArgs &a, size_t &lds) {
   const size_t rs = (size_t)sl_record(a) * sizeof(double);
-  const size_t tab = (size_t)a.NU * sizeof(int);
-  if (rs + tab > kSlLdsBudget) return false;
-  a.PB = (int)std::min<size_t>(16, (kSlLdsBudget - tab) / rs);
-  lds = (size_t)a.PB * rs + tab;
+  const size_t tab = (size_t)(a.NU + 1) / 2 * 2 * sizeof(int);
+  if (rs + tab + 12 > kSlLdsBudget) return false;
+  a.PB = (int)std::min<size_t>(16, (kSlLdsBudget - tab) / (rs + 12));
+  lds = (size_t)a.PB * (rs + 12) + tab;  // records + tab + Z / base index per pair
   return a.PB >= 1;
 }
 

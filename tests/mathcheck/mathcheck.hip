@@ -5,7 +5,11 @@
 // against libm.
 #include <hip/hip_runtime.h>
 
+#include "vbhem_log_table.h"
 #include "vbhem_math.h"
+
+static const double kLogTabHost[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
+__device__ const double kLogTabDev[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
 
 namespace {
 
@@ -19,6 +23,14 @@ __global__ void math_kernel(int n, const double* __restrict__ x, double* __restr
   r[i] = vbhem::rcp_pos(v);
 }
 
+__global__ void logtab_kernel(int n, const double* __restrict__ x, double* __restrict__ l) {
+  __shared__ __attribute__((aligned(16))) double tab[vbhem::kLogTabDoubles];
+  for (int k = threadIdx.x; k < vbhem::kLogTabDoubles; k += blockDim.x) tab[k] = kLogTabDev[k];
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) l[i] = vbhem::log_tab(x[i], tab);
+}
+
 }  // namespace
 
 extern "C" {
@@ -30,6 +42,27 @@ void mathcheck_host(int n, const double* x, double* e, double* l, double* r) {
     l[i] = vbhem::log_pos(x[i]);
     r[i] = vbhem::rcp_pos(x[i]);
   }
+}
+
+// table-driven log (backward sweep): host / device
+void logtab_host(int n, const double* x, double* l) {
+  for (int i = 0; i < n; i++) l[i] = vbhem::log_tab(x[i], kLogTabHost);
+}
+
+int logtab_device(int n, const double* x, double* l) {
+  double *dx = nullptr, *dl = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)(n > 0 ? n : 1);
+  hipError_t st = hipMalloc(&dx, bytes);
+  if (st == hipSuccess) st = hipMalloc(&dl, bytes);
+  if (st == hipSuccess) st = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+  if (st == hipSuccess && n > 0) {
+    logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl);
+    st = hipGetLastError();
+  }
+  if (st == hipSuccess) st = hipMemcpy(l, dl, sizeof(double) * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(dl);
+  return (int)st;
 }
 
 // Same on device 0 (host arrays in/out).  Returns 0 or a hipError_t.

@@ -215,8 +215,9 @@ def test_c4_deterministic(c4_full):
 
 
 def test_c4_gated_matches_dense(c4_full):
-    """Both fused schedules at full size: same statistics (sums in a different
-    order: ~1e-15 relative), identical hat_Z and L_elbo (same backward code)."""
+    """Both fused schedules at full size: same statistics, hat_Z and L_elbo up to
+    rounding (sums in a different order; the gated backward pass uses the
+    table-driven log, <= 1 ulp like log_pos)."""
     from vbhem_amd import _capi
     eng, tN = c4_full["eng"], c4_full["tN"]
     prev = _capi.set_fused_mode(_capi.FUSED_GATED)
@@ -227,8 +228,9 @@ def test_c4_gated_matches_dense(c4_full):
         d = eng.fused(tN).clone()
     finally:
         _capi.set_fused_mode(prev)
-    assert rel_err(g.cpu().numpy(), d.cpu().numpy()) < 1e-11
-    assert torch.equal(hz, eng.hatZ) and torch.equal(LL, eng.LL)
+    assert rel_err(g.cpu().numpy(), d.cpu().numpy()) < 1e-10
+    assert rel_err(LL.cpu().numpy(), eng.LL.cpu().numpy()) < 1e-13
+    assert rel_err(hz.cpu().numpy(), eng.hatZ.cpu().numpy()) < 1e-9
 
 
 def test_c4_shard_additivity(vb, c4_full):

@@ -57,3 +57,25 @@ def test_device_build(mathcheck):
     rc, e, l, r = _run(mathcheck.mathcheck_device, x)
     assert rc == 0
     _check(x, e, l, r)
+
+
+def _check_logtab(fn):
+    x = _samples()
+    x = np.concatenate([x, np.random.default_rng(7).uniform(0.99, 1.01, N // 4)])
+    dp = ctypes.POINTER(ctypes.c_double)
+    l = np.zeros_like(x)
+    rc = fn(len(x), x.ctypes.data_as(dp), l.ctypes.data_as(dp))
+    pos = x >= 1e-200
+    assert _ulps(l[pos], np.log(x[pos])).max() <= 1.0
+    assert l[2] == 0.0
+    return rc
+
+
+def test_logtab_host_build(mathcheck):
+    """Table-driven log of the backward sweep (log_tab_n), host build."""
+    _check_logtab(mathcheck.logtab_host)
+
+
+@pytest.mark.gpu
+def test_logtab_device_build(mathcheck):
+    assert _check_logtab(mathcheck.logtab_device) == 0
