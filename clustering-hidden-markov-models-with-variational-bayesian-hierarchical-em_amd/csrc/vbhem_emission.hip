@@ -103,7 +103,9 @@ __global__ __launch_bounds__(kEmThreads) void emission_prep_kernel(EmissionArgs 
 // chunks of 8 row tiles (32 fp64 accumulators per lane).
 // ---------------------------------------------------------------------------
 constexpr int kEmRowChunk = 8;
-constexpr int kEmRawSlot = 16 * 64 + 16 * 8;  // doubles per wave: 16 cols x (d*d <= 64, d <= 8)
+// doubles per wave: 16 cols x (d*d <= 64, d <= 8), rows padded to an odd stride
+// (dd + 1, d + 1) so the 16 lanes of a k-group read 16 different bank pairs
+constexpr int kEmRawSlot = 16 * 65 + 16 * 9;
 
 template <bool RAW>
 __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
@@ -118,8 +120,12 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
   const int nctile = (ncols + 15) / 16;
   int *tab = reinterpret_cast<int *>(lds);                 // [KD] (a | b << 8 | kind << 16)
   double *slot = lds + (KD + 1) / 2 + 1 + wave * kEmRawSlot;
-  double *rawc = slot;                                     // [16][dd]
-  double *mus = slot + 16 * dd;                            // [16][d] (unshifted)
+  const int dds = dd | 1, ds = d | 1;                      // odd row strides
+  double *rawc = slot;                                     // [16][dds], [dd] = 0
+  double *mus = slot + 16 * dds;                           // [16][ds] (shifted by z)
+  double *zsh = lds + (KD + 1) / 2 + 1 + 4 * kEmRawSlot;   // [d] the shift z (RAW)
+  if (RAW)
+    for (int a = tid; a < d; a += kEmThreads) zsh[a] = p.shift[a];
   for (int e = tid; e < KD; e += kEmThreads) {
     int a, b, kind;
     if (e < NPF) {
@@ -130,7 +136,17 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
       a = b = e - NPF;
       kind = 3;
     }
-    tab[e] = a | (b << 8) | (kind << 16);
+    if (RAW) {
+      // u = raw[oA] + raw[oB] + f * mu'_a mu'_b + g * mu'_a, offsets within the column's
+      // padded covariance row (dd = its zero slot); dd <= 64, d <= 8 on this path
+      const int z = dd;
+      const int oA = kind == 0 ? a * d + a : kind == 1 ? a * d + b : kind == 2 ? a : z;
+      const int oB = kind == 1 ? b * d + a : z;
+      const int f = kind == 1 ? 2 : kind == 3 ? 0 : 1, g = kind == 3 ? 1 : 0;
+      tab[e] = oA | (oB << 7) | (a << 14) | (b << 18) | (f << 22) | (g << 24);
+    } else {
+      tab[e] = a | (b << 8) | (kind << 16);
+    }
   }
   __syncthreads();
   const int kl = lane >> 4, cl = lane & 15;
@@ -172,13 +188,21 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
     if (RAW) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // previous tile's LDS reads done
-      double2 *r2 = reinterpret_cast<double2 *>(rawc);
 #pragma unroll
       for (int k = 0; k < kPre; ++k) {
-        const int x = lane + 64 * k;
-        if (x < 8 * dd) r2[x] = pre_c[k];
+        const int x = lane + 64 * k;  // elements 2x, 2x+1 of the tile's [16][dd] block
+        if (x < 8 * dd) {
+          const int c = (2 * x) / dd, o = 2 * x - c * dd;  // dd even: the pair stays in a row
+          rawc[c * dds + o] = pre_c[k].x;
+          rawc[c * dds + o + 1] = pre_c[k].y;
+        }
       }
-      if (lane < 8 * d) reinterpret_cast<double2 *>(mus)[lane] = pre_m;
+      if (lane < 16) rawc[lane * dds + dd] = 0.0;  // the zero slot of every column
+      if (lane < 8 * d) {
+        const int c = (2 * lane) / d, o = 2 * lane - c * d;
+        mus[c * ds + o] = pre_m.x - zsh[o];
+        mus[c * ds + o + 1] = pre_m.y - zsh[o + 1];
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -206,20 +230,24 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
         const int e = 4 * t + kl;
         double u = 0.0;
         if (e < KD) {
-          const int tb = tab[e], a = tb & 0xff, b = (tb >> 8) & 0xff, kind = tb >> 16;
+          const int tb = tab[e];
           double ma, mb, caa;
           if (RAW) {
-            ma = mus[cl * d + a] - p.shift[a];
-            mb = mus[cl * d + b] - p.shift[b];
-            caa = kind <= 1 ? rawc[cl * dd + a * d + b] : (kind == 2 ? rawc[cl * dd + a] : 0.0);
-            if (kind == 1) caa += rawc[cl * dd + b * d + a];
+            const int oA = tb & 127, oB = (tb >> 7) & 127, a = (tb >> 14) & 15,
+                      b = (tb >> 18) & 15;
+            const double f = (double)((tb >> 22) & 3), g = (double)((tb >> 24) & 1);
+            ma = mus[cl * ds + a];
+            mb = mus[cl * ds + b];
+            caa = rawc[cl * dds + oA] + rawc[cl * dds + oB];
+            u = fma(f * ma, mb, fma(g, ma, caa));
           } else {
+            const int a = tb & 0xff, b = (tb >> 8) & 0xff, kind = tb >> 16;
             ma = Mg[a] - p.shift[a];
             mb = Mg[b] - p.shift[b];
             caa = kind <= 1 ? Cg[a * d + b] : (kind == 2 ? Cg[a] : 0.0);
             if (kind == 1) caa += Cg[b * d + a];
+            u = kind == 3 ? ma : (kind == 1 ? fma(2.0 * ma, mb, caa) : fma(ma, ma, caa));
           }
-          u = kind == 3 ? ma : (kind == 1 ? fma(2.0 * ma, mb, caa) : fma(ma, ma, caa));
           u = cv ? u : 0.0;
         }
 #pragma unroll
@@ -254,7 +282,7 @@ bool plan_emission(EmissionArgs &a, size_t &lds) {
   const int dd = full ? d * d : d;
   a.wfull = (dd <= 64 && d <= 8 && dd % 2 == 0 && d % 2 == 0);  // RAW: tile staged in LDS
   lds = ((size_t)(a.KD + 1) / 2 + 1) * sizeof(double) +
-        (a.wfull ? (size_t)4 * kEmRawSlot * sizeof(double) : 0);
+        (a.wfull ? (size_t)4 * kEmRawSlot * sizeof(double) : 0) + (size_t)d * sizeof(double);
   a.CB = 16;
   return true;
 }
