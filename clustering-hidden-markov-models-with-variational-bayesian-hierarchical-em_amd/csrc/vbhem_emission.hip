@@ -107,10 +107,15 @@ constexpr int kEmRowChunk = 8;
 // (dd + 1, d + 1) so the 16 lanes of a k-group read 16 different bank pairs
 constexpr int kEmRawSlot = 16 * 65 + 16 * 9;
 
-template <bool RAW>
-__global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
+constexpr int kEmMaxThreads = 512;
+
+// RAW: the tile's covariances / means staged in LDS (d <= 8); WL: W staged in LDS
+// once per (persistent) block, operand A read by ds_read instead of L2 loads.
+template <bool RAW, bool WL>
+__global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NTH = blockDim.x, NW = NTH / 64;
   const int d = p.d, SB = p.SB, KS = p.K * p.S, KD = p.KD;
   const bool full = p.covmode == kCovFull;
   const int NPF = full ? d * (d + 1) / 2 : d;
@@ -118,15 +123,19 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
   const int RT = (KS + 15) / 16, KQ = (KD + 3) / 4;
   const int ncols = (p.i_end - p.i_begin) * SB;
   const int nctile = (ncols + 15) / 16;
-  int *tab = reinterpret_cast<int *>(lds);                 // [KD] (a | b << 8 | kind << 16)
-  double *slot = lds + (KD + 1) / 2 + 1 + wave * kEmRawSlot;
+  int *tab = reinterpret_cast<int *>(lds);                 // [KD] packed operand descriptor
+  double *Wl = lds + (KD + 1) / 2 + 1;                     // [KD][KS] (WL)
+  double *slots = Wl + (WL ? (size_t)KD * KS : 0);
+  double *slot = slots + wave * kEmRawSlot;
   const int dds = dd | 1, ds = d | 1;                      // odd row strides
   double *rawc = slot;                                     // [16][dds], [dd] = 0
   double *mus = slot + 16 * dds;                           // [16][ds] (shifted by z)
-  double *zsh = lds + (KD + 1) / 2 + 1 + 4 * kEmRawSlot;   // [d] the shift z (RAW)
+  double *zsh = slots + (RAW ? NW * kEmRawSlot : 0);      // [d] the shift z (RAW)
   if (RAW)
-    for (int a = tid; a < d; a += kEmThreads) zsh[a] = p.shift[a];
-  for (int e = tid; e < KD; e += kEmThreads) {
+    for (int a = tid; a < d; a += NTH) zsh[a] = p.shift[a];
+  if (WL)
+    for (int x = tid; x < KD * KS; x += NTH) Wl[x] = p.W[x];
+  for (int e = tid; e < KD; e += NTH) {
     int a, b, kind;
     if (e < NPF) {
       a = b = e;
@@ -151,8 +160,8 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
   __syncthreads();
   const int kl = lane >> 4, cl = lane & 15;
   const size_t ldE = (size_t)p.e_ld;
-  const int wstride = gridDim.x * (kEmThreads / 64);
-  int ct = blockIdx.x * (kEmThreads / 64) + wave;
+  const int wstride = gridDim.x * NW;
+  int ct = blockIdx.x * NW + wave;
 
   // register prefetch of a tile's raw covariances (16 cols x dd <= 1024 doubles) and
   // means (16 x d <= 128): 8 + 1 double2 per lane, fully coalesced
@@ -217,7 +226,7 @@ __global__ __launch_bounds__(kEmThreads) void emission_kernel(EmissionArgs p) {
       double wc[kEmRowChunk], wn[kEmRowChunk];
       auto loadw = [&](int t, double (&w)[kEmRowChunk]) {
         const int e = 4 * t + kl;
-        const double *We = p.W + (size_t)(e < KD ? e : 0) * KS;
+        const double *We = (WL ? Wl : p.W) + (size_t)(e < KD ? e : 0) * KS;
 #pragma unroll
         for (int q = 0; q < kEmRowChunk; ++q) {
           const int row = (r0 + q) * 16 + cl;
@@ -281,8 +290,14 @@ bool plan_emission(EmissionArgs &a, size_t &lds) {
   a.KD = full ? d * (d + 1) / 2 + d : 2 * d;
   const int dd = full ? d * d : d;
   a.wfull = (dd <= 64 && d <= 8 && dd % 2 == 0 && d % 2 == 0);  // RAW: tile staged in LDS
-  lds = ((size_t)(a.KD + 1) / 2 + 1) * sizeof(double) +
-        (a.wfull ? (size_t)4 * kEmRawSlot * sizeof(double) : 0) + (size_t)d * sizeof(double);
+  // 8 waves per block with W in LDS when it fits one block per CU, else 4 waves
+  // reading W through L1/L2
+  const size_t head = ((size_t)(a.KD + 1) / 2 + 1 + d) * sizeof(double);
+  const size_t wbytes = (size_t)a.KD * a.K * a.S * sizeof(double);
+  const size_t slot = a.wfull ? (size_t)kEmRawSlot * sizeof(double) : 0;
+  a.wlds = head + wbytes + 8 * slot <= 160 * 1024;
+  a.nwave = a.wlds ? 8 : 4;
+  lds = head + (a.wlds ? wbytes : 0) + (size_t)a.nwave * slot;
   a.CB = 16;
   return true;
 }
@@ -292,25 +307,39 @@ hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <bool RAW>
-static hipError_t launch_emission_t(const EmissionArgs &a, size_t lds, unsigned grid,
-                                    hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&emission_kernel<RAW>),
+template <bool RAW, bool WL>
+static hipError_t launch_emission_t(const EmissionArgs &a, size_t lds, hipStream_t st) {
+  auto *fn = &emission_kernel<RAW, WL>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(emission_kernel<RAW>, dim3(grid), dim3(kEmThreads), lds, st, a);
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, a.nwave * 64, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int ncols = (a.i_end - a.i_begin) * a.SB;
+  const int nctile = (ncols + 15) / 16;
+  // persistent: every resident block, every wave walks 16-column tiles
+  const unsigned grid = (unsigned)std::min((nctile + a.nwave - 1) / a.nwave, cus * per_cu);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(a.nwave * 64), lds, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   if (ncols <= 0) return hipSuccess;
-  const int nctile = (ncols + 15) / 16;
-  const int per_block = kEmThreads / 64;
-  // persistent: ~4 resident blocks per CU, every wave walks 16-column tiles
-  const unsigned grid = (unsigned)std::min((nctile + per_block - 1) / per_block, 256 * 4);
-  return a.wfull ? launch_emission_t<true>(a, lds, grid, st)
-                 : launch_emission_t<false>(a, lds, grid, st);
+  if (a.wfull) return a.wlds ? launch_emission_t<true, true>(a, lds, st)
+                             : launch_emission_t<true, false>(a, lds, st);
+  return a.wlds ? launch_emission_t<false, true>(a, lds, st)
+                : launch_emission_t<false, false>(a, lds, st);
 }
 
 }  // namespace vbhem

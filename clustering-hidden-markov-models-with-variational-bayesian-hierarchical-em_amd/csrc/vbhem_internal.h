@@ -74,6 +74,8 @@ struct SplitLayout {
 struct EmissionArgs {
   int SB, d, covmode, K, S, KD, CB;
   bool wfull;  // column tiles staged in LDS (d <= 8); else read through L1/L2
+  bool wlds;   // W staged in LDS (8-wave blocks); else read through L1/L2 (4-wave blocks)
+  int nwave;
   int i_begin, i_end, i_buf0;
   long long e_ld;  // row stride of E = (bases in the buffer) * SB
   const double *centres, *covars, *m, *P, *c;
