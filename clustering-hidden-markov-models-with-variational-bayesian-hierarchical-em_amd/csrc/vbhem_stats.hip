@@ -666,7 +666,8 @@ bool plan_stats_list(StatsArgs &a, size_t &lds) {
   const size_t rs = (size_t)sl_record(a) * sizeof(double);
   const size_t tab = (size_t)(a.NU + 1) / 2 * 2 * sizeof(int);
   if (rs + tab + 12 > kSlLdsBudget) return false;
-  a.PB = (int)std::min<size_t>(16, (kSlLdsBudget - tab) / (rs + 12));
+  // small batches: many resident blocks hide the gather latency (6 measured best at C4)
+  a.PB = (int)std::min<size_t>(6, (kSlLdsBudget - tab) / (rs + 12));
   lds = (size_t)a.PB * (rs + 12) + tab;  // records + tab + Z / base index per pair
   return a.PB >= 1;
 }

@@ -1,0 +1,8 @@
+# A/B an environment knob on the C4 bench: scripts/ab_env.sh VAR v1 v2 ...
+set -o pipefail
+VAR=$1; shift
+for v in "$@"; do
+  if [ "$v" = "-" ]; then unset $VAR; else export $VAR=$v; fi
+  timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/ab.json 2>&1 || exit 1
+  tail -1 gpurun_out/ab.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$VAR=$v', 'value',round(d['value'],2),'bwd',round(d['roofline']['kernel_ms'],3),'fwd',round(d['gated_forward']['kernel_ms'],3),'stats',round(d['stats_kernels_ms_per_step'],3),'em',round(d['emission_kernel_ms'],3))"
+done
