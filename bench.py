@@ -250,9 +250,10 @@ def main():
     achieved = fpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e12
     bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split, backward_only=gated)
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
-    lpc = 1 if S <= 4 else 2 if S <= 8 else 4
-    kname = (f"vbhem::fb_split_kernel<{S}, {lpc}, {1 if gated else 0}>" if split
-             else "vbhem::fb_pairs_kernel")
+    lpc = 1 if S <= 4 else 2 if S <= 8 else 4      # split_lpc (dense / list modes)
+    lpc_bwd = 1 if S <= 8 else 2                    # split_lpc_bwd (backward mode)
+    kname = (f"vbhem::fb_split_kernel<{S}, {lpc_bwd if gated else lpc}, {1 if gated else 0}>"
+             if split else "vbhem::fb_pairs_kernel")
     traffic, traffic_src = committed_traffic(args.config, N, world, kname)
     gf_ms = tk["gated_fwd_ms"] / max(1, tk["gated_fwd_launches"])
     res = {

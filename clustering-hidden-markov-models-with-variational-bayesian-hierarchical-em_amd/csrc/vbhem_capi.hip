@@ -403,9 +403,11 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     ca.flag_count = flags; ca.flag_list = flags + 2;
     const unsigned ntile = (unsigned)((i_end - i_begin + sp.ppb - 1) / sp.ppb);
     unsigned grid = ntile * (unsigned)ca.K;
-    if (mode == vbhem::kFbBackward)  // persistent: whole tiles-per-cluster strides
-      grid = (unsigned)ca.K *
-             std::max(1u, std::min(ntile, list_grid(ca, sp.lds_bwd) / (unsigned)ca.K));
+    if (mode == vbhem::kFbBackward) {  // persistent: NB blocks per cluster (x8 when possible)
+      unsigned nb = std::max(1u, std::min(ntile, list_grid(ca, sp.lds_bwd) / (unsigned)ca.K));
+      if (nb >= 8) nb = nb / 8 * 8;
+      grid = (unsigned)ca.K * nb;
+    }
     e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? sp.lds_bwd : sp.lds, st);
     if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
   } else {

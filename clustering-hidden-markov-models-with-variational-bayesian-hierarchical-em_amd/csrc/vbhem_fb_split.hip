@@ -559,13 +559,24 @@ void fb_split_kernel(const SplitArgs p) {
     stage_cluster(j);
     run_pair(j, p.i_begin + (int)(blockIdx.x / K) * PPB, p.i_end, nullptr);
   } else if constexpr (MODE == kFbBackward) {
-    // persistent: block b keeps cluster b % K and strides over the tiles
+    // persistent: NB blocks per cluster, each keeps its cluster and strides over the
+    // tiles.  XCD-aware when NB % 8 == 0: workgroups are dealt round-robin to the 8
+    // XCDs (b % 8), so the K blocks that walk the same tiles (same base transitions,
+    // read by all K clusters) are put on one XCD and share its L2.
     for (int x = tid; x < kLogTabDoubles; x += NT) ltab[x] = kLogTab[x];
-    const int j = blockIdx.x % K;
+    const int b = blockIdx.x, NB = (int)gridDim.x / K;
+    int j, t0;
+    if (NB % 8 == 0) {
+      const int r = b / 8;
+      j = r % K;
+      t0 = (r / K) * 8 + b % 8;
+    } else {
+      j = b % K;
+      t0 = b / K;
+    }
     stage_cluster(j);  // (its barriers also publish the table)
     const int ntile = (p.i_end - p.i_begin + PPB - 1) / PPB;
-    const int stride = (int)gridDim.x / K;
-    for (int tile = (int)blockIdx.x / K; tile < ntile; tile += stride)
+    for (int tile = t0; tile < ntile; tile += NB)
       run_pair(j, p.i_begin + tile * PPB, p.i_end, nullptr);
   } else {
     // work items: cluster j owns ceil(list_tot[j] / PPB) consecutive items
