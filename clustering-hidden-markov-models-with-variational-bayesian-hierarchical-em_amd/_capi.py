@@ -15,7 +15,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libvbhem_estep.so")
+# VBHEM_LIB_PATH: another build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("VBHEM_LIB_PATH") or os.path.join(HERE, "lib", "libvbhem_estep.so")
 
 VBHEM_COV_DIAG, VBHEM_COV_FULL = 0, 1
 _c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p

@@ -247,6 +247,7 @@ struct FusedWs {
   int slab_len;
   int *flags;
   int *gate_cnt, *list, *list_tot;  // gated schedule: [nslab][K], [K][group], [K]
+  double *Atg;                      // gated schedule: [K][S][S] A' for the backward pass
   double *scratch, *nu1, *xi, *tnu, *Z, *slabs;
   double *E, *W, *bias, *shift;
 };
@@ -276,6 +277,7 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.gate_cnt = cv.take<int>((size_t)w.nslab * K);
   w.list = cv.take<int>(g * K);
   w.list_tot = cv.take<int>((size_t)K);
+  w.Atg = cv.take<double>((size_t)K * S * S);
   return cv.off + 256;
 }
 
@@ -537,6 +539,11 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   sa.list = w.list; sa.list_tot = w.list_tot; sa.list_cap = w.group;
   rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st);
   if (rc != VBHEM_OK) return rc;
+  if (gated) {
+    ctx.bwd.a.Atg = w.Atg;
+    e = vbhem::launch_split_prep(ctx.bwd.a, w.Atg, st);
+    if (e != hipSuccess) return hip_fail(e, "split_prep_kernel");
+  }
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);
     const long long e_ld = (long long)w.group * SB;

@@ -282,6 +282,9 @@ void fb_split_kernel(const SplitArgs p) {
     // A'(rows of every owner block, my columns r0..r0+SH): register-resident for both sweeps
     // (occupancy is bounded by LDS, not registers)
     constexpr bool kAtReg = LPC * SH * SH <= 48;  // <= 96 VGPRs
+    // LPC = 1 (one lane per column, rows uniform across the wave): A' is read as
+    // scalar operands from global memory (s_load, scalar cache) instead of LDS
+    constexpr bool kAtScalar = MODE == kFbBackward && LPC == 1 && !kAtReg;
     double atr[kAtReg ? LPC * SH : 1][SH];
     if constexpr (kAtReg) {
 #pragma unroll
@@ -310,12 +313,20 @@ void fb_split_kernel(const SplitArgs p) {
       }
       // partial Z for every owner's rows, then reduce-scatter
       double Pz[LPC * SH];
+      typedef const double __attribute__((address_space(4))) cdouble;
+      // (the kernel argument itself, not the laundered pointer: an asm output counts
+      // as divergent, which would turn these into vector loads)
+      const double *Agp = p.Atg + __builtin_amdgcn_readfirstlane(j * S * S);
 #pragma unroll
       for (int r = 0; r < LPC * SH; ++r) {
         double ar[SH];
         if constexpr (kAtReg) {
 #pragma unroll
           for (int k = 0; k < SH; ++k) ar[k] = atr[r][k];
+        } else if constexpr (kAtScalar) {
+          const cdouble *Ac = (const cdouble *)Agp;
+#pragma unroll
+          for (int k = 0; k < SH; ++k) ar[k] = Ac[r * S + k];
         } else {
           const int ra = rel_row<SH>(r, h);
           load_row<S, SH, LPC>(ar, At + (ra < S ? ra : S - 1) * S, r0);
@@ -607,6 +618,24 @@ void fb_split_kernel(const SplitArgs p) {
       run_pair(jj, (wi - pre[jj]) * PPB, tot, p.list + (size_t)jj * p.list_cap);
     }
   }
+}
+
+// A' = exp(logA - rowmax) of every cluster in global memory (backward mode, LPC = 1)
+__global__ __launch_bounds__(256) void split_prep_kernel(const double *logA, int KS, int S,
+                                                         double *Atg) {
+  const int r = blockIdx.x * 256 + threadIdx.x;  // row (j, rho)
+  if (r >= KS) return;
+  const double *la = logA + (size_t)r * S;
+  double mx = la[0];
+  for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
+  for (int s2 = 0; s2 < S; ++s2) Atg[(size_t)r * S + s2] = exp_nonpos(la[s2] - mx);
+}
+
+hipError_t launch_split_prep(const SplitArgs &a, double *Atg, hipStream_t st) {
+  const int KS = a.K * a.S;
+  hipLaunchKernelGGL(split_prep_kernel, dim3((KS + 255) / 256), dim3(256), 0, st, a.logA, KS, a.S,
+                     Atg);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -108,12 +108,14 @@ struct SplitArgs {
   int *flag_count, *flag_list;
   const int *list, *list_tot;  // kFbList: gated bases per cluster (gate_list_kernel)
   int list_cap;
+  const double *Atg;           // kFbBackward, LPC 1: [K][S][S] A' (split_prep_kernel)
 };
 bool split_supported(int S, int SB, int d);
 int split_lpc(int S);      // lanes per column
 int split_lpc_bwd(int S);  // lanes per column, alternative for kFbBackward (BwdLPC)
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
 int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mode
+hipError_t launch_split_prep(const SplitArgs &a, double *Atg, hipStream_t st);
 
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
