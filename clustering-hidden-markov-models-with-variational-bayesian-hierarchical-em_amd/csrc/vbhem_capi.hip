@@ -169,7 +169,7 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T, int LPC) {
       x.mode = vbhem::kFbDense;
       sp.lds = lds;
       x.off_T = off_R + 2;
-      sp.lds_bwd = ((size_t)x.off_T + vbhem::kLogTabDoubles) * sizeof(double);
+      sp.lds_bwd = ((size_t)x.off_T + vbhem::kLogTabDoubles + vbhem::kExpTabDoubles) * sizeof(double);
       sp.lds_list = lds_list;
       sp.ppb = ppb;
       sp.ok = true;

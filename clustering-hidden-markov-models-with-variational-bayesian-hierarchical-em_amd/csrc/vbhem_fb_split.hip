@@ -40,6 +40,7 @@ constexpr double kZMinS = 1e-200;
 
 // log_tab_n's table (backward mode stages it in LDS once per persistent block)
 __device__ const double kLogTab[kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
+__device__ const double kExpTab[kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
 
 // ---- DPP lane exchange inside aligned lane quads -------------------------------
 template <int CTRL>
@@ -199,7 +200,8 @@ void fb_split_kernel(const SplitArgs p) {
   double *lpi = amax + S;        // [S]
   double *R = lds + p.off_R;     // lattice [(T-2)][SH][NT]
   int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
-  double *ltab = lds + p.off_T;  // [kLogTabDoubles] (kTab)
+  double *ltab = lds + p.off_T;                // [kLogTabDoubles] (kTab)
+  double *etab = ltab + kLogTabDoubles;        // [kExpTabDoubles] (kTab)
 
   // ---------------- cluster constants: A' = exp(logA - rowmax), rowmax, logPi --------------
   auto stage_cluster = [&](int j) {
@@ -309,7 +311,8 @@ void fb_split_kernel(const SplitArgs p) {
         double ex[SH];
 #pragma unroll
         for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
-        exp_nonpos_n<SH>(G, ex);
+        if constexpr (kTab) exp_tab_n<SH>(G, ex, etab);
+        else exp_nonpos_n<SH>(G, ex);
       }
       // partial Z for every owner's rows, then reduce-scatter
       double Pz[LPC * SH];
@@ -575,6 +578,7 @@ void fb_split_kernel(const SplitArgs p) {
     // XCDs (b % 8), so the K blocks that walk the same tiles (same base transitions,
     // read by all K clusters) are put on one XCD and share its L2.
     for (int x = tid; x < kLogTabDoubles; x += NT) ltab[x] = kLogTab[x];
+    for (int x = tid; x < kExpTabDoubles; x += NT) etab[x] = kExpTab[x];
     const int b = blockIdx.x, NB = (int)gridDim.x / K;
     int j, t0;
     if (NB % 8 == 0) {

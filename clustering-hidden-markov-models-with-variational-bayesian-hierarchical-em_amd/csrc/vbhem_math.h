@@ -225,6 +225,48 @@ __host__ __device__ __forceinline__ void log_tab_n(double (&y)[N], const double 
   }
 }
 
+// ---- table-driven exp for the backward sweep ----
+// x <= 0: n = rint(x * 256/ln2), r = x - n ln2/256 (|r| <= ln2/512, Cody-Waite with a
+// 33-bit hi part: n*hi exact for |n| < 2^20), exp(x) = 2^(n>>8) * 2^((n&255)/256) *
+// (1 + p(r)), p(r) = r + r^2 (1/2 + r/6 + r^2/24) (truncation < 0.2 ulp);
+// 2^(j/256) = hi + lo from the 256-entry table (vbhem_log_table.h, 2 doubles per
+// entry).  ~17 VALU + 1 LDS read instead of ~20.
+constexpr int kExpTabEntries = 256;
+constexpr int kExpTabDoubles = 2 * kExpTabEntries;
+
+template <int N>
+__host__ __device__ __forceinline__ void exp_tab_n(double (&y)[N], const double (&xin)[N],
+                                                   const double *tab) {
+  constexpr double kInvLn2N = 369.3299304675746;        // 256 / ln 2
+  constexpr double kLn2NHi = 0x1.62e42ff000000p-9;     // ln 2 / 256, 33 bits
+  constexpr double kLn2NLo = -0x1.718432a1b0e26p-43;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double x = fmax(xin[i], -800.0);
+    const double n = rint(x * kInvLn2N);
+    double r = fma(-n, kLn2NHi, x);
+    r = fma(-n, kLn2NLo, r);
+    const int ni = (int)n;
+    const int j = ni & 255, k = ni >> 8;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double2 t = *reinterpret_cast<const double2 *>(__builtin_assume_aligned(tab + 2 * j, 16));
+    const double th = t.x, tl = t.y;
+#else
+    const double th = tab[2 * j], tl = tab[2 * j + 1];
+#endif
+    const double q = fma(fma(r, 1.0 / 24.0, 1.0 / 6.0), r, 0.5);
+    const double p = fma(q, r * r, r);
+    y[i] = ldexp(th + fma(th, p, tl), k);
+  }
+}
+
+__host__ __device__ __forceinline__ double exp_tab(double x, const double *tab) {
+  double y[1];
+  const double xin[1] = {x};
+  exp_tab_n<1>(y, xin, tab);
+  return y[0];
+}
+
 __host__ __device__ __forceinline__ double log_tab(double z, const double *tab) {
   double y[1];
   const double zin[1] = {z};

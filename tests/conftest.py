@@ -104,9 +104,9 @@ def mathcheck():
     lib.mathcheck_host.restype = None
     lib.mathcheck_device.argtypes = [ctypes.c_int, dp, dp, dp, dp]
     lib.mathcheck_device.restype = ctypes.c_int
-    lib.logtab_host.argtypes = [ctypes.c_int, dp, dp]
+    lib.logtab_host.argtypes = [ctypes.c_int, dp, dp, dp]
     lib.logtab_host.restype = None
-    lib.logtab_device.argtypes = [ctypes.c_int, dp, dp]
+    lib.logtab_device.argtypes = [ctypes.c_int, dp, dp, dp]
     lib.logtab_device.restype = ctypes.c_int
     return lib
 

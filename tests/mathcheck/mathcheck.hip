@@ -10,6 +10,8 @@
 
 static const double kLogTabHost[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
 __device__ const double kLogTabDev[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
+static const double kExpTabHost[vbhem::kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
+__device__ const double kExpTabDev[vbhem::kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
 
 namespace {
 
@@ -23,12 +25,18 @@ __global__ void math_kernel(int n, const double* __restrict__ x, double* __restr
   r[i] = vbhem::rcp_pos(v);
 }
 
-__global__ void logtab_kernel(int n, const double* __restrict__ x, double* __restrict__ l) {
+__global__ void logtab_kernel(int n, const double* __restrict__ x, double* __restrict__ l,
+                              double* __restrict__ e) {
   __shared__ __attribute__((aligned(16))) double tab[vbhem::kLogTabDoubles];
+  __shared__ __attribute__((aligned(16))) double etab[vbhem::kExpTabDoubles];
   for (int k = threadIdx.x; k < vbhem::kLogTabDoubles; k += blockDim.x) tab[k] = kLogTabDev[k];
+  for (int k = threadIdx.x; k < vbhem::kExpTabDoubles; k += blockDim.x) etab[k] = kExpTabDev[k];
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) l[i] = vbhem::log_tab(x[i], tab);
+  if (i < n) {
+    l[i] = vbhem::log_tab(x[i], tab);
+    e[i] = vbhem::exp_tab(-x[i], etab);
+  }
 }
 
 }  // namespace
@@ -44,24 +52,30 @@ void mathcheck_host(int n, const double* x, double* e, double* l, double* r) {
   }
 }
 
-// table-driven log (backward sweep): host / device
-void logtab_host(int n, const double* x, double* l) {
-  for (int i = 0; i < n; i++) l[i] = vbhem::log_tab(x[i], kLogTabHost);
+// table-driven log / exp (backward sweep): log at x, exp at -x; host / device
+void logtab_host(int n, const double* x, double* l, double* e) {
+  for (int i = 0; i < n; i++) {
+    l[i] = vbhem::log_tab(x[i], kLogTabHost);
+    e[i] = vbhem::exp_tab(-x[i], kExpTabHost);
+  }
 }
 
-int logtab_device(int n, const double* x, double* l) {
-  double *dx = nullptr, *dl = nullptr;
+int logtab_device(int n, const double* x, double* l, double* e) {
+  double *dx = nullptr, *dl = nullptr, *de = nullptr;
   const size_t bytes = sizeof(double) * (size_t)(n > 0 ? n : 1);
   hipError_t st = hipMalloc(&dx, bytes);
   if (st == hipSuccess) st = hipMalloc(&dl, bytes);
+  if (st == hipSuccess) st = hipMalloc(&de, bytes);
   if (st == hipSuccess) st = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
   if (st == hipSuccess && n > 0) {
-    logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl);
+    logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
     st = hipGetLastError();
   }
   if (st == hipSuccess) st = hipMemcpy(l, dl, sizeof(double) * n, hipMemcpyDeviceToHost);
+  if (st == hipSuccess) st = hipMemcpy(e, de, sizeof(double) * n, hipMemcpyDeviceToHost);
   (void)hipFree(dx);
   (void)hipFree(dl);
+  (void)hipFree(de);
   return (int)st;
 }
 

@@ -60,14 +60,17 @@ def test_device_build(mathcheck):
 
 
 def _check_logtab(fn):
+    """log_tab at x and exp_tab at -x (the backward sweep's table-driven pair)."""
     x = _samples()
     x = np.concatenate([x, np.random.default_rng(7).uniform(0.99, 1.01, N // 4)])
     dp = ctypes.POINTER(ctypes.c_double)
-    l = np.zeros_like(x)
-    rc = fn(len(x), x.ctypes.data_as(dp), l.ctypes.data_as(dp))
+    l, e = np.zeros_like(x), np.zeros_like(x)
+    rc = fn(len(x), x.ctypes.data_as(dp), l.ctypes.data_as(dp), e.ctypes.data_as(dp))
     pos = x >= 1e-200
     assert _ulps(l[pos], np.log(x[pos])).max() <= 1.0
     assert l[2] == 0.0
+    m = x <= 700
+    assert _ulps(e[m], np.exp(-x[m])).max() <= 1.0
     return rc
 
 
