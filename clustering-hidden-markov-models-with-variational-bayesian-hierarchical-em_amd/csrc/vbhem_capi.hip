@@ -258,6 +258,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   const size_t per_base = (size_t)K * (S + (size_t)S * S + 2 * (size_t)S * SB) * sizeof(double);
   size_t g = std::max<size_t>(1, kGroupBudget / std::max<size_t>(1, per_base));
   g = std::min<size_t>(g, (size_t)std::max(1, b->N));
+  if (const char *ev = std::getenv("VBHEM_GROUP_BASES"))  // tests: force several groups
+    g = std::max<size_t>(1, std::min<size_t>(g, (size_t)std::atoll(ev)));
   w.group = (int)g;
   int maxslab = kMaxSlabs;
   if (const char *ev = std::getenv("VBHEM_NSLAB")) maxslab = std::max(1, std::min(8192, std::atoi(ev)));

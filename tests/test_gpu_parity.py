@@ -88,6 +88,27 @@ def test_fused_matches_oracle(vb, vo, shape, fused_mode, tscale):
     assert rel_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
+def test_fused_multigroup(vb, vo, fused_mode, monkeypatch):
+    """The fused call split into several base groups (VBHEM_GROUP_BASES: E, the
+    per-pair scratch and the gate lists are per group; the slabs accumulate)."""
+    name, N, K, S, Sb, d, cov, T = "multigroup", 300, 6, 5, 4, 3, 1, 7
+    monkeypatch.setenv("VBHEM_GROUP_BASES", "64")
+    monkeypatch.setenv("VBHEM_NSLAB", "7")
+    cs = make_case(N, K, S, Sb, d, cov, seed=seed_of(name), ragged=True, tau=T)
+    base, consts = cs["base"], cs["consts"]
+    pairs = vo.c_estep_pairs(base, consts, T, nthreads=4)
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, pairs, cov)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, cov)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert rel_err(got[k], st[k]) < 1e-9, k
+    assert rel_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
+    assert rel_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
 def adversarial_case(cov=1, S=4, Sb=4, d=3, N=4, K=3, T=6):
     """Cluster 0's transitions put all mass on sigma+1 while its emissions put
     all mass on state 0: the factorised normaliser Z ~ e^-600 underflows the
