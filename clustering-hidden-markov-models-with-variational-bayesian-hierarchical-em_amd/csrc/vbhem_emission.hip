@@ -32,7 +32,6 @@ namespace vbhem {
 namespace {
 typedef double double4_t __attribute__((ext_vector_type(4)));
 constexpr double kLog2PiE = 1.8378770664093454835606594728112353;
-constexpr int kEmThreads = 256;
 
 __device__ __forceinline__ void packed_ab(int e, int d, int &a, int &b) {
   a = 0;
@@ -46,48 +45,59 @@ __device__ __forceinline__ void packed_ab(int e, int d, int &a, int &b) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// prep: z (mean of all cluster means), bias[K*S], W[KD][K*S]
+// prep: z (mean of all cluster means), bias[K*S], W[KD][K*S]; one block per
+// cluster row r = (j, s), threads over the packed entries (every block forms z
+// in the same fixed order, block 0 publishes it)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kEmThreads) void emission_prep_kernel(EmissionArgs p) {
-  __shared__ double zs[64];
-  const int tid = threadIdx.x, d = p.d, KS = p.K * p.S;
+constexpr int kPrepThreads = 64;
+
+__global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArgs p) {
+  __shared__ double zs[64], pm[64];
+  const int tid = threadIdx.x, d = p.d, KS = p.K * p.S, r = blockIdx.x;
   const bool full = p.covmode == kCovFull;
   const int NPF = full ? d * (d + 1) / 2 : d;
-  // z: fixed-order mean over the K*S cluster means
-  for (int a = tid; a < d; a += kEmThreads) {
+  for (int a = tid; a < d; a += kPrepThreads) {
     double s = 0.0;
-    for (int r = 0; r < KS; ++r) s += p.m[(size_t)r * d + a];
+    for (int q = 0; q < KS; ++q) s += p.m[(size_t)q * d + a];
     zs[a] = s / (double)KS;
-    p.shift[a] = zs[a];
+    if (r == 0) p.shift[a] = zs[a];
   }
   __syncthreads();
-  for (int r = tid; r < KS; r += kEmThreads) {
-    const double *mr = p.m + (size_t)r * d;
-    if (full) {
-      const double *P = p.P + (size_t)r * d * d;
-      double q = 0.0;
-      for (int a = 0; a < d; ++a) {
-        double pm = 0.0;  // (P_sym m')_a
-        for (int b = 0; b < d; ++b) {
-          const double ps = 0.5 * (P[a * d + b] + P[b * d + a]);
-          pm = fma(ps, mr[b] - zs[b], pm);
-        }
-        q = fma(mr[a] - zs[a], pm, q);
-        p.W[(size_t)(NPF + a) * KS + r] = -2.0 * pm;
+  const double *mr = p.m + (size_t)r * d;
+  if (full) {
+    const double *P = p.P + (size_t)r * d * d;
+    for (int a = tid; a < d; a += kPrepThreads) {
+      double v = 0.0;  // (P_sym m')_a
+      for (int b = 0; b < d; ++b) {
+        const double ps = 0.5 * (P[a * d + b] + P[b * d + a]);
+        v = fma(ps, mr[b] - zs[b], v);
       }
+      pm[a] = v;
+      p.W[(size_t)(NPF + a) * KS + r] = -2.0 * v;
+    }
+    for (int e = tid; e < NPF; e += kPrepThreads) {
+      int a, b;
+      packed_ab(e, d, a, b);
+      p.W[(size_t)e * KS + r] = (a == b) ? P[a * d + a] : 0.5 * (P[a * d + b] + P[b * d + a]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double q = 0.0;
+      for (int a = 0; a < d; ++a) q = fma(mr[a] - zs[a], pm[a], q);
       p.bias[r] = d * kLog2PiE + p.c[r] + q;
-      int e = 0;
-      for (int a = 0; a < d; ++a)
-        for (int b = a; b < d; ++b, ++e)
-          p.W[(size_t)e * KS + r] = (a == b) ? P[a * d + a] : 0.5 * (P[a * d + b] + P[b * d + a]);
-    } else {
-      const double *P = p.P + (size_t)r * d;
+    }
+  } else {
+    const double *P = p.P + (size_t)r * d;
+    for (int a = tid; a < d; a += kPrepThreads) {
+      const double ma = mr[a] - zs[a];
+      p.W[(size_t)a * KS + r] = P[a];
+      p.W[(size_t)(d + a) * KS + r] = -2.0 * P[a] * ma;
+    }
+    if (tid == 0) {
       double q = 0.0;
       for (int a = 0; a < d; ++a) {
         const double ma = mr[a] - zs[a];
         q = fma(P[a] * ma, ma, q);
-        p.W[(size_t)a * KS + r] = P[a];
-        p.W[(size_t)(d + a) * KS + r] = -2.0 * P[a] * ma;
       }
       p.bias[r] = d * kLog2PiE + p.c[r] + q;
     }
@@ -303,7 +313,7 @@ bool plan_emission(EmissionArgs &a, size_t &lds) {
 }
 
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st) {
-  hipLaunchKernelGGL(emission_prep_kernel, dim3(1), dim3(kEmThreads), 0, st, a);
+  hipLaunchKernelGGL(emission_prep_kernel, dim3(a.K * a.S), dim3(kPrepThreads), 0, st, a);
   return hipGetLastError();
 }
 
