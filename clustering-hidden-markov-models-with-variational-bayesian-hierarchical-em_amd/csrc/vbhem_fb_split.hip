@@ -224,7 +224,8 @@ void fb_split_kernel(const SplitArgs p) {
 
   // ---------------- one pair per LPP lanes: (ic, j) --------------------------------------------
   // pair n0 + q of the item: base i = lst ? lst[n0 + q] : n0 + q, active while n0 + q < lim
-  auto run_pair = [&](int j, int n0, int lim, const int *lst) {
+  // (ipre >= 0: the base index, already loaded by the caller)
+  auto run_pair = [&](int j, int n0, int lim, const int *lst, int ipre) {
     // lane geometry recomputed from an opaque copy of the thread id: in the list
     // mode's item loop this keeps LICM from hoisting every lane-invariant address
     // out of the loop (which costs ~90 VGPRs of live ranges)
@@ -247,7 +248,7 @@ void fb_split_kernel(const SplitArgs p) {
     double *X = lds + LY::OFF_X + (valid ? q : 0) * LY::XP;   // slab [col][XCS]
     double *Y = lds + pa.off_Y + (valid ? q : 0) * S;
     const bool active = valid && n0 + q < lim;
-    const int i = active ? (lst ? lst[n0 + q] : n0 + q) : pa.i_begin;
+    const int i = active ? (ipre >= 0 ? ipre : lst ? lst[n0 + q] : n0 + q) : pa.i_begin;
     const int ic = i;
     const size_t lp = (size_t)(ic - pa.i_buf0) * K + j;
     if (valid && w == 0) F[q] = 0;  // read back only after this pair's later syncs
@@ -571,7 +572,7 @@ void fb_split_kernel(const SplitArgs p) {
   if constexpr (MODE == kFbDense) {
     const int j = blockIdx.x % K;
     stage_cluster(j);
-    run_pair(j, p.i_begin + (int)(blockIdx.x / K) * PPB, p.i_end, nullptr);
+    run_pair(j, p.i_begin + (int)(blockIdx.x / K) * PPB, p.i_end, nullptr, -1);
   } else if constexpr (MODE == kFbBackward) {
     // persistent: NB blocks per cluster, each keeps its cluster and strides over the
     // tiles.  XCD-aware when NB % 8 == 0: workgroups are dealt round-robin to the 8
@@ -592,7 +593,7 @@ void fb_split_kernel(const SplitArgs p) {
     stage_cluster(j);  // (its barriers also publish the table)
     const int ntile = (p.i_end - p.i_begin + PPB - 1) / PPB;
     for (int tile = t0; tile < ntile; tile += NB)
-      run_pair(j, p.i_begin + tile * PPB, p.i_end, nullptr);
+      run_pair(j, p.i_begin + tile * PPB, p.i_end, nullptr, -1);
   } else {
     // work items: cluster j owns ceil(list_tot[j] / PPB) consecutive items
     int *pre = reinterpret_cast<int *>(lds + p.off_L);  // [K + 1]
@@ -608,18 +609,29 @@ void fb_split_kernel(const SplitArgs p) {
     const int nitem = __builtin_amdgcn_readfirstlane(pre[K]);  // block-uniform: keep in SGPRs
     const int per = (nitem + (int)gridDim.x - 1) / (int)gridDim.x;
     const int w0 = (int)blockIdx.x * per, w1 = min(nitem, w0 + per);
-    int jcur = -1;
-    for (int wi = w0; wi < w1; ++wi) {
-      int jj = jcur < 0 ? 0 : jcur;
+    // the item's cluster (block-uniform) and this lane's base, -1 past the list's end
+    const int q = tid / LPP;
+    auto item = [&](int wi, int jfrom, int &jj) -> int {
+      jj = jfrom;
       while (pre[jj + 1] <= wi) ++jj;
       jj = __builtin_amdgcn_readfirstlane(jj);
+      const int n = (wi - pre[jj]) * PPB + q;
+      return (q < PPB && n < p.list_tot[jj]) ? p.list[(size_t)jj * p.list_cap + n] : -1;
+    };
+    int jn = 0;
+    int inext = w0 < w1 ? item(w0, 0, jn) : -1;
+    int jcur = -1;
+    for (int wi = w0; wi < w1; ++wi) {
+      const int jj = jn;
+      const int icur = inext;
+      if (wi + 1 < w1) inext = item(wi + 1, jj, jn);  // next item's base: in flight now
       __syncthreads();  // previous item's LDS traffic (slabs, lattice, parked H) done
       if (jj != jcur) {
         stage_cluster(jj);
         jcur = jj;
       }
       const int tot = __builtin_amdgcn_readfirstlane(p.list_tot[jj]);
-      run_pair(jj, (wi - pre[jj]) * PPB, tot, p.list + (size_t)jj * p.list_cap);
+      run_pair(jj, (wi - pre[jj]) * PPB, tot, nullptr, icur);
     }
   }
 }
