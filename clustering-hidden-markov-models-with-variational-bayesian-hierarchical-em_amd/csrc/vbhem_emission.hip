@@ -113,6 +113,7 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
 // chunks of 8 row tiles (32 fp64 accumulators per lane).
 // ---------------------------------------------------------------------------
 constexpr int kEmRowChunk = 8;
+constexpr int kEmMaxKQ = 11;  // RAW path: KD <= 44 (d <= 8 full)
 // doubles per wave: 16 cols x (d*d <= 64, d <= 8), rows padded to an odd stride
 // (dd + 1, d + 1) so the 16 lanes of a k-group read 16 different bank pairs
 constexpr int kEmRawSlot = 16 * 65 + 16 * 9;
@@ -228,6 +229,25 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p)
       if (ct + wstride < nctile) prefetch(ct + wstride);  // next tile, overlaps the MFMAs
     }
     const size_t cbuf = (size_t)(p.i_begin - p.i_buf0) * SB + col;
+    // RAW: the whole B operand of the tile (this lane's k-rows 4t + kl of column cl)
+    // built once into registers, so the k-loop is W reads + MFMAs only
+    double ub[kEmMaxKQ];
+    if (RAW) {
+#pragma unroll
+      for (int t = 0; t < kEmMaxKQ; ++t) {
+        const int e = 4 * t + kl;
+        double u = 0.0;
+        if (t < KQ && e < KD) {
+          const int tb = tab[e];
+          const int oA = tb & 127, oB = (tb >> 7) & 127, a = (tb >> 14) & 15, b = (tb >> 18) & 15;
+          const double f = (double)((tb >> 22) & 3), g = (double)((tb >> 24) & 1);
+          const double ma = mus[cl * ds + a], mb = mus[cl * ds + b];
+          const double caa = rawc[cl * dds + oA] + rawc[cl * dds + oB];
+          u = cv ? fma(f * ma, mb, fma(g, ma, caa)) : 0.0;
+        }
+        ub[t] = u;
+      }
+    }
     for (int r0 = 0; r0 < RT; r0 += kEmRowChunk) {
       double4_t acc[kEmRowChunk];
 #pragma unroll
@@ -244,36 +264,39 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p)
         }
       };
       loadw(0, wc);
-      for (int t = 0; t < KQ; ++t) {
-        if (t + 1 < KQ) loadw(t + 1, wn);
-        const int e = 4 * t + kl;
-        double u = 0.0;
-        if (e < KD) {
-          const int tb = tab[e];
-          double ma, mb, caa;
-          if (RAW) {
-            const int oA = tb & 127, oB = (tb >> 7) & 127, a = (tb >> 14) & 15,
-                      b = (tb >> 18) & 15;
-            const double f = (double)((tb >> 22) & 3), g = (double)((tb >> 24) & 1);
-            ma = mus[cl * ds + a];
-            mb = mus[cl * ds + b];
-            caa = rawc[cl * dds + oA] + rawc[cl * dds + oB];
-            u = fma(f * ma, mb, fma(g, ma, caa));
-          } else {
+      if (RAW) {
+#pragma unroll
+        for (int t = 0; t < kEmMaxKQ; ++t) {
+          if (t < KQ) {
+            if (t + 1 < KQ) loadw(t + 1, wn);
+#pragma unroll
+            for (int q = 0; q < kEmRowChunk; ++q)
+              if (r0 + q < RT)
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], ub[t], acc[q], 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
+          }
+        }
+      } else {
+        for (int t = 0; t < KQ; ++t) {
+          if (t + 1 < KQ) loadw(t + 1, wn);
+          const int e = 4 * t + kl;
+          double u = 0.0;
+          if (e < KD) {
+            const int tb = tab[e];
             const int a = tb & 0xff, b = (tb >> 8) & 0xff, kind = tb >> 16;
-            ma = Mg[a] - p.shift[a];
-            mb = Mg[b] - p.shift[b];
-            caa = kind <= 1 ? Cg[a * d + b] : (kind == 2 ? Cg[a] : 0.0);
+            const double ma = Mg[a] - p.shift[a], mb = Mg[b] - p.shift[b];
+            double caa = kind <= 1 ? Cg[a * d + b] : (kind == 2 ? Cg[a] : 0.0);
             if (kind == 1) caa += Cg[b * d + a];
             u = kind == 3 ? ma : (kind == 1 ? fma(2.0 * ma, mb, caa) : fma(ma, ma, caa));
+            u = cv ? u : 0.0;
           }
-          u = cv ? u : 0.0;
+#pragma unroll
+          for (int q = 0; q < kEmRowChunk; ++q)
+            if (r0 + q < RT) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], u, acc[q], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
         }
-#pragma unroll
-        for (int q = 0; q < kEmRowChunk; ++q)
-          if (r0 + q < RT) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], u, acc[q], 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
       }
       if (cv) {
 #pragma unroll
