@@ -38,6 +38,11 @@ EXPORTS = {
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "vbhem_estep_pairs_host": (_c_int, [_c_int, ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
                                         _vp, _vp, _vp, _vp, _vp, _vp]),
+    "vhem_estep_pairs": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
+                                  ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _c_size, _vp]),
+    "vhem_estep_pairs_host": (_c_int, [_c_int, ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT),
+                                       _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp]),
     "vbhem_stats_nu": (_c_size, [_c_int, _c_int]),
     "vbhem_stats_len": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "vbhem_fused_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int]),

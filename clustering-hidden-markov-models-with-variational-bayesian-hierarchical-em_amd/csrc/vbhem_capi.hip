@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -291,7 +292,8 @@ struct FbCtx {
   size_t em_lds = 0;
 };
 
-int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T) {
+int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T,
+               double smooth = 1.0) {
   c.split = plan_split(b->SB, b->d, b->covmode, cl->K, cl->S, T, vbhem::split_lpc(cl->S));
   // backward-only pass: half the lanes per column (no forward-sweep registers to
   // hold), more rows per lane: no DPP for S <= 8, more independent exp/log chains
@@ -299,6 +301,7 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
   if (c.split.ok) {
     vbhem::EmissionArgs &e = c.em;
     e.SB = b->SB; e.d = b->d; e.covmode = b->covmode; e.K = cl->K; e.S = cl->S;
+    e.smooth = smooth;
     e.centres = b->centres; e.covars = b->covars; e.m = cl->m; e.P = cl->P; e.c = cl->c;
     if (!vbhem::plan_emission(e, c.em_lds)) c.split.ok = false;
   }
@@ -312,6 +315,7 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
   // fields the exact fallback kernel needs even when the generic plan is unused
   c.plan.a.SB = b->SB; c.plan.a.d = b->d; c.plan.a.covmode = b->covmode;
   c.plan.a.K = cl->K; c.plan.a.S = cl->S; c.plan.a.T = T;
+  c.plan.a.smooth = smooth;
   if (c.split.ok) {
     vbhem::SplitArgs &a = c.split.a;
     a.prior = b->prior; a.A = b->A; a.logA = cl->logA; a.logPi = cl->logPi;
@@ -451,11 +455,17 @@ size_t vbhem_pairs_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster
   return carve_pairs(nullptr, base, clus, T, true, w);
 }
 
-int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
-                      double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
-                      double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
-                      double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
-                      void *stream) {
+}  // extern "C"
+
+namespace {
+
+int estep_pairs_impl(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T, double smooth,
+                     double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
+                     double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
+                     double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
+                     void *stream) {
+  if (!(smooth > 0.0) || !std::isfinite(smooth))
+    return fail(VBHEM_ERR_ARG, "smooth must be a positive finite number");
   int rc = check_inputs(base, clus, T);
   if (rc != VBHEM_OK) return rc;
   if (base->N == 0) return VBHEM_OK;
@@ -469,7 +479,7 @@ int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   double *tnu = sum_t_nu_dev ? sum_t_nu_dev : w.tnu;
   hipStream_t st = static_cast<hipStream_t>(stream);
   FbCtx ctx;
-  rc = prepare_fb(ctx, base, clus, T);
+  rc = prepare_fb(ctx, base, clus, T, smooth);
   if (rc != VBHEM_OK) return rc;
   hipError_t e0 = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
   if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
@@ -487,6 +497,30 @@ int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   hipError_t e = vbhem::launch_emit(ea, st);
   if (e != hipSuccess) return hip_fail(e, "pair_emit_kernel");
   return VBHEM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vbhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
+                      double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
+                      double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
+                      void *stream) {
+  return estep_pairs_impl(base, clus, T, 1.0, LL_elbo_dev, sum_nu_1_dev, emit_pr_dev, emit_mu_dev,
+                          emit_Mu_dev, sum_xi_dev, sum_t_nu_dev, workspace_dev, workspace_bytes,
+                          stream);
+}
+
+int vhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T, double smooth,
+                     double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
+                     double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
+                     double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
+                     void *stream) {
+  return estep_pairs_impl(base, clus, T, smooth, LL_elbo_dev, sum_nu_1_dev, emit_pr_dev,
+                          emit_mu_dev, emit_Mu_dev, sum_xi_dev, sum_t_nu_dev, workspace_dev,
+                          workspace_bytes, stream);
 }
 
 size_t vbhem_fused_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T) {
@@ -681,9 +715,13 @@ int vbhem_last_fallback_count(void *stream, const void *workspace_dev) {
   return std::max(v[0], v[1]);
 }
 
-int vbhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_cluster_t *ch, int T,
-                           double *LL_elbo, double *sum_nu_1, double *emit_pr, double *emit_mu,
-                           double *emit_Mu, double *sum_xi) {
+}  // extern "C"
+
+namespace {
+
+int estep_pairs_host_impl(int device, const vbhem_base_t *bh, const vbhem_cluster_t *ch, int T,
+                          double smooth, double *LL_elbo, double *sum_nu_1, double *emit_pr,
+                          double *emit_mu, double *emit_Mu, double *sum_xi) {
   int rc = check_inputs(bh, ch, T);
   if (rc != VBHEM_OK) return rc;
   if (bh->N == 0) return VBHEM_OK;
@@ -722,8 +760,8 @@ int vbhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_clust
     if (e != hipSuccess) rc = hip_fail(e, "hipMalloc(workspace)");
   }
   if (rc == VBHEM_OK)
-    rc = vbhem_estep_pairs(&bd, &cd, T, d_out[0], d_out[1], d_out[2], d_out[3], d_out[4], d_out[5],
-                           nullptr, ws, wsb, nullptr);
+    rc = estep_pairs_impl(&bd, &cd, T, smooth, d_out[0], d_out[1], d_out[2], d_out[3], d_out[4],
+                          d_out[5], nullptr, ws, wsb, nullptr);
   if (rc == VBHEM_OK) {
     e = hipDeviceSynchronize();
     if (e != hipSuccess) rc = hip_fail(e, "kernel execution");
@@ -736,6 +774,24 @@ int vbhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_clust
   for (int k = 0; k < 6; ++k) if (d_out[k]) (void)hipFree(d_out[k]);
   if (ws) (void)hipFree(ws);
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vbhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_cluster_t *ch, int T,
+                           double *LL_elbo, double *sum_nu_1, double *emit_pr, double *emit_mu,
+                           double *emit_Mu, double *sum_xi) {
+  return estep_pairs_host_impl(device, bh, ch, T, 1.0, LL_elbo, sum_nu_1, emit_pr, emit_mu,
+                               emit_Mu, sum_xi);
+}
+
+int vhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_cluster_t *ch, int T,
+                          double smooth, double *LL_elbo, double *sum_nu_1, double *emit_pr,
+                          double *emit_mu, double *emit_Mu, double *sum_xi) {
+  return estep_pairs_host_impl(device, bh, ch, T, smooth, LL_elbo, sum_nu_1, emit_pr, emit_mu,
+                               emit_Mu, sum_xi);
 }
 
 }  // extern "C"

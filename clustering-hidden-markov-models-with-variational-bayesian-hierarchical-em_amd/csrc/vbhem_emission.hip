@@ -306,7 +306,10 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p)
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
               const int row = rt * 16 + kl + 4 * v;
-              if (row < KS) p.E[(size_t)row * ldE + cbuf] = -0.5 * (p.bias[row] + acc[q][v]);
+              if (row < KS) {
+                const double ev = -0.5 * (p.bias[row] + acc[q][v]);
+                p.E[(size_t)row * ldE + cbuf] = p.smooth != 1.0 ? ev / p.smooth : ev;
+              }
             }
           }
         }

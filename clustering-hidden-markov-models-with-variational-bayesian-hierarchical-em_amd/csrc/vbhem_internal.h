@@ -24,6 +24,7 @@ struct FbArgs {
   int off_At, off_amax, off_lpi, off_Ab, off_pib, off_flag, off_reg;
   int off_k1m, off_k1P, off_k1c, off_k1mu, off_k1C;
   int pair_stride;
+  double smooth;  // E /= smooth when != 1 (VHEM sibling, hem_hmm_bwd_fwd_mex.c:848-860)
 };
 
 struct EmitArgs {
@@ -81,6 +82,7 @@ struct EmissionArgs {
   const double *centres, *covars, *m, *P, *c;
   double *W, *bias, *shift;  // [KD][K*S], [K*S], [d] (emission_prep_kernel)
   double *E;                 // [K*S][(i - i_buf0) * SB + b]  (row stride e_ld)
+  double smooth;             // E /= smooth when != 1 (VHEM sibling)
 };
 bool plan_emission(EmissionArgs &a, size_t &lds);
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st);

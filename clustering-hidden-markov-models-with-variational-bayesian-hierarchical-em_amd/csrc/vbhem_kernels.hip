@@ -218,6 +218,7 @@ __global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
       E = emission_full<D>(d, k1m + cs * MS, k1P + cs * PS, k1c[cs], k1mu + bs * MS, k1C + bs * PS);
     else
       E = emission_diag<D>(d, k1m + cs * MS, k1P + cs * PS, k1c[cs], k1mu + bs * MS, k1C + bs * PS);
+    if (p.smooth != 1.0) E = E / p.smooth;
   }
   __syncthreads();  // K1 staging region is reused below
 
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(64) void fb_exact_kernel(const FbArgs p, double *sc
             ell += P[r] * (x * x);
           }
         }
-        E[s * SB + be] = -0.5 * ell;
+        E[s * SB + be] = p.smooth != 1.0 ? (-0.5 * ell) / p.smooth : -0.5 * ell;
         L[s * SB + be] = 0.0;
       }
     for (int t = T - 1; t >= 1; --t) {

@@ -79,8 +79,11 @@ class EStepEngine:
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     # -- MEX-equivalent per-pair outputs ------------------------------------
-    def pairs(self, want_tnu: bool = False) -> dict:
-        """LL_elbo, sum_nu_1, emit_pr, emit_mu, emit_Mu, sum_xi (+ sum_t_nu), [N][K][...]."""
+    def pairs(self, want_tnu: bool = False, smooth=None) -> dict:
+        """LL_elbo, sum_nu_1, emit_pr, emit_mu, emit_Mu, sum_xi (+ sum_t_nu), [N][K][...].
+
+        smooth: None = vbhem_hmm_bwd_fwd_mex; a number = the VHEM sibling
+        hem_hmm_bwd_fwd_mex (cluster constants from host.vhem_cluster_constants)."""
         N, K, S, d, SB = self.N, self.K, self.S, self.base.d, self.base.SB
         dv = self.device
         dC = (d, d) if self.base.covmode == COV_FULL else (d,)
@@ -96,13 +99,18 @@ class EStepEngine:
             nb = int(self.lib.vbhem_pairs_workspace_bytes(ctypes.byref(self._bt),
                                                           ctypes.byref(self._ct), self.T))
             self._ws_pairs = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dv)
-        rc = self.lib.vbhem_estep_pairs(
-            ctypes.byref(self._bt), ctypes.byref(self._ct), self.T,
-            _capi.ptr(out["LL_elbo"]), _capi.ptr(out["sum_nu_1"]), _capi.ptr(out["emit_pr"]),
-            _capi.ptr(out["emit_mu"]), _capi.ptr(out["emit_Mu"]), _capi.ptr(out["sum_xi"]),
-            _capi.ptr(out.get("sum_t_nu")), _capi.ptr(self._ws_pairs),
-            self._ws_pairs.numel(), self._stream())
-        _capi.check(rc, "vbhem_estep_pairs")
+        outs = (_capi.ptr(out["LL_elbo"]), _capi.ptr(out["sum_nu_1"]), _capi.ptr(out["emit_pr"]),
+                _capi.ptr(out["emit_mu"]), _capi.ptr(out["emit_Mu"]), _capi.ptr(out["sum_xi"]),
+                _capi.ptr(out.get("sum_t_nu")), _capi.ptr(self._ws_pairs), self._ws_pairs.numel(),
+                self._stream())
+        if smooth is None:
+            rc = self.lib.vbhem_estep_pairs(ctypes.byref(self._bt), ctypes.byref(self._ct), self.T,
+                                            *outs)
+            _capi.check(rc, "vbhem_estep_pairs")
+        else:
+            rc = self.lib.vhem_estep_pairs(ctypes.byref(self._bt), ctypes.byref(self._ct), self.T,
+                                           float(smooth), *outs)
+            _capi.check(rc, "vhem_estep_pairs")
         return out
 
     # -- fused E-step --------------------------------------------------------

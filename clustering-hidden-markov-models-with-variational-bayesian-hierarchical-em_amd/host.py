@@ -43,6 +43,27 @@ def cluster_constants(post: Posterior, covmode: int) -> dict:
                 m=np.ascontiguousarray(post.m), P=np.ascontiguousarray(P))
 
 
+def vhem_cluster_constants(red: dict, covmode: int) -> dict:
+    """E-step constants of the VHEM sibling (hem_hmm_bwd_fwd_mex.c) from point-estimate
+    reduced HMMs red = {A [K][S][S], prior [K][S], centres [K][S][d], covars [K][S][d,d]|[K][S][d]}:
+    logA = log(A) (:906-922), logPi = log(prior) (:1004-1019), m = centres, and
+    full: P = inv(covars), c = log(det(covars))  (hem_h3m_c_step.m:198-205);
+    diag: P = 1 ./ covars, c = sum(log(covars))  (hem_hmm_bwd_fwd_mex.c:711-733)."""
+    A = np.asarray(red["A"], dtype=np.float64)
+    prior = np.asarray(red["prior"], dtype=np.float64)
+    cov = np.asarray(red["covars"], dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        logA, logPi = np.log(A), np.log(prior)
+    if covmode == COV_FULL:
+        P = np.linalg.inv(cov)
+        c = np.log(np.linalg.det(cov))
+    else:
+        P = 1.0 / cov
+        c = np.log(cov).sum(-1)
+    return dict(logA=logA, logPi=logPi, m=np.asarray(red["centres"], dtype=np.float64).copy(),
+                P=P, c=c)
+
+
 def log_omega_tilde(alpha: np.ndarray) -> np.ndarray:
     return digamma(alpha) - digamma(alpha.sum())
 

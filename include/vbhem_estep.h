@@ -87,6 +87,26 @@ int vbhem_estep_pairs_host(int device, const vbhem_base_t *base_host,
                            double *sum_nu_1, double *emit_pr, double *emit_mu,
                            double *emit_Mu, double *sum_xi);
 
+/* VHEM sibling: replaces src/compare_mtds/hem/vhem_h3m/hem_hmm_bwd_fwd_mex.c
+ * (called at hem_h3m_c_step.m:191-192 / :208-209).  The same recursions on
+ * point-estimate reduced HMMs, with the expected emission log-likelihood
+ * divided by `smooth` (hem_hmm_bwd_fwd_mex.c:848-860; smooth > 0).  The cluster
+ * descriptor then carries (hem_hmm_bwd_fwd_mex.c:565-600, 906-922, 1004-1019):
+ *   logA  = log(hmm_r.A)            logPi = log(hmm_r.prior)
+ *   m     = emit{k}.centres
+ *   P     = inv(emit{k}.covars) = invCovR      | 1 ./ covars (diag)
+ *   c     = log(det(emit{k}.covars)) = logdetCovR | sum(log(covars)) (diag)
+ * Workspace: vbhem_pairs_workspace_bytes.  Outputs as vbhem_estep_pairs. */
+int vhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T, double smooth,
+                     double *LL_elbo_dev, double *sum_nu_1_dev, double *emit_pr_dev,
+                     double *emit_mu_dev, double *emit_Mu_dev, double *sum_xi_dev,
+                     double *sum_t_nu_dev, void *workspace_dev, size_t workspace_bytes,
+                     void *stream);
+int vhem_estep_pairs_host(int device, const vbhem_base_t *base_host,
+                          const vbhem_cluster_t *clus_host, int T, double smooth,
+                          double *LL_elbo, double *sum_nu_1, double *emit_pr, double *emit_mu,
+                          double *emit_Mu, double *sum_xi);
+
 /* Fused E-step for one EM iteration on this device's shard of base HMMs:
  *   pairs (mex.c) -> responsibilities (step_fc.m:271-283) -> gated, Z-weighted
  *   statistic sums (vbhem_compute_Statistics.m:33-55) -> ELBO partials

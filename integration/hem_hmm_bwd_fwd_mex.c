@@ -1,68 +1,66 @@
 /*
- * integration/vbhem_hmm_bwd_fwd_mex.c -- MATLAB MEX gateway that replaces the
- * reference's src/vbhem/vbhem_hmm_bwd_fwd_mex.c with a call into the MI355X
- * E-step (libvbhem_estep.so, include/vbhem_estep.h).
+ * integration/hem_hmm_bwd_fwd_mex.c -- MATLAB MEX gateway that replaces the
+ * reference's VHEM sibling src/compare_mtds/hem/vhem_h3m/hem_hmm_bwd_fwd_mex.c
+ * with a call into the MI355X E-step (vhem_estep_pairs_host, include/vbhem_estep.h).
  *
  * Same MATLAB signature, argument checks, error identifiers and output shapes
- * as the reference gateway (mex.c:288-409, output cells mex.c:1108-1122,
- * 1312-1345):
+ * as the reference gateway (hem_hmm_bwd_fwd_mex.c:288-409):
  *
  *   [LL_elbo, sum_nu_1, update_emit_pr, update_emit_mu, update_emit_Mu, sum_xi] =
- *       vbhem_hmm_bwd_fwd_mex(h3m_b.hmm, h3m_r.hmm, T, maxN, maxN2
- *                             [, logdetCovPlusDdivlamR, invCovR])
+ *       hem_hmm_bwd_fwd_mex(h3m_b.hmm, h3m_r.hmm, T, smooth, maxN, maxN2
+ *                           [, logdetCovR, invCovR])
  *
- * 5 inputs = diagonal covariances, 7 inputs = full (mex.c:335-346).  The
- * gateway only repacks MATLAB's column-major cell/struct data into the dense
- * row-major arrays of vbhem_base_t / vbhem_cluster_t, calls
- * vbhem_estep_pairs_host(), and scatters the results back into MATLAB cells.
- *
- * Emission constants, as the reference kernel reads them:
- *   full: c = logdetCovPlusDdivlamR{j}(rho), P = invCovR{j}(:,:,rho)   (mex.c:785-830)
- *   diag: c = emit{rho}.logLambdaTildePlusDdivlamda, P = emit{rho}.v * emit{rho}.W
- *                                                                        (mex.c:718-760)
- * The GPU device is taken from the environment variable VBHEM_DEVICE (default 0).
- *
- * Build (MATLAB):  mex -R2017b -I../include vbhem_hmm_bwd_fwd_mex.c -L../lib -lvbhem_estep
- * (see INTEGRATION.md).  In this repository the file is also built against a
- * test double of the mx API (tests/mxshim) so the gateway itself is tested.
+ * 6 inputs = diagonal covariances, 8 inputs = full (:334-346), called from
+ * hem_h3m_c_step.m:191-192 / :208-209.  The reduced HMMs are point estimates
+ * {A, prior, emit{k}.centres, emit{k}.covars}; the gateway turns them into the
+ * cluster constants the kernels read:
+ *   logA = log(A) (:906-922), logPi = log(prior) (:1004-1019), m = centres,
+ *   full: c = logdetCovR{j}(k), P = invCovR{j}(:,:,k)  (:585-600)
+ *   diag: c = sum(log(covars)), P = 1 ./ covars        (:711-733)
+ * and the kernels divide the expected emission log-likelihood by `smooth`
+ * (:848-860).  The GPU device is taken from VBHEM_DEVICE (default 0).
  */
+#include <math.h>
+
 #include "h3m_mex_common.h"
 
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
-  if ((nrhs != 5) && (nrhs != 7))
-    mexErrMsgIdAndTxt("MyToolbox:arrayProduct:nrhs", "5 or 7 inputs required.");
+  if ((nrhs != 6) && (nrhs != 8))
+    mexErrMsgIdAndTxt("MyToolbox:arrayProduct:nrhs", "4 or 6 inputs required.");
   if (nlhs != 6) mexErrMsgIdAndTxt("MyToolbox:arrayProduct:nlhs", "6 output required.");
-  const int covmode = (nrhs == 7) ? VBHEM_COV_FULL : VBHEM_COV_DIAG;
-  if (!mxIsCell(prhs[0])) mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "1st arg must be cell");
-  if (!mxIsCell(prhs[1])) mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "2nd arg must be cell");
+  const int covmode = (nrhs == 8) ? VBHEM_COV_FULL : VBHEM_COV_DIAG;
+  if (!mxIsCell(prhs[0])) mexErrMsgIdAndTxt("vbhmm_fb_mex:invalidinput", "1st arg must be cell");
+  if (!mxIsCell(prhs[1])) mexErrMsgIdAndTxt("vbhmm_fb_mex:invalidinput", "2nd arg must be cell");
   const mxArray *h3m_b = prhs[0], *h3m_r = prhs[1];
   const int Kr = (int)mxGetNumberOfElements(h3m_r);
   const int Kb = (int)mxGetNumberOfElements(h3m_b);
   const int T = (int)parse_scalar(prhs[2]);
-  const int maxN = (int)parse_scalar(prhs[3]);
-  const int maxN2 = (int)parse_scalar(prhs[4]);
+  const double smooth = parse_scalar(prhs[3]);
+  const int maxN = (int)parse_scalar(prhs[4]);
+  const int maxN2 = (int)parse_scalar(prhs[5]);
   const mxArray *logdetR = NULL, *invCovR = NULL;
   if (covmode == VBHEM_COV_FULL) {
-    logdetR = prhs[5];
-    invCovR = prhs[6];
+    logdetR = prhs[6];
+    invCovR = prhs[7];
     if (!mxIsCell(logdetR) || (int)mxGetNumberOfElements(logdetR) != Kr)
-      mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "6th arg must be a cell {1xKr}");
-    if (!mxIsCell(invCovR) || (int)mxGetNumberOfElements(invCovR) != Kr)
       mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "7th arg must be a cell {1xKr}");
+    if (!mxIsCell(invCovR) || (int)mxGetNumberOfElements(invCovR) != Kr)
+      mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "8th arg must be a cell {1xKr}");
   }
-  if (Kr < 1 || Kb < 0 || T < 1 || maxN < 1 || maxN2 < 1)
-    mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "invalid sizes (Kr=%d Kb=%d T=%d maxN=%d maxN2=%d)",
-                      Kr, Kb, T, maxN, maxN2);
+  if (Kr < 1 || Kb < 0 || T < 1 || maxN < 1 || maxN2 < 1 || !(smooth > 0.0))
+    mexErrMsgIdAndTxt("vbhem_mex:invalidinput",
+                      "invalid sizes (Kr=%d Kb=%d T=%d maxN=%d maxN2=%d smooth=%g)", Kr, Kb, T,
+                      maxN, maxN2, smooth);
 
-  /* ---- cluster HMMs (mex.c:433-457): all clusters must have maxN2 states -------- */
+  /* ---- reduced HMMs (:428-447): all clusters must have maxN2 states ----------------- */
   int d = -1;
   {
     const mxArray *hr = mxGetCell(h3m_r, 0);
     const mxArray *e = hr ? mxGetField(hr, 0, "emit") : NULL;
     const mxArray *e0 = e ? mxGetCell(e, 0) : NULL;
-    const mxArray *m0 = e0 ? mxGetField(e0, 0, "m") : NULL;
-    if (!m0) mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{1}.emit{1}.m missing");
-    d = (int)mxGetN(m0);
+    const mxArray *c0 = e0 ? mxGetField(e0, 0, "centres") : NULL;
+    if (!c0) mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{1}.emit{1}.centres missing");
+    d = (int)mxGetNumberOfElements(c0);
   }
   const int S = maxN2, SB = maxN;
   const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
@@ -79,17 +77,17 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
       free_buffers(&b);
       mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d} must be a struct", j + 1);
     }
-    const mxArray *lA = mxGetField(hr, 0, "logATilde");
-    if (!lA || (int)mxGetM(lA) != S || (int)mxGetN(lA) != S) {
+    const mxArray *mA = mxGetField(hr, 0, "A");
+    if (!mA || (int)mxGetM(mA) != S || (int)mxGetN(mA) != S) {
       free_buffers(&b);
       mexErrMsgIdAndTxt("vbhem_mex:unsupported",
-                        "h3m_r{%d}.logATilde must be maxN2 x maxN2 (all clusters equal size)", j + 1);
+                        "h3m_r{%d}.A must be maxN2 x maxN2 (all clusters equal size)", j + 1);
     }
-    const double *pA = mxGetPr(lA);
-    const double *pPi = field_pr(hr, "logPiTilde", (size_t)S, "h3m_r");
+    const double *pA = mxGetPr(mA);
+    const double *pPi = field_pr(hr, "prior", (size_t)S, "h3m_r");
     for (int r = 0; r < S; r++) {
-      b.logPi[(size_t)j * S + r] = pPi[r];
-      for (int s = 0; s < S; s++) b.logA[((size_t)j * S + r) * S + s] = pA[r + (size_t)s * S];
+      b.logPi[(size_t)j * S + r] = log(pPi[r]);
+      for (int s = 0; s < S; s++) b.logA[((size_t)j * S + r) * S + s] = log(pA[r + (size_t)s * S]);
     }
     const mxArray *emit = mxGetField(hr, 0, "emit");
     const double *ldet = NULL, *icov = NULL;
@@ -99,7 +97,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
           mxGetNumberOfElements(ic) != (size_t)S * d * d) {
         free_buffers(&b);
         mexErrMsgIdAndTxt("vbhem_mex:invalidinput",
-                          "logdetCovPlusDdivlamR{%d} / invCovR{%d} have wrong sizes", j + 1, j + 1);
+                          "logdetCovR{%d} / invCovR{%d} have wrong sizes", j + 1, j + 1);
       }
       ldet = mxGetPr(lc);
       icov = mxGetPr(ic);
@@ -110,21 +108,23 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
         free_buffers(&b);
         mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d}.emit{%d} missing", j + 1, s + 1);
       }
-      const double *pm = field_pr(es, "m", (size_t)d, "h3m_r emit");
+      const double *pm = field_pr(es, "centres", (size_t)d, "h3m_r emit");
       double *dm = b.m + ((size_t)j * S + s) * d;
       for (int a = 0; a < d; a++) dm[a] = pm[a];
       double *dP = b.P + ((size_t)j * S + s) * dd;
       if (covmode == VBHEM_COV_FULL) {
         b.c[(size_t)j * S + s] = ldet[s];
-        /* invCovR{j}(a,b,s) at a + b*d + s*d*d (column-major) */
         for (int a = 0; a < d; a++)
           for (int c2 = 0; c2 < d; c2++)
             dP[(size_t)a * d + c2] = icov[a + (size_t)c2 * d + (size_t)s * d * d];
       } else {
-        const double *pW = field_pr(es, "W", (size_t)d, "h3m_r emit");
-        const double v = field_pr(es, "v", 1, "h3m_r emit")[0];
-        b.c[(size_t)j * S + s] = field_pr(es, "logLambdaTildePlusDdivlamda", 1, "h3m_r emit")[0];
-        for (int a = 0; a < d; a++) dP[a] = v * pW[a];
+        const double *pv = field_pr(es, "covars", (size_t)d, "h3m_r emit");
+        double lsum = 0.0;
+        for (int a = 0; a < d; a++) {
+          lsum += log(pv[a]);
+          dP[a] = 1.0 / pv[a];
+        }
+        b.c[(size_t)j * S + s] = lsum;
       }
     }
   }
@@ -144,11 +144,11 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     vbhem_cluster_t clus = {Kr, S, b.logA, b.logPi, b.m, b.P, b.c};
     const char *dev_env = getenv("VBHEM_DEVICE");
     const int device = dev_env ? atoi(dev_env) : 0;
-    const int st = vbhem_estep_pairs_host(device, &base, &clus, T, b.LL, b.nu1, b.pr, b.mu, b.Mu,
-                                          b.xi);
+    const int st = vhem_estep_pairs_host(device, &base, &clus, T, smooth, b.LL, b.nu1, b.pr, b.mu,
+                                         b.Mu, b.xi);
     if (st != VBHEM_OK) {
       free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:gpu", "vbhem_estep_pairs_host failed (%d): %s", st,
+      mexErrMsgIdAndTxt("vbhem_mex:gpu", "vhem_estep_pairs_host failed (%d): %s", st,
                         vbhem_last_error());
     }
   }

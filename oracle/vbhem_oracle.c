@@ -55,6 +55,8 @@ typedef struct {
 typedef struct {
   int K, S;
   const double *logA, *logPi, *m, *P, *c;
+  double smooth;           /* E /= smooth when != 1 (VHEM, hem mex.c:848-860)        */
+  const double *vcov;      /* VHEM diag: [K][S][d] covars of the reduced HMMs, or NULL */
 } oracle_cluster;
 
 /* column log-sum-exp: max first, then sum of exp(x - max) in index order
@@ -76,6 +78,21 @@ static double emission_term(const oracle_base *b, const oracle_cluster *r,
   const int d = b->d;
   const double *mu = b->centres + ((size_t)i * b->SB + beta) * d;
   const double *mm = r->m + ((size_t)j * r->S + sigma) * d;
+  if (r->vcov) {
+    /* VHEM diag (hem_hmm_bwd_fwd_mex.c:711-733): log, trace and Mahalanobis terms by
+     * division, per dimension */
+    const double *sr = r->vcov + ((size_t)j * r->S + sigma) * d;
+    const double *C = b->covars + ((size_t)i * b->SB + beta) * d;
+    double ell = d * log(2.0 * M_PI);
+    for (int a = 0; a < d; a++) {
+      ell += log(sr[a]);
+      ell += C[a] / sr[a];
+      double x = mu[a] - mm[a];
+      ell += x * x / sr[a];
+    }
+    ell *= -0.5;
+    return r->smooth != 1.0 ? ell / r->smooth : ell;
+  }
   double ell = d * log(2.0 * M_PI) + r->c[(size_t)j * r->S + sigma];
   if (b->covmode == ORACLE_COV_FULL) {
     const double *P = r->P + ((size_t)j * r->S + sigma) * d * d;
@@ -97,7 +114,7 @@ static double emission_term(const oracle_base *b, const oracle_cluster *r,
       ell += P[a] * (x * x);
     }
   }
-  return -0.5 * ell;
+  return r->smooth != 1.0 ? (-0.5 * ell) / r->smooth : -0.5 * ell;
 }
 
 /* One (base i, cluster j) pair.  Scratch `w` must hold
@@ -234,6 +251,10 @@ static void pair_estep(const oracle_base *b, const oracle_cluster *r, int T,
   }
 }
 
+static int run_pairs(const oracle_base *bp, const oracle_cluster *rp, int T, double *LL_elbo,
+                     double *sum_nu_1, double *sum_xi, double *emit_pr, double *emit_mu,
+                     double *emit_Mu, double *sum_t_nu, int nthreads);
+
 /* All pairs; outputs [N][K][...].  tnu_out (sum_t nu, [N][K][S][SB]) may be NULL.
  * nthreads > 1 parallelises over pairs (the reference MEX is single-threaded). */
 int oracle_estep_pairs(int N, int SB, int d, int covmode, const int *nstates,
@@ -247,7 +268,50 @@ int oracle_estep_pairs(int N, int SB, int d, int covmode, const int *nstates,
   for (int i = 0; i < N; i++)
     if (nstates[i] < 1 || nstates[i] > SB) return -2;
   oracle_base b = {N, SB, d, covmode, nstates, prior, A, centres, covars};
-  oracle_cluster r = {K, S, logA, logPi, m, P, c};
+  oracle_cluster r = {K, S, logA, logPi, m, P, c, 1.0, NULL};
+  return run_pairs(&b, &r, T, LL_elbo, sum_nu_1, sum_xi, emit_pr, emit_mu, emit_Mu, sum_t_nu,
+                   nthreads);
+}
+
+/* VHEM sibling (src/compare_mtds/hem/vhem_h3m/hem_hmm_bwd_fwd_mex.c): point-estimate
+ * reduced HMMs Ar [K][S][S], priorr [K][S], centresr [K][S][d], covarsr [K][S][d|d*d];
+ * full covariances read logdetCov [K][S] and invCov [K][S][d][d] (hem_h3m_c_step.m:
+ * 198-205); log(Ar), log(priorr) as at hem mex.c:906-922, 1004-1019; E /= smooth. */
+int oracle_vhem_estep_pairs(int N, int SB, int d, int covmode, const int *nstates,
+                            const double *prior, const double *A, const double *centres,
+                            const double *covars, int K, int S, const double *Ar,
+                            const double *priorr, const double *centresr, const double *covarsr,
+                            const double *logdetCov, const double *invCov, int T, double smooth,
+                            double *LL_elbo, double *sum_nu_1, double *sum_xi, double *emit_pr,
+                            double *emit_mu, double *emit_Mu, double *sum_t_nu, int nthreads) {
+  if (N < 0 || K < 0 || S < 1 || SB < 1 || d < 1 || T < 1 || !(smooth > 0.0)) return -1;
+  for (int i = 0; i < N; i++)
+    if (nstates[i] < 1 || nstates[i] > SB) return -2;
+  double *lA = (double *)malloc(sizeof(double) * ((size_t)K * S * S + 1));
+  double *lP = (double *)malloc(sizeof(double) * ((size_t)K * S + 1));
+  if (!lA || !lP) {
+    free(lA);
+    free(lP);
+    return -3;
+  }
+  for (size_t k = 0; k < (size_t)K * S * S; k++) lA[k] = log(Ar[k]);
+  for (size_t k = 0; k < (size_t)K * S; k++) lP[k] = log(priorr[k]);
+  oracle_base b = {N, SB, d, covmode, nstates, prior, A, centres, covars};
+  oracle_cluster r = {K, S, lA, lP, centresr, invCov, logdetCov, smooth,
+                      covmode == ORACLE_COV_FULL ? NULL : covarsr};
+  const int rc = run_pairs(&b, &r, T, LL_elbo, sum_nu_1, sum_xi, emit_pr, emit_mu, emit_Mu,
+                           sum_t_nu, nthreads);
+  free(lA);
+  free(lP);
+  return rc;
+}
+
+static int run_pairs(const oracle_base *bp, const oracle_cluster *rp, int T, double *LL_elbo,
+                     double *sum_nu_1, double *sum_xi, double *emit_pr, double *emit_mu,
+                     double *emit_Mu, double *sum_t_nu, int nthreads) {
+  const oracle_base b = *bp;
+  const oracle_cluster r = *rp;
+  const int N = b.N, K = r.K, S = r.S, SB = b.SB, d = b.d, covmode = b.covmode;
   const size_t scratch = (size_t)5 * S * SB + (size_t)S * S * SB * T;
   const size_t dMu = covmode == ORACLE_COV_FULL ? (size_t)d * d : (size_t)d;
   int err = 0;

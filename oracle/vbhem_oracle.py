@@ -61,6 +61,11 @@ def load_c_oracle(build_if_missing: bool = True):
         dp, dp, dp, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp,
         ctypes.c_int, dp, dp, dp, dp, dp, dp, dp, ctypes.c_int]
     lib.oracle_estep_pairs.restype = ctypes.c_int
+    lib.oracle_vhem_estep_pairs.argtypes = [
+        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip,
+        dp, dp, dp, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp,
+        ctypes.c_int, ctypes.c_double, dp, dp, dp, dp, dp, dp, dp, ctypes.c_int]
+    lib.oracle_vhem_estep_pairs.restype = ctypes.c_int
     lib.oracle_responsibilities.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp]
     lib.oracle_responsibilities.restype = None
     lib.oracle_statistics.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -111,6 +116,50 @@ def c_estep_pairs(base: dict, consts: dict, T: int, nthreads: int = 1, want_tnu:
     if want_tnu:
         out["sum_t_nu"] = tnu
     del dM
+    return out
+
+
+def c_vhem_estep_pairs(base: dict, red: dict, T: int, smooth: float = 1.0, nthreads: int = 1,
+                       want_tnu: bool = False):
+    """VHEM sibling (hem_hmm_bwd_fwd_mex.c) on point-estimate reduced HMMs
+    red = {A [K][S][S], prior [K][S], centres [K][S][d], covars [K][S][d,d]|[K][S][d]}
+    (+ logdetCov [K][S], invCov [K][S][d][d] computed here for full covariances, as
+    hem_h3m_c_step.m:198-205 does).  Outputs [N][K][...]."""
+    lib = load_c_oracle()
+    N, SB = base["prior"].shape
+    d = base["centres"].shape[2]
+    covmode = base["covmode"]
+    K, S = red["prior"].shape
+    ns = np.ascontiguousarray(base["nstates"], dtype=np.int32)
+    arrs = [_c64(base[k]) for k in ("prior", "A", "centres", "covars")]
+    rarrs = [_c64(red[k]) for k in ("A", "prior", "centres", "covars")]
+    if covmode == COV_FULL:
+        cov = np.asarray(red["covars"], dtype=np.float64)
+        logdet = _c64(np.log(np.linalg.det(cov)))
+        inv = _c64(np.linalg.inv(cov))
+    else:
+        logdet = inv = _c64(np.zeros(1))
+    out = {
+        "LL_elbo": np.zeros((N, K)),
+        "sum_nu_1": np.zeros((N, K, S)),
+        "sum_xi": np.zeros((N, K, S, S)),
+        "emit_pr": np.zeros((N, K, S)),
+        "emit_mu": np.zeros((N, K, S, d)),
+        "emit_Mu": np.zeros((N, K, S, d, d) if covmode == COV_FULL else (N, K, S, d)),
+    }
+    tnu = np.zeros((N, K, S, SB)) if want_tnu else None
+    rc = lib.oracle_vhem_estep_pairs(
+        N, SB, d, covmode, ns.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+        *[_dp(a) for a in arrs], K, S, *[_dp(a) for a in rarrs], _dp(logdet), _dp(inv), int(T),
+        ctypes.c_double(float(smooth)),
+        _dp(out["LL_elbo"]), _dp(out["sum_nu_1"]), _dp(out["sum_xi"]),
+        _dp(out["emit_pr"]), _dp(out["emit_mu"]), _dp(out["emit_Mu"]),
+        _dp(tnu) if tnu is not None else ctypes.POINTER(ctypes.c_double)(),
+        int(nthreads))
+    if rc != 0:
+        raise ValueError(f"oracle_vhem_estep_pairs failed rc={rc}")
+    if want_tnu:
+        out["sum_t_nu"] = tnu
     return out
 
 
@@ -177,6 +226,39 @@ def twin_pair_estep(prior, A, centres, covars, covmode, T, m, W, v, lam,
             dterm = np.einsum("ka,ab,kb->k", diff, Wr, diff)
             E[:, rho] = -0.5 * (d * np.log(2 * np.pi) - logLambdaTilde[rho] + d / lam[rho]
                                 + v[rho] * (trcov + dterm))
+    return _twin_recursions(prior, A, centres, covars, covmode, T, E, logATilde, logPiTilde)
+
+
+def twin_vhem_pair_estep(prior, A, centres, covars, covmode, T, smooth, Ar, priorr, centresr,
+                         covarsr):
+    """One pair of the VHEM sibling as in hem_hmm_bwd_fwd.m:1-200 (+ g3m_stats.m for
+    one Gaussian per state): E[beta,rho] = E_b[log N(y | mu_r, Sigma_r)] / smooth
+    (hem_hmm_bwd_fwd.m:76), then the recursions with log(Ar) (:104) and log(prior_r)."""
+    Sb = A.shape[0]
+    S = Ar.shape[0]
+    d = centres.shape[1]
+    E = np.zeros((Sb, S))
+    for rho in range(S):
+        diff = centres - centresr[rho][None, :]
+        if covmode == COV_DIAG:
+            sr = covarsr[rho]
+            ell = (d * np.log(2 * np.pi) + np.log(sr).sum() + (covars / sr[None, :]).sum(1)
+                   + ((diff ** 2) / sr[None, :]).sum(1))
+        else:
+            inv = np.linalg.inv(covarsr[rho])
+            ell = (d * np.log(2 * np.pi) + np.log(np.linalg.det(covarsr[rho]))
+                   + np.einsum("ab,kab->k", inv, covars) + np.einsum("ka,ab,kb->k", diff, inv, diff))
+        E[:, rho] = -0.5 * ell
+    E = E / smooth
+    with np.errstate(divide="ignore"):
+        lA, lP = np.log(Ar), np.log(priorr)
+    return _twin_recursions(prior, A, centres, covars, covmode, T, E, lA, lP)
+
+
+def _twin_recursions(prior, A, centres, covars, covmode, T, E, logATilde, logPiTilde):
+    """K2-K5 of the twin (fast.m:170-380) given E [Sb,S], logA [S,S], logPi [S]."""
+    Sb = A.shape[0]
+    S = E.shape[1]
     # backward recursion (fast.m:170-227)
     Theta = np.zeros((S, S, Sb, T))
     LL_old = np.zeros((Sb, S))

@@ -70,3 +70,26 @@ SHAPES = [
     ("S20", 2, 2, 20, 20, 2, 1, 4, False),
     ("T50_SbgtS", 3, 3, 2, 6, 2, 0, 50, True),
 ]
+
+
+def make_reduced(K=3, S=3, d=2, covmode=1, seed=0, zero_transition=False) -> dict:
+    """Point-estimate reduced HMMs for the VHEM sibling (hem_hmm_bwd_fwd_mex.c):
+    Dirichlet rows for A and prior, means in [0, 5]^d, SPD covariances
+    (L L'/d + 0.5 I) or diagonal U[0.5, 1.5].  zero_transition sets A[0][0][-1]
+    (renormalised) and prior[0][-1] to 0, so log(A) and log(prior) hold -inf."""
+    rng = np.random.default_rng(4000 + seed)
+    A = rng.dirichlet(np.ones(S), size=(K, S))
+    prior = rng.dirichlet(np.ones(S), size=K)
+    if zero_transition and S > 1:
+        A[0, 0, -1] = 0.0
+        A[0, 0] /= A[0, 0].sum()
+        prior[0, -1] = 0.0
+        prior[0] /= prior[0].sum()
+    centres = rng.uniform(0.0, 5.0, (K, S, d))
+    if covmode == 1:
+        L = rng.normal(size=(K, S, d, d))
+        covars = np.einsum("ksab,kscb->ksac", L, L) / d + 0.5 * np.eye(d)
+    else:
+        covars = rng.uniform(0.5, 1.5, (K, S, d))
+    return dict(A=A, prior=prior, centres=centres, covars=covars)
+

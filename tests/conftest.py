@@ -25,6 +25,7 @@ import vbhem_oracle  # noqa: E402
 PKG_DIR = pkgload.PKG_DIR
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libvbhem_estep.so")
 GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "vbhem_hmm_bwd_fwd_mex.so")
+HEM_GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "hem_hmm_bwd_fwd_mex.so")
 MXSHIM_PATH = os.path.join(ROOT, "tests", "mxshim", "libmxshim.so")
 MATHCHECK_PATH = os.path.join(ROOT, "tests", "mathcheck", "libmathcheck.so")
 GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
@@ -91,6 +92,16 @@ def gateway():
         _make("mex")
     shim = ctypes.CDLL(MXSHIM_PATH, mode=ctypes.RTLD_GLOBAL)
     gw = ctypes.CDLL(GATEWAY_PATH, mode=ctypes.RTLD_GLOBAL)
+    return gw, shim
+
+
+@pytest.fixture(scope="session")
+def hem_gateway():
+    """(mexFunction of the VHEM sibling gateway, mxshim)."""
+    if not (os.path.exists(HEM_GATEWAY_PATH) and os.path.exists(MXSHIM_PATH)):
+        _make("mex")
+    shim = ctypes.CDLL(MXSHIM_PATH, mode=ctypes.RTLD_GLOBAL)
+    gw = ctypes.CDLL(HEM_GATEWAY_PATH, mode=ctypes.RTLD_GLOBAL)
     return gw, shim
 
 

@@ -17,7 +17,7 @@ def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
-    return sorted(set(re.findall(r"\b(vbhem_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b((?:vbhem|vhem)_[a-z0-9_]+)\s*\(", src)))
 
 
 def header_constants():

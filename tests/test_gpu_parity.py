@@ -311,3 +311,35 @@ def test_c4_em_iterations_vs_oracle_sample(vb, vo):
     for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
         assert rel_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, k
     assert rel_err(res.hatZ.cpu().numpy(), ref["hat_Z"]) < RTOL_NORTH_STAR
+
+
+# ----------------------------------------------------------------------------
+# VHEM sibling (vhem_estep_pairs, hem_hmm_bwd_fwd_mex.c) against its oracle
+# ----------------------------------------------------------------------------
+from test_oracle import VHEM_SHAPES  # noqa: E402
+
+
+@pytest.mark.parametrize("shape", VHEM_SHAPES, ids=[s[0] for s in VHEM_SHAPES])
+def test_vhem_pairs_match_oracle(vb, vo, shape):
+    from cases import make_reduced
+    name, N, K, S, Sb, d, cov, T, ragged, smooth, zt = shape
+    seed = seed_of(name)
+    cs = make_case(N, K, S, Sb, d, cov, seed=seed, ragged=ragged, tau=T)
+    red = make_reduced(K, S, d, cov, seed=seed, zero_transition=zt)
+    ref = vo.c_vhem_estep_pairs(cs["base"], red, T, smooth, nthreads=4, want_tnu=True)
+    eng = engine(vb, cs["base"], vb.host.vhem_cluster_constants(red, cov), T)
+    got = eng.pairs(want_tnu=True, smooth=smooth)
+    torch.cuda.synchronize()
+    for k in PAIR_KEYS + ("sum_t_nu",):
+        e = rel_err(got[k].cpu().numpy(), ref[k])
+        assert e < RTOL_PAIRS, (name, k, e)
+
+
+def test_vhem_rejects_bad_smooth(vb):
+    from vbhem_amd import _capi
+    from cases import make_reduced
+    cs = make_case(3, 2, 2, 2, 2, 1, seed=5, tau=4)
+    eng = engine(vb, cs["base"], vb.host.vhem_cluster_constants(make_reduced(2, 2, 2, 1), 1), 4)
+    for bad in (0.0, -1.0, float("nan")):
+        with pytest.raises(_capi.VbhemError):
+            eng.pairs(smooth=bad)

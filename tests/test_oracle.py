@@ -200,3 +200,63 @@ def test_statistics_c_vs_numpy(vo, cov):
         np.testing.assert_allclose(st["Nr"][j], (Z[g, j, None] * o["emit_pr"][g, j]).sum(0),
                                    rtol=1e-13)
         np.testing.assert_allclose(st["Nj"][j], Z[:, j].sum(), rtol=1e-14)
+
+
+# ----------------------------------------------------------------------------
+# VHEM sibling (hem_hmm_bwd_fwd_mex.c): C restatement vs the numpy twin of
+# hem_hmm_bwd_fwd.m, and vs the VBHEM oracle fed the equivalent constants
+# ----------------------------------------------------------------------------
+VHEM_SHAPES = [  # (name, N, K, S, Sb, d, cov, T, ragged, smooth, zero_transition)
+    ("vhem_full", 5, 3, 3, 3, 2, 1, 6, False, 1.0, False),
+    ("vhem_diag", 5, 3, 3, 3, 2, 0, 6, False, 1.0, False),
+    ("vhem_full_smooth", 6, 3, 4, 3, 3, 1, 7, True, 2.5, False),
+    ("vhem_diag_smooth", 6, 3, 4, 3, 3, 0, 7, True, 0.4, False),
+    ("vhem_zero_transition", 5, 2, 3, 3, 2, 1, 5, False, 1.0, True),
+]
+
+
+def vhem_twin_pairs(vo, base, red, T, smooth):
+    N = base["prior"].shape[0]
+    K = red["prior"].shape[0]
+    res = None
+    for i in range(N):
+        Sb = int(base["nstates"][i])
+        for j in range(K):
+            o = vo.twin_vhem_pair_estep(base["prior"][i, :Sb], base["A"][i, :Sb, :Sb],
+                                        base["centres"][i, :Sb], base["covars"][i, :Sb],
+                                        base["covmode"], T, smooth, red["A"][j], red["prior"][j],
+                                        red["centres"][j], red["covars"][j])
+            if res is None:
+                res = {k: np.zeros((N, K) + np.shape(v)) for k, v in o.items() if k != "sum_t_nu"}
+            for k, v in o.items():
+                if k != "sum_t_nu":
+                    res[k][i, j] = v
+    return res
+
+
+@pytest.mark.parametrize("shape", VHEM_SHAPES, ids=[s[0] for s in VHEM_SHAPES])
+def test_vhem_oracle_matches_twin(vo, shape):
+    from cases import make_reduced
+    name, N, K, S, Sb, d, cov, T, ragged, smooth, zt = shape
+    seed = zlib.crc32(name.encode()) % 1000
+    cs = make_case(N, K, S, Sb, d, cov, seed=seed, ragged=ragged, tau=T)
+    red = make_reduced(K, S, d, cov, seed=seed, zero_transition=zt)
+    c = vo.c_vhem_estep_pairs(cs["base"], red, T, smooth, nthreads=4)
+    tw = vhem_twin_pairs(vo, cs["base"], red, T, smooth)
+    for k in PAIR_KEYS:
+        assert np.isfinite(c[k]).all(), k
+        assert rel_err(c[k], tw[k]) < 1e-12, (k, rel_err(c[k], tw[k]))
+
+
+def test_vhem_full_equals_vbhem_with_point_constants(vo, vb):
+    """Full covariances at smooth = 1: the VHEM recursion is the VBHEM one fed
+    logA = log A_r, logPi = log prior_r, P = inv(Sigma_r), c = log det(Sigma_r)
+    (the product's vhem_cluster_constants) -- identical code path in the oracle."""
+    from cases import make_reduced
+    cs = make_case(5, 3, 3, 3, 2, 1, seed=17, tau=6)
+    red = make_reduced(3, 3, 2, 1, seed=17)
+    consts = vb.host.vhem_cluster_constants(red, 1)
+    a = vo.c_vhem_estep_pairs(cs["base"], red, 6, 1.0)
+    b = vo.c_estep_pairs(cs["base"], consts, 6)
+    for k in PAIR_KEYS:
+        assert rel_err(a[k], b[k]) < 1e-13, k
