@@ -32,6 +32,21 @@ class ClusterT(ctypes.Structure):
                 ("P", _vp), ("c", _vp)]
 
 
+class PostT(ctypes.Structure):  # include/vbhem_em.h vbhem_post_t
+    _fields_ = [("K", _c_int), ("S", _c_int), ("d", _c_int), ("covmode", _c_int),
+                ("alpha", _vp), ("eta", _vp), ("epsilon", _vp), ("lam", _vp), ("v", _vp),
+                ("m", _vp), ("W", _vp)]
+
+
+class EmOptT(ctypes.Structure):  # include/vbhem_em.h vbhem_em_opt_t
+    _fields_ = [("alpha0", ctypes.c_double), ("eta0", ctypes.c_double),
+                ("epsilon0", ctypes.c_double), ("lambda0", ctypes.c_double),
+                ("v0", ctypes.c_double), ("m0", _vp), ("W0", _vp), ("W0_len", _c_int),
+                ("Nv", ctypes.c_double), ("max_iter", _c_int), ("minDiff", ctypes.c_double)]
+
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(_c_int, _vp, _c_size, _vp, _vp)
+
 EXPORTS = {
     "vbhem_pairs_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int]),
     "vbhem_estep_pairs": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
@@ -58,6 +73,15 @@ EXPORTS = {
     "vbhem_timing_read_gated": (_c_int, [ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_set_fused_mode": (_c_int, [_c_int]),
+    "vbhem_em_prelude": (_c_int, [ctypes.POINTER(PostT), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "vbhem_em_lower_bound": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp, _vp,
+                                      _vp, _vp, _vp, ctypes.POINTER(ctypes.c_double)]),
+    "vbhem_em_mstep": (_c_int, [ctypes.POINTER(EmOptT), _vp, ctypes.POINTER(PostT)]),
+    "vbhem_em_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), _c_int, _c_int, _c_int]),
+    "vbhem_em_run": (_c_int, [ctypes.POINTER(BaseT), _vp, _c_int, ctypes.POINTER(EmOptT),
+                              ctypes.POINTER(PostT), _vp, ctypes.POINTER(_c_int),
+                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int), _vp, _vp,
+                              _vp, _vp, _c_size, _vp, ALLREDUCE_FN, _vp]),
     "vbhem_last_error": (ctypes.c_char_p, []),
     "vbhem_version": (ctypes.c_char_p, []),
 }

@@ -1,0 +1,411 @@
+// vbhem_em.hip -- the VBHEM-H3M EM host loop (include/vbhem_em.h), host C++.
+//
+// Mirrors, per EM iteration, src/vbhem/vbhem_h3m_c_step_fc.m:
+//   psi prelude            :118-165, 180-191, 271-273      vbhem_em_prelude
+//   E-step (device)        :168-198, 270-296               vbhem_estep_fused
+//   lower bound            vbhemh3m_lb.m:64-186            vbhem_em_lower_bound
+//   convergence / NaN      :311-374                        vbhem_em_run
+//   statistics + M-step    vbhem_compute_Statistics.m:57-82,
+//                          vbhem_mstep_component.m:42-70, :396   vbhem_em_mstep
+// The arithmetic follows vbhem_amd/host.py (the Python host path, itself checked
+// against the oracle's restatement of the MATLAB code); psi is evaluated by
+// recurrence to x >= 8 plus the asymptotic series, lgamma is libm's, and the
+// d x d inverse / determinant use LU with partial pivoting (as MATLAB's inv/det).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "vbhem_em.h"
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+
+// digamma for x > 0: psi(x) = psi(x + n) - sum_{k<n} 1/(x + k), then the
+// asymptotic expansion ln x - 1/(2x) - sum B_2k / (2k x^2k) at x >= 8.
+double psi(double x) {
+  double acc = 0.0;
+  while (x < 8.0) {
+    acc -= 1.0 / x;
+    x += 1.0;
+  }
+  const double r = 1.0 / x, r2 = r * r;
+  const double series =
+      r2 * (1.0 / 12 - r2 * (1.0 / 120 - r2 * (1.0 / 252 - r2 * (1.0 / 240 - r2 * (1.0 / 132 -
+      r2 * (691.0 / 32760 - r2 * (1.0 / 12)))))));
+  return acc + std::log(x) - 0.5 * r - series;
+}
+
+// LU with partial pivoting of a d x d row-major matrix (in place); returns det.
+double lu_det(std::vector<double> &a, int d, std::vector<int> &piv) {
+  double det = 1.0;
+  piv.resize(d);
+  for (int k = 0; k < d; ++k) {
+    int p = k;
+    for (int r = k + 1; r < d; ++r)
+      if (std::fabs(a[(size_t)r * d + k]) > std::fabs(a[(size_t)p * d + k])) p = r;
+    piv[k] = p;
+    if (p != k) {
+      for (int c = 0; c < d; ++c) std::swap(a[(size_t)k * d + c], a[(size_t)p * d + c]);
+      det = -det;
+    }
+    const double pk = a[(size_t)k * d + k];
+    det *= pk;
+    if (pk == 0.0) continue;
+    for (int r = k + 1; r < d; ++r) {
+      const double f = a[(size_t)r * d + k] / pk;
+      a[(size_t)r * d + k] = f;
+      for (int c = k + 1; c < d; ++c) a[(size_t)r * d + c] -= f * a[(size_t)k * d + c];
+    }
+  }
+  return det;
+}
+
+double det_of(const double *m, int d) {
+  std::vector<double> a(m, m + (size_t)d * d);
+  std::vector<int> piv;
+  return lu_det(a, d, piv);
+}
+
+// inverse through the LU factors (solve for the identity columns)
+void inv_of(const double *m, int d, double *out) {
+  std::vector<double> a(m, m + (size_t)d * d);
+  std::vector<int> piv;
+  lu_det(a, d, piv);
+  for (int col = 0; col < d; ++col) {
+    std::vector<double> x(d, 0.0);
+    x[col] = 1.0;
+    for (int k = 0; k < d; ++k) std::swap(x[k], x[piv[k]]);
+    for (int r = 0; r < d; ++r)
+      for (int c = 0; c < r; ++c) x[r] -= a[(size_t)r * d + c] * x[c];
+    for (int r = d - 1; r >= 0; --r) {
+      for (int c = r + 1; c < d; ++c) x[r] -= a[(size_t)r * d + c] * x[c];
+      x[r] /= a[(size_t)r * d + r];
+    }
+    for (int r = 0; r < d; ++r) out[(size_t)r * d + col] = x[r];
+  }
+}
+
+bool post_ok(const vbhem_post_t *p) {
+  return p && p->K >= 1 && p->S >= 1 && p->d >= 1 &&
+         (p->covmode == VBHEM_COV_DIAG || p->covmode == VBHEM_COV_FULL) && p->alpha && p->eta &&
+         p->epsilon && p->lam && p->v && p->m && p->W;
+}
+
+bool opt_ok(const vbhem_em_opt_t *o, int d) {
+  return o && o->m0 && o->W0 && (o->W0_len == 1 || o->W0_len == d) && o->max_iter >= 0;
+}
+
+// W0 as a full matrix and its inverse (host.py::_W0)
+void w0_inv(const vbhem_em_opt_t *o, int d, std::vector<double> &W0inv) {
+  std::vector<double> W0((size_t)d * d, 0.0);
+  for (int a = 0; a < d; ++a) W0[(size_t)a * d + a] = o->W0_len == 1 ? o->W0[0] : o->W0[a];
+  W0inv.assign((size_t)d * d, 0.0);
+  inv_of(W0.data(), d, W0inv.data());
+}
+
+// packed statistics accessors (include/vbhem_estep.h: Nj | N1 | M | Lt1 Lt7 | U)
+struct Stats {
+  const double *Nj, *N1, *M, *U;
+  double Lt1, Lt7;
+  int NU;
+  Stats(const double *v, int K, int S, int d, int covmode) {
+    NU = (int)vbhem_stats_nu(d, covmode);
+    size_t o = 0;
+    Nj = v + o; o += K;
+    N1 = v + o; o += (size_t)K * S;
+    M = v + o; o += (size_t)K * S * S;
+    Lt1 = v[o];
+    Lt7 = v[o + 1];
+    o += 2;
+    U = v + o;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int vbhem_em_prelude(const vbhem_post_t *post, double *logA, double *logPi, double *m, double *P,
+                     double *c, double *logLambdaTilde, double *logOmega) {
+  if (!post_ok(post) || !logA || !logPi || !m || !P || !c || !logLambdaTilde || !logOmega)
+    return VBHEM_ERR_ARG;
+  const int K = post->K, S = post->S, d = post->d;
+  const bool full = post->covmode == VBHEM_COV_FULL;
+  const size_t dd = full ? (size_t)d * d : (size_t)d;
+  for (int k = 0; k < K; ++k) {
+    for (int s = 0; s < S; ++s) {
+      const size_t ks = (size_t)k * S + s;
+      const double v = post->v[ks];
+      double t1 = 0.0;
+      for (int q = 1; q <= d; ++q) t1 += psi(0.5 * (v + 1.0) - 0.5 * q);
+      const double *W = post->W + ks * dd;
+      double logdet;
+      if (full) {
+        logdet = std::log(det_of(W, d));
+      } else {
+        logdet = 0.0;
+        for (int a = 0; a < d; ++a) logdet += std::log(W[a]);
+      }
+      const double lLT = t1 + d * std::log(2.0) + logdet;
+      logLambdaTilde[ks] = lLT;
+      c[ks] = -lLT + d / post->lam[ks];
+      for (size_t x = 0; x < dd; ++x) P[ks * dd + x] = v * W[x];
+      for (int a = 0; a < d; ++a) m[ks * d + a] = post->m[ks * d + a];
+      // logATilde row (step_fc.m:156-157)
+      const double *eps = post->epsilon + ks * S;
+      double es = 0.0;
+      for (int s2 = 0; s2 < S; ++s2) es += eps[s2];
+      const double pes = psi(es);
+      for (int s2 = 0; s2 < S; ++s2) logA[ks * S + s2] = psi(eps[s2]) - pes;
+    }
+    double ets = 0.0;
+    for (int s = 0; s < S; ++s) ets += post->eta[(size_t)k * S + s];
+    const double pet = psi(ets);
+    for (int s = 0; s < S; ++s)
+      logPi[(size_t)k * S + s] = psi(post->eta[(size_t)k * S + s]) - pet;
+  }
+  double as = 0.0;
+  for (int k = 0; k < K; ++k) as += post->alpha[k];
+  const double pas = psi(as);
+  for (int k = 0; k < K; ++k) logOmega[k] = psi(post->alpha[k]) - pas;
+  return VBHEM_OK;
+}
+
+int vbhem_em_lower_bound(const vbhem_post_t *post, const vbhem_em_opt_t *opt,
+                         const double *stats, const double *logLambdaTilde, const double *logA,
+                         const double *logPi, const double *logOmega, double *L) {
+  if (!post_ok(post) || !opt_ok(opt, post->d) || !stats || !logLambdaTilde || !logA || !logPi ||
+      !logOmega || !L)
+    return VBHEM_ERR_ARG;
+  const int K = post->K, S = post->S, d = post->d;
+  const bool full = post->covmode == VBHEM_COV_FULL;
+  const size_t dd = full ? (size_t)d * d : (size_t)d;
+  const Stats st(stats, K, S, d, post->covmode);
+  const double a0 = opt->alpha0, e0 = opt->eta0, ep0 = opt->epsilon0, l0 = opt->lambda0,
+               v0 = opt->v0;
+  std::vector<double> W0inv;
+  w0_inv(opt, d, W0inv);
+  double logdetW0inv = 0.0;
+  if (opt->W0_len == 1) logdetW0inv = d * std::log(W0inv[0]);
+  else for (int a = 0; a < d; ++a) logdetW0inv += std::log(W0inv[(size_t)a * d + a]);
+  double sg0 = 0.0;
+  for (int q = 1; q <= d; ++q) sg0 += std::lgamma(0.5 * (v0 + 1 - q));
+  const double logCalpha0 = std::lgamma(K * a0) - K * std::lgamma(a0);
+  const double logCeta0 = std::lgamma(S * e0) - S * std::lgamma(e0);
+  const double logCepsilon0 = std::lgamma(S * ep0) - S * std::lgamma(ep0);
+  const double logB0 = (v0 / 2) * logdetW0inv - (v0 * d / 2) * std::log(2.0) -
+                       (d * (d - 1) / 4.0) * std::log(kPi) - sg0;
+  const double const2 = d * std::log(l0 / (2 * kPi));
+  double asum = 0.0, lga = 0.0;
+  for (int k = 0; k < K; ++k) {
+    asum += post->alpha[k];
+    lga += std::lgamma(post->alpha[k]);
+  }
+  const double logCalpha = std::lgamma(asum) - lga;
+  double Lt2 = 0.0, sumLO = 0.0, Lt8b = 0.0;
+  for (int k = 0; k < K; ++k) {
+    Lt2 += (st.Nj[k] + 1e-50) * logOmega[k];
+    sumLO += logOmega[k];
+    Lt8b += (post->alpha[k] - 1) * logOmega[k];
+  }
+  double sumLPi = 0.0, sumLA = 0.0;
+  for (size_t x = 0; x < (size_t)K * S; ++x) sumLPi += logPi[x];
+  for (size_t x = 0; x < (size_t)K * S * S; ++x) sumLA += logA[x];
+  const double Lt3 = K * logCeta0 + (e0 - 1) * sumLPi;
+  const double Lt4 = K * S * logCepsilon0 + (ep0 - 1) * sumLA;
+  const double Lt6 = logCalpha0 + (a0 - 1) * sumLO;
+  const double Lt8 = logCalpha + Lt8b;
+  double Lt5 = 0.0, Lt9 = 0.0, Lt10 = 0.0;
+  std::vector<double> Wf((size_t)d * d);
+  for (int k = 0; k < K; ++k) {
+    double H = 0.0, Lt51 = 0.0, sumLLT = 0.0, sumVtr = 0.0, lt10a = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const size_t ks = (size_t)k * S + s;
+      const double v = post->v[ks], lam = post->lam[ks], lLT = logLambdaTilde[ks];
+      const double *W = post->W + ks * dd;
+      if (full) {
+        for (size_t x = 0; x < dd; ++x) Wf[x] = W[x];
+      } else {
+        std::fill(Wf.begin(), Wf.end(), 0.0);
+        for (int a = 0; a < d; ++a) Wf[(size_t)a * d + a] = W[a];
+      }
+      double sg = 0.0;
+      for (int q = 1; q <= d; ++q) sg += std::lgamma(0.5 * (v + 1 - q));
+      const double logBk = -(v / 2) * std::log(det_of(Wf.data(), d)) - (v * d / 2) * std::log(2.0) -
+                           (d * (d - 1) / 4.0) * std::log(kPi) - sg;
+      H += -logBk - 0.5 * (v - d - 1) * lLT + 0.5 * v * d;
+      double mWm = 0.0, trW = 0.0;
+      const double *mk = post->m + ks * d;
+      for (int a = 0; a < d; ++a)
+        for (int b = 0; b < d; ++b) {
+          mWm += (mk[a] - opt->m0[a]) * Wf[(size_t)a * d + b] * (mk[b] - opt->m0[b]);
+          trW += W0inv[(size_t)a * d + b] * Wf[(size_t)b * d + a];
+        }
+      Lt51 += const2 + lLT - d * l0 / lam - l0 * v * mWm;
+      sumLLT += lLT;
+      sumVtr += v * trW;
+      lt10a += lLT + d * std::log(lam / (2 * kPi));
+    }
+    Lt5 += 0.5 * Lt51 + S * logB0 + 0.5 * (v0 - d - 1) * sumLLT - 0.5 * sumVtr;
+    // Lt9: Dirichlet entropies of eta and epsilon rows
+    double es = 0.0, lge = 0.0, ept = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double e = post->eta[(size_t)k * S + s];
+      es += e;
+      lge += std::lgamma(e);
+      ept += (e - 1) * logPi[(size_t)k * S + s];
+    }
+    Lt9 += std::lgamma(es) - lge + ept;
+    for (int r = 0; r < S; ++r) {
+      double ps = 0.0, lgp = 0.0, pt = 0.0;
+      for (int s = 0; s < S; ++s) {
+        const size_t x = ((size_t)k * S + r) * S + s;
+        ps += post->epsilon[x];
+        lgp += std::lgamma(post->epsilon[x]);
+        pt += (post->epsilon[x] - 1) * logA[x];
+      }
+      Lt9 += std::lgamma(ps) - lgp + pt;
+    }
+    Lt10 += 0.5 * lt10a - 0.5 * d * S - H;
+  }
+  *L = st.Lt1 + Lt2 + Lt3 + Lt4 + Lt5 + Lt6 - st.Lt7 - Lt8 - Lt9 - Lt10;
+  return VBHEM_OK;
+}
+
+int vbhem_em_mstep(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t *post) {
+  if (!post_ok(post) || !opt_ok(opt, post->d) || !stats) return VBHEM_ERR_ARG;
+  const int K = post->K, S = post->S, d = post->d;
+  const bool full = post->covmode == VBHEM_COV_FULL;
+  const size_t dd = full ? (size_t)d * d : (size_t)d;
+  const Stats st(stats, K, S, d, post->covmode);
+  const double l0 = opt->lambda0;
+  std::vector<double> W0inv;
+  w0_inv(opt, d, W0inv);
+  std::vector<double> y(d), SC((size_t)d * d), Mt((size_t)d * d), tW((size_t)d * d);
+  for (int k = 0; k < K; ++k) {
+    post->alpha[k] = opt->alpha0 + (st.Nj[k] + 1e-50);
+    for (int s = 0; s < S; ++s) {
+      const size_t ks = (size_t)k * S + s;
+      const double *u = st.U + ks * st.NU;
+      // vbhem_compute_Statistics.m:57-82
+      const double Nr = u[0] + 1e-50;
+      for (int a = 0; a < d; ++a) y[a] = u[1 + a] / Nr;
+      std::fill(SC.begin(), SC.end(), 0.0);
+      if (full) {
+        int e = 1 + d;
+        for (int a = 0; a < d; ++a)
+          for (int b = a; b < d; ++b, ++e) {
+            SC[(size_t)a * d + b] = u[e] / Nr - y[a] * y[b];
+            SC[(size_t)b * d + a] = u[e] / Nr - y[b] * y[a];
+          }
+      } else {
+        for (int a = 0; a < d; ++a) SC[(size_t)a * d + a] = u[1 + d + a] / Nr - y[a] * y[a];
+      }
+      // vbhem_mstep_component.m:42-70
+      const double lam = l0 + Nr, v = opt->v0 + Nr + 1.0, mult1 = l0 * Nr / (l0 + Nr);
+      post->lam[ks] = lam;
+      post->v[ks] = v;
+      for (int a = 0; a < d; ++a)
+        post->m[ks * d + a] = (l0 * opt->m0[a] + Nr * y[a]) / (l0 + Nr);
+      for (int a = 0; a < d; ++a)
+        for (int b = 0; b < d; ++b)
+          Mt[(size_t)a * d + b] = W0inv[(size_t)a * d + b] + Nr * SC[(size_t)a * d + b] +
+                                  mult1 * (y[a] - opt->m0[a]) * (y[b] - opt->m0[b]);
+      inv_of(Mt.data(), d, tW.data());
+      double *W = post->W + ks * dd;
+      if (full) {
+        for (int a = 0; a < d; ++a)
+          for (int b = 0; b < d; ++b)
+            W[(size_t)a * d + b] = (tW[(size_t)a * d + b] + tW[(size_t)b * d + a]) / 2;
+      } else {
+        for (int a = 0; a < d; ++a) W[a] = (tW[(size_t)a * d + a] + tW[(size_t)a * d + a]) / 2;
+      }
+      post->eta[ks] = opt->eta0 + st.N1[ks];
+      for (int s2 = 0; s2 < S; ++s2)
+        post->epsilon[ks * S + s2] = opt->epsilon0 + (S > 1 ? st.M[ks * S + s2] : 1e-12);
+    }
+  }
+  return VBHEM_OK;
+}
+
+size_t vbhem_em_workspace_bytes(const vbhem_base_t *base, int K, int S, int T) {
+  if (!base || K < 1 || S < 1) return 0;
+  const int d = base->d;
+  const size_t dd = base->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
+  vbhem_cluster_t c = {K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const size_t fused = vbhem_fused_workspace_bytes(base, &c, T);
+  if (fused == 0) return 0;
+  const size_t consts = (size_t)K * S * S + (size_t)K * S + (size_t)K * S * d + (size_t)K * S * dd +
+                        (size_t)K * S + (size_t)K;
+  return (fused + 255) / 256 * 256 + consts * sizeof(double) + 256;
+}
+
+int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
+                 const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
+                 double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
+                 double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
+                 vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
+  if (!base || !post_ok(post) || !opt_ok(opt, post->d) || !LogLs || !iters || !L_final ||
+      !stable || !stats_dev || post->d != base->d || post->covmode != base->covmode)
+    return VBHEM_ERR_ARG;
+  const int K = post->K, S = post->S, d = post->d;
+  const size_t dd = post->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
+  const size_t need = vbhem_em_workspace_bytes(base, K, S, T);
+  if (need == 0 || !workspace_dev || workspace_bytes < need) return VBHEM_ERR_WORKSPACE;
+  vbhem_cluster_t c0 = {K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const size_t fused = (vbhem_fused_workspace_bytes(base, &c0, T) + 255) / 256 * 256;
+  // device constants: logA | logPi | m | P | c | logOmega (one upload per iteration)
+  const size_t nA = (size_t)K * S * S, nPi = (size_t)K * S, nm = (size_t)K * S * d,
+               nP = (size_t)K * S * dd, nc = (size_t)K * S, nO = (size_t)K;
+  std::vector<double> h(nA + nPi + nm + nP + nc + nO), lLT(nc);
+  double *dc = reinterpret_cast<double *>(static_cast<char *>(workspace_dev) + fused);
+  vbhem_cluster_t cl = {K, S, dc, dc + nA, dc + nA + nPi, dc + nA + nPi + nm,
+                        dc + nA + nPi + nm + nP};
+  const double *dlogOmega = dc + nA + nPi + nm + nP + nc;
+  const size_t slen = vbhem_stats_len(K, S, d, post->covmode);
+  std::vector<double> stats(slen);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  double lastL = -DBL_MAX, L = -INFINITY;
+  int it = 0;
+  *stable = 1;
+  while (true) {
+    double *hA = h.data(), *hPi = hA + nA, *hm = hPi + nPi, *hP = hm + nm, *hc = hP + nP,
+           *hO = hc + nc;
+    int rc = vbhem_em_prelude(post, hA, hPi, hm, hP, hc, lLT.data(), hO);
+    if (rc != VBHEM_OK) return rc;
+    hipError_t e = hipMemcpyAsync(dc, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return VBHEM_ERR_HIP;
+    rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hatZ_dev, LL_dev,
+                           workspace_dev, fused, stream);
+    if (rc != VBHEM_OK) return rc;
+    if (allreduce && allreduce(stats_dev, slen, stream, allreduce_ctx) != 0) return VBHEM_ERR_HIP;
+    e = hipMemcpyAsync(stats.data(), stats_dev, slen * sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return VBHEM_ERR_HIP;
+    rc = vbhem_em_lower_bound(post, opt, stats.data(), lLT.data(), hA, hPi, hO, &L);
+    if (rc != VBHEM_OK) return rc;
+    bool do_break = false;
+    if (it > 1 && std::fabs((L - lastL) / lastL) <= opt->minDiff) do_break = true;
+    if (it == opt->max_iter) do_break = true;
+    if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, stop before the M-step
+      L = -INFINITY;
+      *stable = 0;
+      break;
+    }
+    rc = vbhem_em_mstep(opt, stats.data(), post);
+    if (rc != VBHEM_OK) return rc;
+    LogLs[it] = L;
+    ++it;
+    lastL = L;
+    if (do_break) break;
+  }
+  *iters = it;
+  *L_final = L;
+  return VBHEM_OK;
+}
+
+}  // extern "C"

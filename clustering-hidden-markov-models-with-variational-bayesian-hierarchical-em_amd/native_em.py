@@ -1,0 +1,133 @@
+"""The EM loop in C++ (include/vbhem_em.h).
+
+:func:`run` drives ``vbhem_em_run``: the whole of vbhem_h3m_c_step_fc.m:1-449
+(psi prelude, fused device E-step, lower bound, convergence test, M-step) runs
+in the library; Python only allocates the device buffers and, with several
+ranks, supplies the all-reduce of the packed statistics as a callback.  The
+host steps are also exposed one by one (:func:`prelude`, :func:`mstep`,
+:func:`lower_bound`) and are checked against :mod:`vbhem_amd.host`.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+
+from . import _capi
+from .em import EMResult
+from .estep import EStepEngine
+from .h3m import COV_FULL, Posterior
+
+
+class _PostBuf:
+    """Contiguous float64 host copies of a Posterior plus its vbhem_post_t view."""
+
+    def __init__(self, post: Posterior, covmode: int):
+        self.a = {k: np.ascontiguousarray(getattr(post, k), dtype=np.float64).copy()
+                  for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W")}
+        K, S, d = self.a["m"].shape
+        self.W0mode = post.W0mode
+        p = {k: self.a[k].ctypes.data for k in self.a}
+        self.t = _capi.PostT(K, S, d, covmode, p["alpha"], p["eta"], p["epsilon"], p["lam"],
+                             p["v"], p["m"], p["W"])
+
+    def posterior(self) -> Posterior:
+        return Posterior(W0mode=self.W0mode, **{k: v.copy() for k, v in self.a.items()})
+
+
+class _OptBuf:
+    def __init__(self, opt: dict):
+        self.m0 = np.ascontiguousarray(opt["m0"], dtype=np.float64).reshape(-1)
+        self.W0 = np.ascontiguousarray(np.array(opt["W0"], dtype=np.float64, ndmin=1))
+        self.t = _capi.EmOptT(float(opt["alpha0"]), float(opt["eta0"]), float(opt["epsilon0"]),
+                              float(opt["lambda0"]), float(opt["v0"]), self.m0.ctypes.data,
+                              self.W0.ctypes.data, int(self.W0.size), float(opt["Nv"]),
+                              int(opt["max_iter"]), float(opt["minDiff"]))
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def prelude(post: Posterior, covmode: int) -> dict:
+    """vbhem_em_prelude: the E-step constants + logOmega (cf. host.cluster_constants)."""
+    pb = _PostBuf(post, covmode)
+    K, S, d = post.m.shape
+    out = dict(logA=np.zeros((K, S, S)), logPi=np.zeros((K, S)), m=np.zeros((K, S, d)),
+               P=np.zeros((K, S, d, d) if covmode == COV_FULL else (K, S, d)), c=np.zeros((K, S)),
+               logLambdaTilde=np.zeros((K, S)), logOmega=np.zeros(K))
+    _capi.check(_capi.lib().vbhem_em_prelude(ctypes.byref(pb.t), *(_p(out[k]) for k in (
+        "logA", "logPi", "m", "P", "c", "logLambdaTilde", "logOmega"))), "vbhem_em_prelude")
+    return out
+
+
+def mstep(stats: np.ndarray, post: Posterior, opt: dict, covmode: int) -> Posterior:
+    """vbhem_em_mstep on a packed statistics vector (cf. host.finish_statistics + mstep)."""
+    pb, ob = _PostBuf(post, covmode), _OptBuf(opt)
+    st = np.ascontiguousarray(stats, dtype=np.float64)
+    _capi.check(_capi.lib().vbhem_em_mstep(ctypes.byref(ob.t), _p(st), ctypes.byref(pb.t)),
+                "vbhem_em_mstep")
+    return pb.posterior()
+
+
+def lower_bound(stats: np.ndarray, post: Posterior, opt: dict, covmode: int, consts: dict) -> float:
+    """vbhem_em_lower_bound (cf. host.lower_bound)."""
+    pb, ob = _PostBuf(post, covmode), _OptBuf(opt)
+    st = np.ascontiguousarray(stats, dtype=np.float64)
+    c = {k: np.ascontiguousarray(consts[k], dtype=np.float64)
+         for k in ("logLambdaTilde", "logA", "logPi", "logOmega")}
+    L = ctypes.c_double()
+    _capi.check(_capi.lib().vbhem_em_lower_bound(
+        ctypes.byref(pb.t), ctypes.byref(ob.t), _p(st), _p(c["logLambdaTilde"]), _p(c["logA"]),
+        _p(c["logPi"]), _p(c["logOmega"]), ctypes.byref(L)), "vbhem_em_lower_bound")
+    return float(L.value)
+
+
+def run(post: Posterior, engine: EStepEngine, opt: dict, *, total_N: Optional[int] = None,
+        allreduce: Optional[Callable[[torch.Tensor], None]] = None,
+        max_iter: Optional[int] = None) -> EMResult:
+    """The EM loop in C++ on the engine's base set; same result type as
+    :func:`vbhem_amd.em.vbhem_h3m_c_step_fc`."""
+    from .em import tilde_n
+    covmode = engine.base.covmode
+    total_N = engine.N if total_N is None else int(total_N)
+    opt = dict(opt)
+    if max_iter is not None:
+        opt["max_iter"] = int(max_iter)
+    pb, ob = _PostBuf(post, covmode), _OptBuf(opt)
+    K, S = pb.t.K, pb.t.S
+    tN = tilde_n(engine, opt["Nv"], total_N).contiguous()
+    lib = _capi.lib()
+    nb = int(lib.vbhem_em_workspace_bytes(ctypes.byref(engine._bt), K, S, engine.T))
+    if nb == 0:
+        raise _capi.VbhemError("vbhem_em_workspace_bytes: unsupported shape")
+    ws = torch.empty((nb,), dtype=torch.uint8, device=engine.device)
+    LogLs = np.zeros(int(opt["max_iter"]) + 1)
+    iters, L, stable = ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
+    stats = engine.stats
+
+    def _ar(ptr, n, stream, ctx):  # the statistics buffer is engine.stats
+        try:
+            allreduce(stats)
+            return 0
+        except Exception:  # noqa: BLE001 -- reported as a status code to the C loop
+            return 1
+
+    cb = _capi.ALLREDUCE_FN(_ar) if allreduce is not None else _capi.ALLREDUCE_FN()
+    rc = lib.vbhem_em_run(ctypes.byref(engine._bt), _capi.ptr(tN), engine.T, ctypes.byref(ob.t),
+                          ctypes.byref(pb.t), _p(LogLs), ctypes.byref(iters), ctypes.byref(L),
+                          ctypes.byref(stable), _capi.ptr(stats), _capi.ptr(engine.hatZ),
+                          _capi.ptr(engine.LL), _capi.ptr(ws), ws.numel(), engine._stream(), cb,
+                          None)
+    _capi.check(rc, "vbhem_em_run")
+    it = int(iters.value)
+    res = EMResult(post=pb.posterior(), LogLs=[float(x) for x in LogLs[:it]], LL=float(L.value),
+                   iters=it, stable=bool(stable.value), hatZ=engine.hatZ.clone(),
+                   L_elbo=engine.LL.clone(), Nj=None, syn=None)
+    if res.stable:
+        from . import host
+        res.point = host.convert_to_point(res.post, covmode)
+        res.label = torch.argmax(res.hatZ, dim=1)
+    return res

@@ -1,5 +1,5 @@
 """The C-ABI library (CPU side): it loads, exports every entry point that
-include/vbhem_estep.h declares, and its size queries / argument validation
+include/*.h declare, and its size queries / argument validation
 behave as documented -- without launching anything (no GPU here)."""
 import ctypes
 import os
@@ -14,7 +14,8 @@ HEADER = os.path.join(ROOT, "include", "vbhem_estep.h")
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(os.path.join(ROOT, "include", h)).read()
+                  for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
     return sorted(set(re.findall(r"\b((?:vbhem|vhem)_[a-z0-9_]+)\s*\(", src)))

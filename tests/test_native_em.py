@@ -1,0 +1,110 @@
+"""The EM host loop in C++ (include/vbhem_em.h, vbhem_amd.native_em).
+
+CPU: each host step of the library (psi prelude, M-step, lower bound) against
+the Python host path (vbhem_amd.host, itself checked against the oracle's
+restatement of the MATLAB code) on oracle-generated statistics.
+GPU: the whole loop (vbhem_em_run) against the Python EM loop on the device
+E-step, and against the oracle EM (north-star tolerance)."""
+import numpy as np
+import pytest
+
+from cases import make_case
+from conftest import RTOL_NORTH_STAR, rel_err
+
+
+def packed_stats(vb, vo, cs, cov):
+    """The fused E-step's packed vector [Nj | N1 | M | Lt1 Lt7 | U], built from the oracle."""
+    base, consts, post, T = cs["base"], cs["consts"], cs["post"], cs["T"]
+    N = base["prior"].shape[0]
+    K, S = consts["logPi"].shape
+    d = base["centres"].shape[2]
+    pairs = vo.c_estep_pairs(base, consts, T)
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, post["alpha"])
+    st = vo.c_statistics(Z, pairs, cov)
+    NU = vb.host.stats_nu(d, cov)
+    U = np.zeros((K, S, NU))
+    U[..., 0] = st["Nr"]
+    U[..., 1:1 + d] = st["Y"]
+    if cov == 1:
+        iu = np.triu_indices(d)
+        U[..., 1 + d:] = st["SC"][..., iu[0], iu[1]]
+    else:
+        U[..., 1 + d:] = st["SC"]
+    Lt1 = float((Z * pairs["LL_elbo"]).sum())
+    Lt7 = float((hz * np.log(hz)).sum())
+    vec = np.concatenate([st["Nj"], st["N1"].ravel(), st["M"].ravel(), [Lt1, Lt7], U.ravel()])
+    assert vec.size == vb.host.stats_len(K, S, d, cov)
+    return vec
+
+
+CASES = [("full", 1, 3), ("diag", 0, 3), ("full_S1", 1, 1)]
+
+
+@pytest.mark.parametrize("name,cov,S", CASES, ids=[c[0] for c in CASES])
+def test_prelude_matches_host(vb, name, cov, S):
+    from vbhem_amd import native_em
+    cs = make_case(6, 3, S, 3, 3, cov, seed=11 + cov)
+    got = native_em.prelude(cs["P"], cov)
+    ref = vb.host.cluster_constants(cs["P"], cov)
+    for k in ("logA", "logPi", "m", "P", "c", "logLambdaTilde"):
+        assert rel_err(got[k], ref[k]) < 1e-13, k
+    assert rel_err(got["logOmega"], vb.host.log_omega_tilde(cs["P"].alpha)) < 1e-14
+
+
+@pytest.mark.parametrize("name,cov,S", CASES, ids=[c[0] for c in CASES])
+def test_mstep_and_bound_match_host(vb, vo, name, cov, S):
+    from vbhem_amd import native_em
+    cs = make_case(8, 3, S, 3, 3, cov, seed=21 + cov, tau=6)
+    K, d = 3, 3
+    vec = packed_stats(vb, vo, cs, cov)
+    P, opt = cs["P"], cs["opt"]
+    # M-step
+    got = native_em.mstep(vec, P, opt, cov)
+    st = vb.host.unpack_stats(vec, K, S, d, cov)
+    ref = vb.host.mstep(vb.host.finish_statistics(st, cov), st["Nj"] + 1e-50, opt, cov, P.W0mode)
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert rel_err(getattr(got, k), getattr(ref, k)) < 1e-12, k
+    # lower bound
+    consts = vb.host.cluster_constants(P, cov)
+    logOm = vb.host.log_omega_tilde(P.alpha)
+    Lref = vb.host.lower_bound(st["Lt1"], st["Lt7"], st["Nj"] + 1e-50, logOm, P, consts, opt, cov)
+    Lgot = native_em.lower_bound(vec, P, opt, cov, dict(consts, logOmega=logOm))
+    assert abs(Lgot - Lref) <= 1e-11 * abs(Lref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cov", [1, 0])
+def test_native_em_matches_python_em(vb, cov):
+    """vbhem_em_run (C++ loop) vs em.vbhem_h3m_c_step_fc (Python loop), same device E-step."""
+    import torch
+    from vbhem_amd import native_em
+    from vbhem_amd.em import vbhem_h3m_c_step_fc
+    from vbhem_amd.estep import EStepEngine
+    cs = make_case(300, 4, 3, 3, 2, cov, seed=31 + cov, tau=8)
+    opt = dict(cs["opt"], max_iter=6)
+    e1 = EStepEngine(cs["bs"], 4, 3, 8, device="cuda:0")
+    ref = vbhem_h3m_c_step_fc(cs["P"], e1, opt)
+    e2 = EStepEngine(cs["bs"], 4, 3, 8, device="cuda:0")
+    got = native_em.run(cs["P"], e2, opt)
+    assert got.iters == ref.iters and got.stable == ref.stable
+    np.testing.assert_allclose(got.LogLs, ref.LogLs, rtol=1e-11)
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert rel_err(getattr(got.post, k), getattr(ref.post, k)) < 1e-10, k
+    assert torch.equal(got.label, ref.label)
+
+
+@pytest.mark.gpu
+def test_native_em_c4_slice_vs_oracle(vb, vo):
+    """Three EM iterations on a 2,000-base C4 slice: the C++ loop vs the oracle EM."""
+    from vbhem_amd import native_em
+    from vbhem_amd.estep import EStepEngine
+    from cases import post_dict
+    base, P, opt = vb.synth_workload("C4", N=2000)
+    opt = dict(opt, max_iter=3)
+    eng = EStepEngine(base, P.K, P.S, opt["tau"], device="cuda:0")
+    res = native_em.run(P, eng, opt)
+    ref = vo.em_step_fc(post_dict(P), base.numpy(), opt)
+    np.testing.assert_allclose(res.LogLs, ref["LogLs"], rtol=RTOL_NORTH_STAR)
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert rel_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, k
