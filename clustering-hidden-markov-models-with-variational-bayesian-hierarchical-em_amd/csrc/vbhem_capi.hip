@@ -57,7 +57,8 @@ int hip_fail(hipError_t e, const char *where) {
 
 constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
-constexpr int kExactThreads = 256;                // fallback kernel threads
+constexpr int kExactThreads = vbhem::kExactBlock;  // fallback kernel threads
+constexpr int kChunkMinBases = 32;                 // fused epilogue: bases per chunk, at least
 constexpr size_t kGroupBudget = (size_t)8 << 30;  // per-pair buffers per group (fused)
 constexpr int kMaxSlabs = 512;    // statistics chunks (= resp/stats blocks per group)
 
@@ -326,9 +327,13 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
 }
 
 // W, bias, shift of the emission GEMM: once per call (depends on the clusters only)
-int run_emission_prep(FbCtx &c, double *W, double *bias, double *shift, hipStream_t st) {
+int run_emission_prep(FbCtx &c, double *W, double *bias, double *shift, hipStream_t st,
+                      int *zero_ints = nullptr, int n_zero = 0, double *Atg = nullptr,
+                      const double *logA = nullptr) {
   if (!c.split.ok) return VBHEM_OK;
   c.em.W = W; c.em.bias = bias; c.em.shift = shift;
+  c.em.zero_ints = zero_ints; c.em.n_zero = zero_ints ? n_zero : 0;
+  c.em.Atg = Atg; c.em.logA = logA;
   hipError_t e = vbhem::launch_emission_prep(c.em, st);
   if (e != hipSuccess) return hip_fail(e, "emission_prep_kernel");
   return VBHEM_OK;
@@ -354,8 +359,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
                 const int *list_tot, int list_cap, int *flags, double *scratch, double *LL,
                 hipStream_t st) {
   if (i_end <= i_begin) return VBHEM_OK;
-  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  // flags[0] is zero here: the backward pass's fb_exact_kernel reset it
   vbhem::SplitArgs ca = c.split.a;
   ca.mode = vbhem::kFbList;
   ca.E = Ebuf; ca.e_ld = e_ld;
@@ -364,7 +368,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   ca.flag_count = flags; ca.flag_list = flags + 2;
   ca.list = list; ca.list_tot = list_tot; ca.list_cap = list_cap;
   hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
-  e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_list), c.split.lds_list, st);
+  hipError_t e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_list), c.split.lds_list, st);
   if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
   if (g_timing.on) g_timing.gf.emplace_back(ev0, timing_event(st));
   vbhem::FbArgs a = c.plan.a;
@@ -390,8 +394,11 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
   a.flag_count = flags;
   a.flag_list = flags + 2;
-  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  hipError_t e = hipSuccess;
+  if (!c.split.ok) {  // split path: zeroed by emission_prep_kernel, reset by fb_exact_kernel
+    e = hipMemsetAsync(flags, 0, sizeof(int), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  }
   if (c.split.ok) {
     vbhem::EmissionArgs ea = c.em;
     ea.i_begin = i_begin; ea.i_end = i_end; ea.i_buf0 = i_buf0; ea.E = Ebuf; ea.e_ld = e_ld;
@@ -481,9 +488,11 @@ int estep_pairs_impl(const vbhem_base_t *base, const vbhem_cluster_t *clus, int 
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T, smooth);
   if (rc != VBHEM_OK) return rc;
-  hipError_t e0 = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
-  if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
-  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st);
+  if (!ctx.split.ok) {
+    hipError_t e0 = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
+    if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
+  }
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, 2);
   if (rc != VBHEM_OK) return rc;
   rc = run_fb(ctx, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.E,
               (long long)base->N * base->SB, w.flags,
@@ -559,11 +568,6 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   if (!vbhem::plan_stats(sa, slds, ngroups))
     return fail(VBHEM_ERR_UNSUPPORTED, "statistics tile does not fit (S or d too large)");
 
-  hipError_t e = hipMemsetAsync(w.slabs, 0, sizeof(double) * (size_t)w.nslab * w.slab_len, st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(slabs)");
-  e = hipMemsetAsync(w.flags + 1, 0, sizeof(int), st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flag total)");
-
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T);
   if (rc != VBHEM_OK) return rc;
@@ -573,13 +577,23 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
                      vbhem::plan_stats_list(sa, sl_lds);
   sa.gate_cnt = gated ? w.gate_cnt : nullptr;
   sa.list = w.list; sa.list_tot = w.list_tot; sa.list_cap = w.group;
-  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st);
-  if (rc != VBHEM_OK) return rc;
-  if (gated) {
-    ctx.bwd.a.Atg = w.Atg;
-    e = vbhem::launch_split_prep(ctx.bwd.a, w.Atg, st);
-    if (e != hipSuccess) return hip_fail(e, "split_prep_kernel");
+  // chunks of >= kChunkMinBases bases; the first group has the most, and in the
+  // gated schedule its kernels write (not add to) every entry of slabs [0, nslab_used)
+  auto chunks = [&w](int nb) { return std::min(w.nslab, (nb + kChunkMinBases - 1) / kChunkMinBases); };
+  const int nslab_used = std::max(1, chunks(std::min(base->N, w.group)));
+  hipError_t e = hipSuccess;
+  if (!gated || base->N == 0) {
+    e = hipMemsetAsync(w.slabs, 0, sizeof(double) * (size_t)nslab_used * w.slab_len, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(slabs)");
   }
+  if (!ctx.split.ok) {
+    e = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
+  }
+  if (gated) ctx.bwd.a.Atg = w.Atg;
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, 2, gated ? w.Atg : nullptr,
+                         clus->logA);
+  if (rc != VBHEM_OK) return rc;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);
     const long long e_ld = (long long)w.group * SB;
@@ -587,7 +601,8 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
                 st, gated ? vbhem::kFbBackward : vbhem::kFbDense);
     if (rc != VBHEM_OK) return rc;
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
-    const int nchunk = std::min(w.nslab, g1 - g0);
+    sa.assign = gated && g0 == 0;
+    const int nchunk = std::max(1, chunks(g1 - g0));
     hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
     e = vbhem::launch_resp(sa, nchunk, st);
     if (e != hipSuccess) return hip_fail(e, "resp_kernel");
@@ -607,7 +622,7 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
     }
     if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
-  e = vbhem::launch_stats_final(w.slabs, w.nslab, w.slab_len, stats_dev, st);
+  e = vbhem::launch_stats_final(w.slabs, nslab_used, w.slab_len, stats_dev, st);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
   return VBHEM_OK;
 }

@@ -26,6 +26,7 @@
 #include <cmath>
 
 #include "vbhem_internal.h"
+#include "vbhem_math.h"
 
 namespace vbhem {
 
@@ -47,18 +48,38 @@ __device__ __forceinline__ void packed_ab(int e, int d, int &a, int &b) {
 // ---------------------------------------------------------------------------
 // prep: z (mean of all cluster means), bias[K*S], W[KD][K*S]; one block per
 // cluster row r = (j, s), threads over the packed entries (every block forms z
-// in the same fixed order, block 0 publishes it)
+// in the same fixed order, block 0 publishes it).  Two per-call jobs ride along
+// so they cost no launch of their own: row r's A' = exp(logA - rowmax) for the
+// backward pass (p.Atg, gated schedule) and, in block 0, zeroing the fallback
+// counters (p.zero_ints).
 // ---------------------------------------------------------------------------
 constexpr int kPrepThreads = 64;
 
 __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArgs p) {
-  __shared__ double zs[64], pm[64];
+  __shared__ double zs[64], pm[64], zp[kPrepThreads];
   const int tid = threadIdx.x, d = p.d, KS = p.K * p.S, r = blockIdx.x;
   const bool full = p.covmode == kCovFull;
   const int NPF = full ? d * (d + 1) / 2 : d;
+  if (r == 0)
+    for (int x = tid; x < p.n_zero; x += kPrepThreads) p.zero_ints[x] = 0;
+  if (p.Atg && tid < p.S) {
+    const double *la = p.logA + (size_t)r * p.S;
+    double mx = la[0];
+    for (int s2 = 1; s2 < p.S; ++s2) mx = fmax(mx, la[s2]);
+    p.Atg[(size_t)r * p.S + tid] = exp_nonpos(la[tid] - mx);
+  }
+  // z: coordinate a = tid % d, the rows q = part, part + NP, ... summed by thread
+  // (a, part), then the NP parts of each coordinate in order (d <= 64)
+  const int NP = kPrepThreads / d, part = tid / d, a0 = tid - part * d;
+  if (part < NP) {
+    double s = 0.0;
+    for (int q = part; q < KS; q += NP) s += p.m[(size_t)q * d + a0];
+    zp[tid] = s;
+  }
+  __syncthreads();
   for (int a = tid; a < d; a += kPrepThreads) {
     double s = 0.0;
-    for (int q = 0; q < KS; ++q) s += p.m[(size_t)q * d + a];
+    for (int q = 0; q < NP; ++q) s += zp[q * d + a];
     zs[a] = s / (double)KS;
     if (r == 0) p.shift[a] = zs[a];
   }

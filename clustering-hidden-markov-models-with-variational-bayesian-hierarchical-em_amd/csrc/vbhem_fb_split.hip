@@ -636,24 +636,6 @@ void fb_split_kernel(const SplitArgs p) {
   }
 }
 
-// A' = exp(logA - rowmax) of every cluster in global memory (backward mode, LPC = 1)
-__global__ __launch_bounds__(256) void split_prep_kernel(const double *logA, int KS, int S,
-                                                         double *Atg) {
-  const int r = blockIdx.x * 256 + threadIdx.x;  // row (j, rho)
-  if (r >= KS) return;
-  const double *la = logA + (size_t)r * S;
-  double mx = la[0];
-  for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
-  for (int s2 = 0; s2 < S; ++s2) Atg[(size_t)r * S + s2] = exp_nonpos(la[s2] - mx);
-}
-
-hipError_t launch_split_prep(const SplitArgs &a, double *Atg, hipStream_t st) {
-  const int KS = a.K * a.S;
-  hipLaunchKernelGGL(split_prep_kernel, dim3((KS + 255) / 256), dim3(256), 0, st, a.logA, KS, a.S,
-                     Atg);
-  return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
 template <int S, int LPC, int MODE>
 static hipError_t launch_split_slm(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {

@@ -50,6 +50,7 @@ struct StatsArgs {
   int *list_tot;   // [K]
   int list_cap;
   int PB;          // pairs per batch of stats_list_kernel
+  int assign;      // gated schedule, first group: write the slab entries instead of adding
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).
@@ -83,6 +84,11 @@ struct EmissionArgs {
   double *W, *bias, *shift;  // [KD][K*S], [K*S], [d] (emission_prep_kernel)
   double *E;                 // [K*S][(i - i_buf0) * SB + b]  (row stride e_ld)
   double smooth;             // E /= smooth when != 1 (VHEM sibling)
+  // per-call side jobs of emission_prep_kernel
+  const double *logA;        // [K][S][S]
+  double *Atg;               // [K][S][S] A' = exp(logA - rowmax), or null
+  int *zero_ints;            // fallback counters zeroed by block 0, or null
+  int n_zero;
 };
 bool plan_emission(EmissionArgs &a, size_t &lds);
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st);
@@ -110,16 +116,16 @@ struct SplitArgs {
   int *flag_count, *flag_list;
   const int *list, *list_tot;  // kFbList: gated bases per cluster (gate_list_kernel)
   int list_cap;
-  const double *Atg;           // kFbBackward, LPC 1: [K][S][S] A' (split_prep_kernel)
+  const double *Atg;           // kFbBackward, LPC 1: [K][S][S] A' (emission_prep_kernel)
 };
 bool split_supported(int S, int SB, int d);
 int split_lpc(int S);      // lanes per column
 int split_lpc_bwd(int S);  // lanes per column, alternative for kFbBackward (BwdLPC)
 hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
 int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mode
-hipError_t launch_split_prep(const SplitArgs &a, double *Atg, hipStream_t st);
 
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
+constexpr int kExactBlock = 256;  // fb_exact_kernel: one block of this many threads
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
                            hipStream_t st);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t st);

@@ -361,9 +361,11 @@ __global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
 
 // ---------------------------------------------------------------------------
 // fb_exact_kernel: reference-order recursion for flagged pairs (one thread per
-// pair, Theta in global scratch).  Mirrors mex.c:715-1298 step by step.
+// pair, Theta in global scratch).  Mirrors mex.c:715-1298 step by step.  One
+// block: it consumes the pass's flag counter and resets it to zero on exit, so
+// the next pass needs no memset of its own (flag_count[1] keeps the total).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void fb_exact_kernel(const FbArgs p, double *scratch,
+__global__ __launch_bounds__(kExactBlock) void fb_exact_kernel(const FbArgs p, double *scratch,
                                                       size_t scratch_stride) {
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int nt = gridDim.x * blockDim.x;
@@ -474,6 +476,8 @@ __global__ __launch_bounds__(64) void fb_exact_kernel(const FbArgs p, double *sc
     }
     for (int k = 0; k < S * SB; ++k) p.tnu[lp * S * SB + k] = tn[k];
   }
+  __syncthreads();  // every thread has read the count
+  if (threadIdx.x == 0) *p.flag_count = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -548,7 +552,8 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
                            hipStream_t st) {
-  hipLaunchKernelGGL(fb_exact_kernel, dim3((nthreads + 63) / 64), dim3(64), 0, st, a, scratch, stride);
+  if (nthreads != kExactBlock) return hipErrorInvalidValue;  // single self-resetting block
+  hipLaunchKernelGGL(fb_exact_kernel, dim3(1), dim3(kExactBlock), 0, st, a, scratch, stride);
   return hipGetLastError();
 }
 

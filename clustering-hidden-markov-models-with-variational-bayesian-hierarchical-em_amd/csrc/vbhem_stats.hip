@@ -134,12 +134,13 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   for (int j = tid; j < K; j += kRespThreads) {
     double s = 0.0;
     for (int w = 0; w < NW * BPW; ++w) s += accNj[w * K + j];
-    slab[j] += s;
+    slab[j] = p.assign ? s : slab[j] + s;
   }
   if (tid < 2) {
     double s = 0.0;
     for (int w = 0; w < NW; ++w) s += accLt[2 * w + tid];
-    slab[(size_t)K + (size_t)K * p.S + (size_t)K * p.S * p.S + tid] += s;
+    double &dst = slab[(size_t)K + (size_t)K * p.S + (size_t)K * p.S * p.S + tid];
+    dst = p.assign ? s : dst + s;
   }
   if (p.gate_cnt)
     for (int j = tid; j < K; j += kRespThreads) p.gate_cnt[(size_t)blockIdx.x * K + j] = gcnt[j];
@@ -162,15 +163,35 @@ __global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs
   int *before = ish;          // [K] this chunk's offset in every cluster's list
   int *total = ish + K;       // [K]
   int *wcnt = ish + 2 * K;    // [NW]
-  for (int x = tid; x < 2 * K; x += kListThreads) ish[x] = 0;
-  __syncthreads();
-  for (int x = tid; x < nchunk * K; x += kListThreads) {
-    const int c = x / K, j = x - c * K;
-    const int v = p.gate_cnt[x];
-    atomicAdd(&total[j], v);
-    if (c < me) atomicAdd(&before[j], v);
+  // this chunk's offset (gate counts of chunks c < me) and cluster totals: thread
+  // (r, j) sums chunks c = r, r + R, ...; then the R partials of each j in order
+  int *pb = wcnt + NW;        // [R][K]
+  int *pt = pb + kListThreads;  // [R][K]
+  for (int j0 = 0; j0 < K; j0 += kListThreads) {
+    const int KC = min(K - j0, kListThreads), R = kListThreads / KC;
+    const int r = tid / KC, j = j0 + (tid - r * KC);
+    if (r < R) {
+      int sb = 0, stt = 0;
+      for (int c = r; c < nchunk; c += R) {
+        const int v = p.gate_cnt[(size_t)c * K + j];
+        stt += v;
+        sb += c < me ? v : 0;
+      }
+      pb[tid] = sb;
+      pt[tid] = stt;
+    }
+    __syncthreads();
+    if (tid < KC) {
+      int sb = 0, stt = 0;
+      for (int q = 0; q < R; ++q) {
+        sb += pb[q * KC + tid];
+        stt += pt[q * KC + tid];
+      }
+      before[j0 + tid] = sb;
+      total[j0 + tid] = stt;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (me == 0)
     for (int j = tid; j < K; j += kListThreads) p.list_tot[j] = total[j];
   int b0, b1;
@@ -300,14 +321,16 @@ __global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs 
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int o = o0 + tid + e * kSlThreads;
+      double *dst = nullptr;
       if (o < S) {
-        slab[K + (size_t)j * S + o] += acc[e];
+        dst = slab + K + (size_t)j * S + o;
       } else if (o < S + S * S) {
-        slab[K + (size_t)K * S + (size_t)j * S * S + (o - S)] += acc[e];
+        dst = slab + K + (size_t)K * S + (size_t)j * S * S + (o - S);
       } else if (o < NO) {
         const int oo = o - S - S * S;
-        slab[K + (size_t)K * S + (size_t)K * S * S + 2 + (size_t)j * S * NU + oo] += acc[e];
+        dst = slab + K + (size_t)K * S + (size_t)K * S * S + 2 + (size_t)j * S * NU + oo;
       }
+      if (dst) *dst = p.assign ? acc[e] : *dst + acc[e];
     }
   }
 }
@@ -649,7 +672,7 @@ hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
 }
 
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st) {
-  const size_t lds = ((size_t)2 * a.K + kListThreads / 64) * sizeof(int);
+  const size_t lds = ((size_t)2 * a.K + kListThreads / 64 + 2 * kListThreads) * sizeof(int);
   hipLaunchKernelGGL(gate_list_kernel, dim3(nchunk), dim3(kListThreads), lds, st, a);
   return hipGetLastError();
 }
