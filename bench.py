@@ -172,11 +172,15 @@ def main():
     eng.set_log_omega(logOm)
     tN = (float(opt["Nv"]) * N) * eng.base.omega
     allreduce = make_allreduce()
+    # the statistics land in pinned host memory (what the host M-step reads)
+    host_stats = torch.empty((eng.stats_len,), dtype=torch.float64, pin_memory=True)
 
     def step():
         st = eng.fused(tN)
         allreduce(st)
-        return st.cpu()
+        host_stats.copy_(st, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        return host_stats
 
     for _ in range(args.warmup):
         step()
@@ -191,6 +195,7 @@ def main():
         stats = step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    stats = stats.clone()
     _capi.timing_enable(False)
     if world > 1:
         dist.barrier()
@@ -219,6 +224,7 @@ def main():
     for _ in range(dense_steps):
         dstats = step()
     torch.cuda.synchronize()
+    dstats = dstats.clone()
     dtd = torch.tensor([time.perf_counter() - td0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dtd, op=dist.ReduceOp.MAX)

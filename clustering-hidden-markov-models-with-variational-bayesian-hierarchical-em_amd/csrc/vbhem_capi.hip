@@ -225,8 +225,8 @@ struct PairsWs {
   double *E, *W, *bias, *shift;  // emission GEMM (split path)
 };
 
-inline size_t emission_kd(int d, int covmode) {
-  return covmode == VBHEM_COV_FULL ? (size_t)d * (d + 1) / 2 + d : (size_t)2 * d;
+inline size_t emission_w_doubles(int d, int covmode, int K, int S) {
+  return (size_t)vbhem::emission_kdp(d, covmode) * vbhem::emission_ksp(K * S);
 }
 
 size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, bool need_tnu,
@@ -237,8 +237,8 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.scratch = cv.take<double>(exact_stride(c->S, b->SB, T) * kExactThreads);
   w.tnu = need_tnu ? cv.take<double>(np * c->S * b->SB) : nullptr;
   w.E = cv.take<double>(np * c->S * b->SB);
-  w.W = cv.take<double>(emission_kd(b->d, b->covmode) * c->K * c->S);
-  w.bias = cv.take<double>((size_t)c->K * c->S);
+  w.W = cv.take<double>(emission_w_doubles(b->d, b->covmode, c->K, c->S));
+  w.bias = cv.take<double>((size_t)vbhem::emission_ksp(c->K * c->S));
   w.shift = cv.take<double>((size_t)b->d);
   return cv.off + 256;
 }
@@ -275,8 +275,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.Z = cv.take<double>(g * K);
   w.slabs = cv.take<double>((size_t)w.nslab * w.slab_len);
   w.E = cv.take<double>(g * K * S * SB);
-  w.W = cv.take<double>(emission_kd(b->d, b->covmode) * K * S);
-  w.bias = cv.take<double>((size_t)K * S);
+  w.W = cv.take<double>(emission_w_doubles(b->d, b->covmode, K, S));
+  w.bias = cv.take<double>((size_t)vbhem::emission_ksp(K * S));
   w.shift = cv.take<double>((size_t)b->d);
   w.gate_cnt = cv.take<int>((size_t)w.nslab * K);
   w.list = cv.take<int>(g * K);
@@ -341,14 +341,7 @@ int run_emission_prep(FbCtx &c, double *W, double *bias, double *shift, hipStrea
 
 // Persistent grid of the list-mode pass: every resident block of the device.
 unsigned list_grid(const vbhem::SplitArgs &a, size_t lds) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 1)
-      cus = 256;
-  }
+  const int cus = vbhem::device_cus();
   const int per_cu = std::max(1, vbhem::split_resident_blocks(a, lds));
   return (unsigned)(cus * per_cu);
 }

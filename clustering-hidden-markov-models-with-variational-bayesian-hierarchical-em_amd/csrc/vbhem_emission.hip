@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
   const int NPF = full ? d * (d + 1) / 2 : d;
   if (r == 0)
     for (int x = tid; x < p.n_zero; x += kPrepThreads) p.zero_ints[x] = 0;
-  if (p.Atg && tid < p.S) {
+  if (p.Atg && tid < p.S && r < KS) {
     const double *la = p.logA + (size_t)r * p.S;
     double mx = la[0];
     for (int s2 = 1; s2 < p.S; ++s2) mx = fmax(mx, la[s2]);
@@ -84,6 +84,16 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
     if (r == 0) p.shift[a] = zs[a];
   }
   __syncthreads();
+  // W' = -W/2 and bias' = -bias/2 (exact scalings), so E = bias' + sum W' U;
+  // rows r >= K*S and k-rows e >= KD are the zero padding of the [kdp][ksp] layout
+  const int KSP = p.ksp;
+  double *Wc = p.W + r;  // column r, row stride ksp
+  if (r >= KS) {
+    for (int e = tid; e < p.kdp; e += kPrepThreads) Wc[(size_t)e * KSP] = 0.0;
+    if (tid == 0) p.bias[r] = 0.0;
+    return;
+  }
+  for (int e = p.KD + tid; e < p.kdp; e += kPrepThreads) Wc[(size_t)e * KSP] = 0.0;
   const double *mr = p.m + (size_t)r * d;
   if (full) {
     const double *P = p.P + (size_t)r * d * d;
@@ -94,25 +104,26 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
         v = fma(ps, mr[b] - zs[b], v);
       }
       pm[a] = v;
-      p.W[(size_t)(NPF + a) * KS + r] = -2.0 * v;
+      Wc[(size_t)(NPF + a) * KSP] = v;  // -(1/2)(-2 v)
     }
     for (int e = tid; e < NPF; e += kPrepThreads) {
       int a, b;
       packed_ab(e, d, a, b);
-      p.W[(size_t)e * KS + r] = (a == b) ? P[a * d + a] : 0.5 * (P[a * d + b] + P[b * d + a]);
+      Wc[(size_t)e * KSP] =
+          -0.5 * ((a == b) ? P[a * d + a] : 0.5 * (P[a * d + b] + P[b * d + a]));
     }
     __syncthreads();
     if (tid == 0) {
       double q = 0.0;
       for (int a = 0; a < d; ++a) q = fma(mr[a] - zs[a], pm[a], q);
-      p.bias[r] = d * kLog2PiE + p.c[r] + q;
+      p.bias[r] = -0.5 * (d * kLog2PiE + p.c[r] + q);
     }
   } else {
     const double *P = p.P + (size_t)r * d;
     for (int a = tid; a < d; a += kPrepThreads) {
       const double ma = mr[a] - zs[a];
-      p.W[(size_t)a * KS + r] = P[a];
-      p.W[(size_t)(d + a) * KS + r] = -2.0 * P[a] * ma;
+      Wc[(size_t)a * KSP] = -0.5 * P[a];
+      Wc[(size_t)(d + a) * KSP] = P[a] * ma;  // -(1/2)(-2 P m')
     }
     if (tid == 0) {
       double q = 0.0;
@@ -120,77 +131,79 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
         const double ma = mr[a] - zs[a];
         q = fma(P[a] * ma, ma, q);
       }
-      p.bias[r] = d * kLog2PiE + p.c[r] + q;
+      p.bias[r] = -0.5 * (d * kLog2PiE + p.c[r] + q);
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// emission_kernel: every wavefront independently walks tiles of 16 columns
-// (i,b).  The tile's covariances and means are contiguous in memory: the wave
-// loads them with coalesced 16-B loads into its private LDS slot (RAW), then
-// each lane forms, per k-step, the MFMA B operand U[4t + (l>>4)][l & 15] from
-// LDS; operand A (W, <= 50 KB) is read through L1/L2.  Rows are processed in
-// chunks of 8 row tiles (32 fp64 accumulators per lane).
+// The GEMM E[(j,s)][col] = bias'[(j,s)] + sum_e W'[e][(j,s)] U[e][col] on
+// v_mfma_f64_16x16x4f64: operand A = W' (16 rows x 4 k), operand B = U (4 k x 16
+// columns), C = 16 rows x 16 columns, lane l holding C[4v + (l>>4)][l & 15].
+// Every wavefront independently walks tiles of 16 columns (i,b); rows are
+// processed in chunks of 8 row tiles (32 fp64 accumulators per lane), all 8
+// always issued (W' is zero-padded to a multiple of 128 rows).
 // ---------------------------------------------------------------------------
 constexpr int kEmRowChunk = 8;
-constexpr int kEmMaxKQ = 11;  // RAW path: KD <= 44 (d <= 8 full)
+constexpr int kEmRawChunk = 4;  // raw kernel: 4 row tiles per chunk (register budget)
 // doubles per wave: 16 cols x (d*d <= 64, d <= 8), rows padded to an odd stride
 // (dd + 1, d + 1) so the 16 lanes of a k-group read 16 different bank pairs
 constexpr int kEmRawSlot = 16 * 65 + 16 * 9;
 
 constexpr int kEmMaxThreads = 512;
 
-// RAW: the tile's covariances / means staged in LDS (d <= 8); WL: W staged in LDS
-// once per (persistent) block, operand A read by ds_read instead of L2 loads.
-template <bool RAW, bool WL>
-__global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p) {
+// emission_raw_kernel<KQ, WL, SM> (d <= 8): the tile's raw covariances and means
+// are loaded with coalesced 16-B loads, prefetched one tile ahead in registers,
+// and committed to the wave's private LDS slot; each lane then forms its whole
+// B operand U[4t + (l>>4)][l & 15], t < KQ, in registers from a per-lane operand
+// descriptor (u = raw[oA] + raw[oB] + f mu'_a mu'_b + g mu'_a).  The k-loop is
+// W' reads (LDS when WL, else L2) + MFMAs only; accumulators start at bias'.
+// KQ = k-steps (compile time: no k-loop branches); SM: E /= smooth (VHEM).
+template <int KQ, bool WL, bool SM>
+__global__ __launch_bounds__(kEmMaxThreads) void emission_raw_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NTH = blockDim.x, NW = NTH / 64;
-  const int d = p.d, SB = p.SB, KS = p.K * p.S, KD = p.KD;
+  const int d = p.d, SB = p.SB, KS = p.K * p.S, KSP = p.ksp;
   const bool full = p.covmode == kCovFull;
   const int NPF = full ? d * (d + 1) / 2 : d;
   const int dd = full ? d * d : d;
-  const int RT = (KS + 15) / 16, KQ = (KD + 3) / 4;
   const int ncols = (p.i_end - p.i_begin) * SB;
   const int nctile = (ncols + 15) / 16;
-  int *tab = reinterpret_cast<int *>(lds);                 // [KD] packed operand descriptor
-  double *Wl = lds + (KD + 1) / 2 + 1;                     // [KD][KS] (WL)
-  double *slots = Wl + (WL ? (size_t)KD * KS : 0);
+  double *bl = lds;                                    // [ksp] bias'
+  double *Wl = bl + KSP;                               // [4 KQ][ksp] (WL)
+  double *slots = Wl + (WL ? (size_t)4 * KQ * KSP : 0);
   double *slot = slots + wave * kEmRawSlot;
-  const int dds = dd | 1, ds = d | 1;                      // odd row strides
-  double *rawc = slot;                                     // [16][dds], [dd] = 0
-  double *mus = slot + 16 * dds;                           // [16][ds] (shifted by z)
-  double *zsh = slots + (RAW ? NW * kEmRawSlot : 0);      // [d] the shift z (RAW)
-  if (RAW)
-    for (int a = tid; a < d; a += NTH) zsh[a] = p.shift[a];
+  double *zsh = slots + NW * kEmRawSlot;               // [d] the shift z
+  const int dds = dd | 1, ds = d | 1;                  // odd row strides
+  double *rawc = slot;                                 // [16][dds], [dd] = 0
+  double *mus = slot + 16 * dds;                       // [16][ds] (shifted by z)
+  for (int a = tid; a < d; a += NTH) zsh[a] = p.shift[a];
+  for (int x = tid; x < KSP; x += NTH) bl[x] = p.bias[x];
   if (WL)
-    for (int x = tid; x < KD * KS; x += NTH) Wl[x] = p.W[x];
-  for (int e = tid; e < KD; e += NTH) {
-    int a, b, kind;
+    for (int x = tid; x < 4 * KQ * KSP; x += NTH) Wl[x] = p.W[x];
+  const int kl = lane >> 4, cl = lane & 15;
+  // this lane's operand descriptors, k-rows e = 4t + kl (e >= KD: u = 0)
+  int desc[KQ];
+#pragma unroll
+  for (int t = 0; t < KQ; ++t) {
+    const int e = 4 * t + kl;
+    int a = 0, b = 0, kind = 4;
     if (e < NPF) {
       a = b = e;
       if (full) packed_ab(e, d, a, b);
       kind = full ? (a == b ? 0 : 1) : 2;
-    } else {
+    } else if (e < NPF + d) {
       a = b = e - NPF;
       kind = 3;
     }
-    if (RAW) {
-      // u = raw[oA] + raw[oB] + f * mu'_a mu'_b + g * mu'_a, offsets within the column's
-      // padded covariance row (dd = its zero slot); dd <= 64, d <= 8 on this path
-      const int z = dd;
-      const int oA = kind == 0 ? a * d + a : kind == 1 ? a * d + b : kind == 2 ? a : z;
-      const int oB = kind == 1 ? b * d + a : z;
-      const int f = kind == 1 ? 2 : kind == 3 ? 0 : 1, g = kind == 3 ? 1 : 0;
-      tab[e] = oA | (oB << 7) | (a << 14) | (b << 18) | (f << 22) | (g << 24);
-    } else {
-      tab[e] = a | (b << 8) | (kind << 16);
-    }
+    const int z = dd;  // the zero slot of a padded covariance row
+    const int oA = kind == 0 ? a * d + a : kind == 1 ? a * d + b : kind == 2 ? a : z;
+    const int oB = kind == 1 ? b * d + a : z;
+    const int f = kind == 1 ? 2 : (kind == 3 || kind == 4) ? 0 : 1, g = kind == 3 ? 1 : 0;
+    desc[t] = oA | (oB << 7) | (a << 14) | (b << 18) | (f << 22) | (g << 24);
   }
   __syncthreads();
-  const int kl = lane >> 4, cl = lane & 15;
   const size_t ldE = (size_t)p.e_ld;
   const int wstride = gridDim.x * NW;
   int ct = blockIdx.x * NW + wave;
@@ -216,9 +229,125 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p)
     const double2 vm = ms[lane < nm2 ? lane : 0];
     pre_m = lane < nm2 ? vm : make_double2(0.0, 0.0);
   };
-  if (RAW && ct < nctile) prefetch(ct);
+  if (ct < nctile) prefetch(ct);
+  const double *Wsrc = WL ? Wl : p.W;
 
   for (; ct < nctile; ct += wstride) {
+    const int c0 = ct * 16;
+    const int ccount = min(16, ncols - c0);
+    const bool cv = cl < ccount;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // previous tile's LDS reads done
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int x = lane + 64 * k;  // elements 2x, 2x+1 of the tile's [16][dd] block
+      if (x < 8 * dd) {
+        const int c = (2 * x) / dd, o = 2 * x - c * dd;  // dd even: the pair stays in a row
+        rawc[c * dds + o] = pre_c[k].x;
+        rawc[c * dds + o + 1] = pre_c[k].y;
+      }
+    }
+    if (lane < 16) rawc[lane * dds + dd] = 0.0;  // the zero slot of every column
+    if (lane < 8 * d) {
+      const int c = (2 * lane) / d, o = 2 * lane - c * d;
+      mus[c * ds + o] = pre_m.x - zsh[o];
+      mus[c * ds + o + 1] = pre_m.y - zsh[o + 1];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (ct + wstride < nctile) prefetch(ct + wstride);  // next tile, overlaps the MFMAs
+    double ub[KQ];
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) {
+      const int tb = desc[t];
+      const int oA = tb & 127, oB = (tb >> 7) & 127, a = (tb >> 14) & 15, b = (tb >> 18) & 15;
+      const double f = (double)((tb >> 22) & 3), g = (double)((tb >> 24) & 1);
+      const double ma = mus[cl * ds + a], mb = mus[cl * ds + b];
+      const double caa = rawc[cl * dds + oA] + rawc[cl * dds + oB];
+      const double u = fma(f * ma, mb, fma(g, ma, caa));
+      ub[t] = cv ? u : 0.0;
+    }
+    double *Ec = p.E + (size_t)(p.i_begin - p.i_buf0) * SB + c0 + cl;  // this lane's column
+    // row stride laundered per tile: otherwise the 32 loop-invariant row offsets
+    // (64-bit) are hoisted out of the tile loop and the kernel spills
+    size_t ldT = ldE;
+    int kspT = KSP;
+    asm volatile("" : "+s"(ldT), "+s"(kspT));
+    for (int r0 = 0; r0 < KSP; r0 += 16 * kEmRawChunk) {
+      double4_t acc[kEmRawChunk];
+      const double *br = bl + r0 + kl;
+      asm volatile("" : "+v"(br));
+#pragma unroll
+      for (int q = 0; q < kEmRawChunk; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[q][v] = br[q * 16 + 4 * v];
+      double wc[kEmRawChunk], wn[kEmRawChunk];
+      const double *Wr = Wsrc + (size_t)kl * kspT + r0 + cl;
+      asm volatile("" : "+v"(Wr));
+#pragma unroll
+      for (int q = 0; q < kEmRawChunk; ++q) wc[q] = Wr[q * 16];
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        if (t + 1 < KQ) {
+#pragma unroll
+          for (int q = 0; q < kEmRawChunk; ++q) wn[q] = Wr[(size_t)4 * (t + 1) * kspT + q * 16];
+        }
+#pragma unroll
+        for (int q = 0; q < kEmRawChunk; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], ub[t], acc[q], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < kEmRawChunk; ++q) wc[q] = wn[q];
+      }
+      if (cv) {
+#pragma unroll
+        for (int q = 0; q < kEmRawChunk; ++q)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int row = r0 + q * 16 + kl + 4 * v;
+            if (row < KS) Ec[(size_t)row * ldT] = SM ? acc[q][v] / p.smooth : acc[q][v];
+          }
+      }
+    }
+  }
+}
+
+// emission_gen_kernel<WL> (d > 8): operand B formed per k-step from the column's
+// covariances and means read through L1/L2.
+template <bool WL>
+__global__ __launch_bounds__(kEmMaxThreads) void emission_gen_kernel(EmissionArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NTH = blockDim.x, NW = NTH / 64;
+  const int d = p.d, SB = p.SB, KS = p.K * p.S, KD = p.KD, KSP = p.ksp;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d;
+  const int dd = full ? d * d : d;
+  const int KQ = p.kdp / 4;
+  const int ncols = (p.i_end - p.i_begin) * SB;
+  const int nctile = (ncols + 15) / 16;
+  int *tab = reinterpret_cast<int *>(lds);                 // [KD] packed operand descriptor
+  double *Wl = lds + (KD + 1) / 2 + 1;                     // [kdp][ksp] (WL)
+  if (WL)
+    for (int x = tid; x < p.kdp * KSP; x += NTH) Wl[x] = p.W[x];
+  for (int e = tid; e < KD; e += NTH) {
+    int a, b, kind;
+    if (e < NPF) {
+      a = b = e;
+      if (full) packed_ab(e, d, a, b);
+      kind = full ? (a == b ? 0 : 1) : 2;
+    } else {
+      a = b = e - NPF;
+      kind = 3;
+    }
+    tab[e] = a | (b << 8) | (kind << 16);
+  }
+  __syncthreads();
+  const int kl = lane >> 4, cl = lane & 15;
+  const size_t ldE = (size_t)p.e_ld;
+  const int wstride = gridDim.x * NW;
+  const double *Wsrc = WL ? Wl : p.W;
+  for (int ct = blockIdx.x * NW + wave; ct < nctile; ct += wstride) {
     const int c0 = ct * 16;
     const int ccount = min(16, ncols - c0);
     const int col = c0 + cl;
@@ -226,114 +355,50 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_kernel(EmissionArgs p)
     const size_t g0 = (size_t)p.i_begin * SB + c0;
     const double *Cg = p.covars + (g0 + (cv ? cl : 0)) * dd;
     const double *Mg = p.centres + (g0 + (cv ? cl : 0)) * d;
-    if (RAW) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // previous tile's LDS reads done
-#pragma unroll
-      for (int k = 0; k < kPre; ++k) {
-        const int x = lane + 64 * k;  // elements 2x, 2x+1 of the tile's [16][dd] block
-        if (x < 8 * dd) {
-          const int c = (2 * x) / dd, o = 2 * x - c * dd;  // dd even: the pair stays in a row
-          rawc[c * dds + o] = pre_c[k].x;
-          rawc[c * dds + o + 1] = pre_c[k].y;
-        }
-      }
-      if (lane < 16) rawc[lane * dds + dd] = 0.0;  // the zero slot of every column
-      if (lane < 8 * d) {
-        const int c = (2 * lane) / d, o = 2 * lane - c * d;
-        mus[c * ds + o] = pre_m.x - zsh[o];
-        mus[c * ds + o + 1] = pre_m.y - zsh[o + 1];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (ct + wstride < nctile) prefetch(ct + wstride);  // next tile, overlaps the MFMAs
-    }
     const size_t cbuf = (size_t)(p.i_begin - p.i_buf0) * SB + col;
-    // RAW: the whole B operand of the tile (this lane's k-rows 4t + kl of column cl)
-    // built once into registers, so the k-loop is W reads + MFMAs only
-    double ub[kEmMaxKQ];
-    if (RAW) {
-#pragma unroll
-      for (int t = 0; t < kEmMaxKQ; ++t) {
-        const int e = 4 * t + kl;
-        double u = 0.0;
-        if (t < KQ && e < KD) {
-          const int tb = tab[e];
-          const int oA = tb & 127, oB = (tb >> 7) & 127, a = (tb >> 14) & 15, b = (tb >> 18) & 15;
-          const double f = (double)((tb >> 22) & 3), g = (double)((tb >> 24) & 1);
-          const double ma = mus[cl * ds + a], mb = mus[cl * ds + b];
-          const double caa = rawc[cl * dds + oA] + rawc[cl * dds + oB];
-          u = cv ? fma(f * ma, mb, fma(g, ma, caa)) : 0.0;
-        }
-        ub[t] = u;
-      }
-    }
-    for (int r0 = 0; r0 < RT; r0 += kEmRowChunk) {
+    for (int r0 = 0; r0 < KSP; r0 += 16 * kEmRowChunk) {
       double4_t acc[kEmRowChunk];
 #pragma unroll
-      for (int q = 0; q < kEmRowChunk; ++q) acc[q] = (double4_t){0.0, 0.0, 0.0, 0.0};
-      // W (operand A) for k-step t, software-pipelined one step ahead
+      for (int q = 0; q < kEmRowChunk; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[q][v] = p.bias[r0 + q * 16 + kl + 4 * v];
       double wc[kEmRowChunk], wn[kEmRowChunk];
-      auto loadw = [&](int t, double (&w)[kEmRowChunk]) {
+      const double *Wr = Wsrc + (size_t)kl * KSP + r0 + cl;
+#pragma unroll
+      for (int q = 0; q < kEmRowChunk; ++q) wc[q] = Wr[q * 16];
+      for (int t = 0; t < KQ; ++t) {
+        if (t + 1 < KQ) {
+#pragma unroll
+          for (int q = 0; q < kEmRowChunk; ++q) wn[q] = Wr[(size_t)4 * (t + 1) * KSP + q * 16];
+        }
         const int e = 4 * t + kl;
-        const double *We = (WL ? Wl : p.W) + (size_t)(e < KD ? e : 0) * KS;
-#pragma unroll
-        for (int q = 0; q < kEmRowChunk; ++q) {
-          const int row = (r0 + q) * 16 + cl;
-          w[q] = (e < KD && row < KS) ? We[row] : 0.0;
+        double u = 0.0;
+        if (e < KD) {
+          const int tb = tab[e];
+          const int a = tb & 0xff, b = (tb >> 8) & 0xff, kind = tb >> 16;
+          const double ma = Mg[a] - p.shift[a], mb = Mg[b] - p.shift[b];
+          double caa = kind <= 1 ? Cg[a * d + b] : (kind == 2 ? Cg[a] : 0.0);
+          if (kind == 1) caa += Cg[b * d + a];
+          u = kind == 3 ? ma : (kind == 1 ? fma(2.0 * ma, mb, caa) : fma(ma, ma, caa));
+          u = cv ? u : 0.0;
         }
-      };
-      loadw(0, wc);
-      if (RAW) {
 #pragma unroll
-        for (int t = 0; t < kEmMaxKQ; ++t) {
-          if (t < KQ) {
-            if (t + 1 < KQ) loadw(t + 1, wn);
+        for (int q = 0; q < kEmRowChunk; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], u, acc[q], 0, 0, 0);
 #pragma unroll
-            for (int q = 0; q < kEmRowChunk; ++q)
-              if (r0 + q < RT)
-                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], ub[t], acc[q], 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
-          }
-        }
-      } else {
-        for (int t = 0; t < KQ; ++t) {
-          if (t + 1 < KQ) loadw(t + 1, wn);
-          const int e = 4 * t + kl;
-          double u = 0.0;
-          if (e < KD) {
-            const int tb = tab[e];
-            const int a = tb & 0xff, b = (tb >> 8) & 0xff, kind = tb >> 16;
-            const double ma = Mg[a] - p.shift[a], mb = Mg[b] - p.shift[b];
-            double caa = kind <= 1 ? Cg[a * d + b] : (kind == 2 ? Cg[a] : 0.0);
-            if (kind == 1) caa += Cg[b * d + a];
-            u = kind == 3 ? ma : (kind == 1 ? fma(2.0 * ma, mb, caa) : fma(ma, ma, caa));
-            u = cv ? u : 0.0;
-          }
-#pragma unroll
-          for (int q = 0; q < kEmRowChunk; ++q)
-            if (r0 + q < RT) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(wc[q], u, acc[q], 0, 0, 0);
-#pragma unroll
-          for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
-        }
+        for (int q = 0; q < kEmRowChunk; ++q) wc[q] = wn[q];
       }
       if (cv) {
 #pragma unroll
-        for (int q = 0; q < kEmRowChunk; ++q) {
-          const int rt = r0 + q;
-          if (rt < RT) {
+        for (int q = 0; q < kEmRowChunk; ++q)
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const int row = rt * 16 + kl + 4 * v;
-              if (row < KS) {
-                const double ev = -0.5 * (p.bias[row] + acc[q][v]);
-                p.E[(size_t)row * ldE + cbuf] = p.smooth != 1.0 ? ev / p.smooth : ev;
-              }
+          for (int v = 0; v < 4; ++v) {
+            const int row = r0 + q * 16 + kl + 4 * v;
+            if (row < KS) {
+              const double ev = acc[q][v];
+              p.E[(size_t)row * ldE + cbuf] = p.smooth != 1.0 ? ev / p.smooth : ev;
             }
           }
-        }
       }
     }
   }
@@ -345,43 +410,40 @@ bool plan_emission(EmissionArgs &a, size_t &lds) {
   const int d = a.d;
   if (d > 64) return false;
   a.KD = full ? d * (d + 1) / 2 + d : 2 * d;
+  a.kdp = emission_kdp(d, a.covmode);
+  a.ksp = emission_ksp(a.K * a.S);
   const int dd = full ? d * d : d;
   a.wfull = (dd <= 64 && d <= 8 && dd % 2 == 0 && d % 2 == 0);  // RAW: tile staged in LDS
-  // 8 waves per block with W in LDS when it fits one block per CU, else 4 waves
-  // reading W through L1/L2
-  const size_t head = ((size_t)(a.KD + 1) / 2 + 1 + d) * sizeof(double);
-  const size_t wbytes = (size_t)a.KD * a.K * a.S * sizeof(double);
-  const size_t slot = a.wfull ? (size_t)kEmRawSlot * sizeof(double) : 0;
-  a.wlds = head + wbytes + 8 * slot <= 160 * 1024;
-  a.nwave = a.wlds ? 8 : 4;
-  lds = head + (a.wlds ? wbytes : 0) + (size_t)a.nwave * slot;
+  // 8 waves per block with W' in LDS when it fits one block per CU, else 4 waves
+  // reading W' through L1/L2
+  const size_t wbytes = (size_t)a.kdp * a.ksp * sizeof(double);
+  if (a.wfull) {
+    const size_t head = ((size_t)a.ksp + d) * sizeof(double);
+    const size_t slot = (size_t)kEmRawSlot * sizeof(double);
+    a.wlds = head + wbytes + 8 * slot <= 160 * 1024;
+    a.nwave = a.wlds ? 8 : 4;
+    lds = head + (a.wlds ? wbytes : 0) + (size_t)a.nwave * slot;
+  } else {
+    const size_t head = ((size_t)(a.KD + 1) / 2 + 1) * sizeof(double);
+    a.wlds = head + wbytes <= 160 * 1024;
+    a.nwave = a.wlds ? 8 : 4;
+    lds = head + (a.wlds ? wbytes : 0);
+  }
   a.CB = 16;
   return true;
 }
 
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st) {
-  hipLaunchKernelGGL(emission_prep_kernel, dim3(a.K * a.S), dim3(kPrepThreads), 0, st, a);
+  hipLaunchKernelGGL(emission_prep_kernel, dim3(a.ksp), dim3(kPrepThreads), 0, st, a);
   return hipGetLastError();
 }
 
-template <bool RAW, bool WL>
-static hipError_t launch_emission_t(const EmissionArgs &a, size_t lds, hipStream_t st) {
-  auto *fn = &emission_kernel<RAW, WL>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+template <typename F>
+static hipError_t launch_emission_fn(F *fn, const EmissionArgs &a, size_t lds, hipStream_t st) {
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 1)
-      cus = 256;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, a.nwave * 64, lds) != hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
+  const int cus = device_cus();
+  const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), a.nwave * 64, lds);
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   const int nctile = (ncols + 15) / 16;
   // persistent: every resident block, every wave walks 16-column tiles
@@ -390,13 +452,33 @@ static hipError_t launch_emission_t(const EmissionArgs &a, size_t lds, hipStream
   return hipGetLastError();
 }
 
+template <int KQ>
+static hipError_t launch_raw_kq(const EmissionArgs &a, size_t lds, hipStream_t st) {
+  const bool sm = a.smooth != 1.0;
+  if (a.wlds) return sm ? launch_emission_fn(&emission_raw_kernel<KQ, true, true>, a, lds, st)
+                        : launch_emission_fn(&emission_raw_kernel<KQ, true, false>, a, lds, st);
+  return sm ? launch_emission_fn(&emission_raw_kernel<KQ, false, true>, a, lds, st)
+            : launch_emission_fn(&emission_raw_kernel<KQ, false, false>, a, lds, st);
+}
+
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   if (ncols <= 0) return hipSuccess;
-  if (a.wfull) return a.wlds ? launch_emission_t<true, true>(a, lds, st)
-                             : launch_emission_t<true, false>(a, lds, st);
-  return a.wlds ? launch_emission_t<false, true>(a, lds, st)
-                : launch_emission_t<false, false>(a, lds, st);
+  if (a.wfull) {
+    // KD = d(d+1)/2 + d (full) or 2d (diag), d <= 8 even: k-steps 2, 4, 7, 11 (full),
+    // 1, 2, 3, 4 (diag)
+    switch (a.kdp / 4) {
+      case 1: return launch_raw_kq<1>(a, lds, st);
+      case 2: return launch_raw_kq<2>(a, lds, st);
+      case 3: return launch_raw_kq<3>(a, lds, st);
+      case 4: return launch_raw_kq<4>(a, lds, st);
+      case 7: return launch_raw_kq<7>(a, lds, st);
+      case 11: return launch_raw_kq<11>(a, lds, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  return a.wlds ? launch_emission_fn(&emission_gen_kernel<true>, a, lds, st)
+                : launch_emission_fn(&emission_gen_kernel<false>, a, lds, st);
 }
 
 }  // namespace vbhem

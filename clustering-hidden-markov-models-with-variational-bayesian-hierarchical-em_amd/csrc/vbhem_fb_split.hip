@@ -640,8 +640,7 @@ void fb_split_kernel(const SplitArgs p) {
 template <int S, int LPC, int MODE>
 static hipError_t launch_split_slm(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
   auto *fn = &fb_split_kernel<S, LPC, MODE>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((fb_split_kernel<S, LPC, MODE>), dim3(grid), dim3(a.nwb * 64), lds, st, a);
   return hipGetLastError();
@@ -658,13 +657,8 @@ static hipError_t launch_split_sl(const SplitArgs &a, unsigned grid, size_t lds,
 
 template <int S, int LPC, int MODE>
 static int resident_slm(const SplitArgs &a, size_t lds) {
-  int n = 0;
-  if (hipFuncSetAttribute(reinterpret_cast<const void *>(&fb_split_kernel<S, LPC, MODE>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_split_kernel<S, LPC, MODE>, a.nwb * 64,
-                                                   lds) != hipSuccess)
-    return 1;
-  return n;
+  return resident_per_cu(reinterpret_cast<const void *>(&fb_split_kernel<S, LPC, MODE>),
+                         a.nwb * 64, lds);
 }
 
 template <int S>

@@ -4,8 +4,53 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 namespace vbhem {
+
+// Host-side launch helpers: the dynamic-LDS attribute and the occupancy query
+// are per (kernel, block, LDS) facts, so they are asked once and remembered
+// (every fused E-step launches the same kernels with the same geometry).
+inline hipError_t set_dyn_lds(const void *fn, size_t lds) {
+  static std::mutex mu;
+  static std::map<const void *, size_t> done;  // largest LDS size already allowed
+  std::lock_guard<std::mutex> g(mu);
+  auto it = done.find(fn);
+  if (it != done.end() && it->second >= lds) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) done[fn] = lds;
+  return e;
+}
+inline int resident_per_cu(const void *fn, int threads, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void *, int, size_t>, int> memo;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = memo.find(std::make_tuple(fn, threads, lds));
+    if (it != memo.end()) return it->second;
+  }
+  int n = 0;
+  if (set_dyn_lds(fn, lds) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, lds) != hipSuccess || n < 1)
+    return 1;  // not remembered: ask again next time
+  std::lock_guard<std::mutex> g(mu);
+  memo[std::make_tuple(fn, threads, lds)] = n;
+  return n;
+}
+inline int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    else
+      return 256;
+  }
+  return cus;
+}
 
 constexpr int kCovDiag = 0;
 constexpr int kCovFull = 1;
@@ -73,15 +118,24 @@ struct SplitLayout {
   static constexpr int OFF_X = (HEAD + 1) / 2 * 2;
 };
 // K1 emission GEMM (vbhem_emission.hip)
+// W' / bias' padding of the emission GEMM: k-rows to a multiple of 4 (MFMA k-step),
+// rows (j, s) to a multiple of 128 (a chunk of 8 MFMA row tiles)
+inline int emission_kdp(int d, int covmode) {
+  const int kd = covmode == kCovFull ? d * (d + 1) / 2 + d : 2 * d;
+  return (kd + 3) / 4 * 4;
+}
+inline int emission_ksp(int ks) { return (ks + 127) / 128 * 128; }
+
 struct EmissionArgs {
   int SB, d, covmode, K, S, KD, CB;
+  int kdp, ksp;  // padded W' dims: [kdp][ksp], bias' [ksp]
   bool wfull;  // column tiles staged in LDS (d <= 8); else read through L1/L2
   bool wlds;   // W staged in LDS (8-wave blocks); else read through L1/L2 (4-wave blocks)
   int nwave;
   int i_begin, i_end, i_buf0;
   long long e_ld;  // row stride of E = (bases in the buffer) * SB
   const double *centres, *covars, *m, *P, *c;
-  double *W, *bias, *shift;  // [KD][K*S], [K*S], [d] (emission_prep_kernel)
+  double *W, *bias, *shift;  // W' = -W/2 [kdp][ksp], bias' = -bias/2 [ksp], z [d] (emission_prep_kernel)
   double *E;                 // [K*S][(i - i_buf0) * SB + b]  (row stride e_ld)
   double smooth;             // E /= smooth when != 1 (VHEM sibling)
   // per-call side jobs of emission_prep_kernel

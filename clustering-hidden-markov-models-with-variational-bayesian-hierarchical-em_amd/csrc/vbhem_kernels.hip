@@ -528,8 +528,7 @@ __global__ __launch_bounds__(256) void pair_emit_kernel(EmitArgs p) {
 // ---------------------------------------------------------------------------
 template <int D>
 static hipError_t launch_fb_d(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&fb_pairs_kernel<D>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&fb_pairs_kernel<D>), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(fb_pairs_kernel<D>, grid, block, lds, st, a);
   return hipGetLastError();

@@ -640,8 +640,7 @@ bool plan_stats(StatsArgs &a, size_t &lds, int &ngroups) {
 template <int TPW>
 static hipError_t launch_stats_t(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
                                  hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_kernel<TPW>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&stats_kernel<TPW>), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((stats_kernel<TPW>), dim3(nchunk, ngroups), dim3(kStatsThreads), lds, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -701,8 +700,7 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   if (NO <= 4 * kSlThreads) {
     hipLaunchKernelGGL((stats_list_kernel<4>), grid, dim3(kSlThreads), lds, st, a);
   } else {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&stats_list_kernel<8>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&stats_list_kernel<8>), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((stats_list_kernel<8>), grid, dim3(kSlThreads), lds, st, a);
   }
