@@ -312,7 +312,7 @@ void fb_split_kernel(const SplitArgs p) {
         double ex[SH];
 #pragma unroll
         for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
-        if constexpr (kTab) exp_tab_n<SH>(G, ex, etab);
+        if constexpr (kTab) exp_tabf_n<SH>(G, ex, etab);
         else exp_nonpos_n<SH>(G, ex);
       }
       // partial Z for every owner's rows, then reduce-scatter
@@ -349,7 +349,7 @@ void fb_split_kernel(const SplitArgs p) {
         bad |= bvalid && rv && !(Z[k] >= kZMinS);
         zz[k] = rv ? Z[k] : 1.0;
       }
-      if constexpr (kTab) log_tab_n<SH>(lz, zz, ltab);
+      if constexpr (kTab) log_tabf_n<SH>(lz, zz, ltab);
       else log_pos_n<SH>(lz, zz);
 #pragma unroll
       for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];

@@ -274,4 +274,89 @@ __host__ __device__ __forceinline__ double log_tab(double z, const double *tab) 
   return y[0];
 }
 
+// ---- reduced-operation variants for the backward-only pass ----
+// The backward pass evaluates one exp and one log per (sigma, b) element and step
+// and is VALU-issue bound, so these drop the compensation terms that buy the last
+// ulp:
+//   log_tabf_n: y = fma(q, r^2, r) + fma(k, ln2, logc)   (no hi/lo split of k ln2
+//     and logc, no TwoSum of the final add): <= 2 ulp on [1e-200, 1e3]
+//     (tests/test_math.py); 12 fp64 ops instead of 17.
+//   exp_tabf_n: 2^(j/256) without its low part (th (1 + p) as one fma): <= 2 ulp
+//     on [-700, 0]; 12 fp64 ops instead of 13.
+template <int N>
+__host__ __device__ __forceinline__ void log_tabf_n(double (&y)[N], const double (&z)[N],
+                                                    const double *tab) {
+  constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned hi = (unsigned)__double2hiint(z[i]);
+    const int lo = __double2loint(z[i]);
+#else
+    unsigned long long bits;
+    __builtin_memcpy(&bits, &z[i], 8);
+    const unsigned hi = (unsigned)(bits >> 32);
+    const unsigned lo = (unsigned)bits;
+#endif
+    const unsigned t = hi - 0x3fe60000u;
+    const int idx = (int)((t >> 13) & 127u);
+    const int k = (int)t >> 20;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double zz = __hiloint2double((int)(hi - (t & 0xfff00000u)), lo);
+    const double2 e01 = *reinterpret_cast<const double2 *>(__builtin_assume_aligned(tab + 4 * idx, 16));
+    const double invc = e01.x, lch = e01.y;
+#else
+    const unsigned long long zb = ((unsigned long long)(hi - (t & 0xfff00000u)) << 32) | lo;
+    double zz;
+    __builtin_memcpy(&zz, &zb, 8);
+    const double invc = tab[4 * idx], lch = tab[4 * idx + 1];
+#endif
+    const double r = fma(zz, invc, -1.0);
+    const double w = fma((double)k, kLn2, lch);
+    const double r2 = r * r;
+    double q = fma(r, -1.0 / 8.0, 1.0 / 7.0);
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -1.0 / 4.0);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    y[i] = fma(q, r2, r) + w;
+  }
+}
+
+template <int N>
+__host__ __device__ __forceinline__ void exp_tabf_n(double (&y)[N], const double (&xin)[N],
+                                                    const double *tab) {
+  constexpr double kInvLn2N = 369.3299304675746;      // 256 / ln 2
+  constexpr double kLn2NHi = 0x1.62e42ff000000p-9;    // ln 2 / 256, 33 bits
+  constexpr double kLn2NLo = -0x1.718432a1b0e26p-43;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double x = fmax(xin[i], -800.0);
+    const double n = rint(x * kInvLn2N);
+    double r = fma(-n, kLn2NHi, x);
+    r = fma(-n, kLn2NLo, r);
+    const int ni = (int)n;
+    const int j = ni & 255, k = ni >> 8;
+    const double th = tab[2 * j];
+    const double q = fma(fma(r, 1.0 / 24.0, 1.0 / 6.0), r, 0.5);
+    const double p = fma(q, r * r, r);
+    y[i] = ldexp(fma(th, p, th), k);
+  }
+}
+
+__host__ __device__ __forceinline__ double exp_tabf(double x, const double *tab) {
+  double y[1];
+  const double xin[1] = {x};
+  exp_tabf_n<1>(y, xin, tab);
+  return y[0];
+}
+
+__host__ __device__ __forceinline__ double log_tabf(double z, const double *tab) {
+  double y[1];
+  const double zin[1] = {z};
+  log_tabf_n<1>(y, zin, tab);
+  return y[0];
+}
+
 }  // namespace vbhem

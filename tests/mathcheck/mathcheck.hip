@@ -26,7 +26,7 @@ __global__ void math_kernel(int n, const double* __restrict__ x, double* __restr
 }
 
 __global__ void logtab_kernel(int n, const double* __restrict__ x, double* __restrict__ l,
-                              double* __restrict__ e) {
+                              double* __restrict__ e, int fast) {
   __shared__ __attribute__((aligned(16))) double tab[vbhem::kLogTabDoubles];
   __shared__ __attribute__((aligned(16))) double etab[vbhem::kExpTabDoubles];
   for (int k = threadIdx.x; k < vbhem::kLogTabDoubles; k += blockDim.x) tab[k] = kLogTabDev[k];
@@ -34,8 +34,13 @@ __global__ void logtab_kernel(int n, const double* __restrict__ x, double* __res
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    l[i] = vbhem::log_tab(x[i], tab);
-    e[i] = vbhem::exp_tab(-x[i], etab);
+    if (fast) {
+      l[i] = vbhem::log_tabf(x[i], tab);
+      e[i] = vbhem::exp_tabf(-x[i], etab);
+    } else {
+      l[i] = vbhem::log_tab(x[i], tab);
+      e[i] = vbhem::exp_tab(-x[i], etab);
+    }
   }
 }
 
@@ -52,7 +57,8 @@ void mathcheck_host(int n, const double* x, double* e, double* l, double* r) {
   }
 }
 
-// table-driven log / exp (backward sweep): log at x, exp at -x; host / device
+// table-driven log / exp: log at x, exp at -x; host / device; the *f variants are
+// the reduced-operation pair of the backward-only pass
 void logtab_host(int n, const double* x, double* l, double* e) {
   for (int i = 0; i < n; i++) {
     l[i] = vbhem::log_tab(x[i], kLogTabHost);
@@ -60,7 +66,14 @@ void logtab_host(int n, const double* x, double* l, double* e) {
   }
 }
 
-int logtab_device(int n, const double* x, double* l, double* e) {
+void logtabf_host(int n, const double* x, double* l, double* e) {
+  for (int i = 0; i < n; i++) {
+    l[i] = vbhem::log_tabf(x[i], kLogTabHost);
+    e[i] = vbhem::exp_tabf(-x[i], kExpTabHost);
+  }
+}
+
+static int logtab_device_impl(int n, const double* x, double* l, double* e, int fast) {
   double *dx = nullptr, *dl = nullptr, *de = nullptr;
   const size_t bytes = sizeof(double) * (size_t)(n > 0 ? n : 1);
   hipError_t st = hipMalloc(&dx, bytes);
@@ -68,7 +81,7 @@ int logtab_device(int n, const double* x, double* l, double* e) {
   if (st == hipSuccess) st = hipMalloc(&de, bytes);
   if (st == hipSuccess) st = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
   if (st == hipSuccess && n > 0) {
-    logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
+    logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de, fast);
     st = hipGetLastError();
   }
   if (st == hipSuccess) st = hipMemcpy(l, dl, sizeof(double) * n, hipMemcpyDeviceToHost);
@@ -77,6 +90,14 @@ int logtab_device(int n, const double* x, double* l, double* e) {
   (void)hipFree(dl);
   (void)hipFree(de);
   return (int)st;
+}
+
+int logtab_device(int n, const double* x, double* l, double* e) {
+  return logtab_device_impl(n, x, l, e, 0);
+}
+
+int logtabf_device(int n, const double* x, double* l, double* e) {
+  return logtab_device_impl(n, x, l, e, 1);
 }
 
 // Same on device 0 (host arrays in/out).  Returns 0 or a hipError_t.

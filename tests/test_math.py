@@ -82,3 +82,28 @@ def test_logtab_host_build(mathcheck):
 @pytest.mark.gpu
 def test_logtab_device_build(mathcheck):
     assert _check_logtab(mathcheck.logtab_device) == 0
+
+
+def _check_logtabf(fn):
+    """Reduced-operation pair of the backward-only pass (log_tabf_n / exp_tabf_n):
+    <= 2 ulp (log) and <= 2 ulp (exp) on the same samples."""
+    x = _samples()
+    x = np.concatenate([x, np.random.default_rng(7).uniform(0.99, 1.01, N // 4)])
+    dp = ctypes.POINTER(ctypes.c_double)
+    l, e = np.zeros_like(x), np.zeros_like(x)
+    rc = fn(len(x), x.ctypes.data_as(dp), l.ctypes.data_as(dp), e.ctypes.data_as(dp))
+    pos = x >= 1e-200
+    assert _ulps(l[pos], np.log(x[pos])).max() <= 2.0
+    assert l[2] == 0.0
+    m = x <= 700
+    assert _ulps(e[m], np.exp(-x[m])).max() <= 2.0
+    return rc
+
+
+def test_logtabf_host_build(mathcheck):
+    _check_logtabf(mathcheck.logtabf_host)
+
+
+@pytest.mark.gpu
+def test_logtabf_device_build(mathcheck):
+    assert _check_logtabf(mathcheck.logtabf_device) == 0
