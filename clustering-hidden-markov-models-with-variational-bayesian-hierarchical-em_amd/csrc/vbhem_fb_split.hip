@@ -39,8 +39,8 @@ namespace {
 constexpr double kZMinS = 1e-200;
 
 // log_tab_n's table (backward mode stages it in LDS once per persistent block)
-__device__ const double kLogTab[kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
-__device__ const double kExpTab[kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
+alignas(16) __device__ const double kLogTab[kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
+alignas(16) __device__ const double kExpTab[kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
 
 // ---- DPP lane exchange inside aligned lane quads -------------------------------
 template <int CTRL>
@@ -200,8 +200,10 @@ void fb_split_kernel(const SplitArgs p) {
   double *lpi = amax + S;        // [S]
   double *R = lds + p.off_R;     // lattice [(T-2)][SH][NT]
   int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
-  double *ltab = lds + p.off_T;                // [kLogTabDoubles] (kTab)
-  double *etab = ltab + kLogTabDoubles;        // [kExpTabDoubles] (kTab)
+  // backward mode: the tables staged in LDS; the other modes (LDS taken by the
+  // lattice) read them from global memory (8 KB, L1/L2-resident)
+  const double *ltab = kTab ? lds + p.off_T : kLogTab;  // [kLogTabDoubles]
+  const double *etab = kTab ? lds + p.off_T + kLogTabDoubles : kExpTab;  // [kExpTabDoubles]
 
   // ---------------- cluster constants: A' = exp(logA - rowmax), rowmax, logPi --------------
   auto stage_cluster = [&](int j) {
@@ -312,8 +314,7 @@ void fb_split_kernel(const SplitArgs p) {
         double ex[SH];
 #pragma unroll
         for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
-        if constexpr (kTab) exp_tabf_n<SH>(G, ex, etab);
-        else exp_nonpos_n<SH>(G, ex);
+        exp_tabf_n<SH>(G, ex, etab);
       }
       // partial Z for every owner's rows, then reduce-scatter
       double Pz[LPC * SH];
@@ -349,8 +350,7 @@ void fb_split_kernel(const SplitArgs p) {
         bad |= bvalid && rv && !(Z[k] >= kZMinS);
         zz[k] = rv ? Z[k] : 1.0;
       }
-      if constexpr (kTab) log_tabf_n<SH>(lz, zz, ltab);
-      else log_pos_n<SH>(lz, zz);
+      log_tabf_n<SH>(lz, zz, ltab);
 #pragma unroll
       for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];
       if (kFwd && t <= T - 2) {
@@ -439,7 +439,7 @@ void fb_split_kernel(const SplitArgs p) {
           double ex[SH];
 #pragma unroll
           for (int k = 0; k < SH; ++k) ex[k] = E[k] - M;
-          exp_nonpos_n<SH>(G, ex);
+          exp_tabf_n<SH>(G, ex, etab);  // the backward sweep's G_{T-1}, bit for bit
         } else {
           const double *slot = R + (size_t)(t - 1) * SH * NT + tid;
 #pragma unroll
@@ -578,8 +578,8 @@ void fb_split_kernel(const SplitArgs p) {
     // tiles.  XCD-aware when NB % 8 == 0: workgroups are dealt round-robin to the 8
     // XCDs (b % 8), so the K blocks that walk the same tiles (same base transitions,
     // read by all K clusters) are put on one XCD and share its L2.
-    for (int x = tid; x < kLogTabDoubles; x += NT) ltab[x] = kLogTab[x];
-    for (int x = tid; x < kExpTabDoubles; x += NT) etab[x] = kExpTab[x];
+    for (int x = tid; x < kLogTabDoubles; x += NT) lds[p.off_T + x] = kLogTab[x];
+    for (int x = tid; x < kExpTabDoubles; x += NT) lds[p.off_T + kLogTabDoubles + x] = kExpTab[x];
     const int b = blockIdx.x, NB = (int)gridDim.x / K;
     int j, t0;
     if (NB % 8 == 0) {
