@@ -63,6 +63,10 @@ EXPORTS = {
     "vbhem_fused_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int]),
     "vbhem_estep_fused": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "vbhem_fused_trials_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT),
+                                                     _c_int, _c_int]),
+    "vbhem_estep_fused_trials": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
+                                          _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "vbhem_last_fallback_count": (_c_int, [_vp, _vp]),
     "vbhem_timing_enable": (_c_int, [_c_int]),
     "vbhem_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),

@@ -254,7 +254,8 @@ struct FusedWs {
   double *E, *W, *bias, *shift;
 };
 
-size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, FusedWs &w) {
+size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, FusedWs &w,
+                   int R = 1) {
   Carver cv(ws);
   const int K = c->K, S = c->S, SB = b->SB;
   const size_t per_base = (size_t)K * (S + (size_t)S * S + 2 * (size_t)S * SB) * sizeof(double);
@@ -266,7 +267,7 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   int maxslab = kMaxSlabs;
   if (const char *ev = std::getenv("VBHEM_NSLAB")) maxslab = std::max(1, std::min(8192, std::atoi(ev)));
   w.nslab = std::min<int>(w.group, maxslab);
-  w.slab_len = (int)vbhem_stats_len(K, S, b->d, b->covmode);
+  w.slab_len = R * (int)vbhem_stats_len(K / R, S, b->d, b->covmode);
   w.flags = cv.take<int>(2 + g * K);
   w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   w.nu1 = cv.take<double>(g * K * S);
@@ -526,25 +527,42 @@ int vhem_estep_pairs(const vbhem_base_t *base, const vbhem_cluster_t *clus, int 
 }
 
 size_t vbhem_fused_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T) {
-  if (check_inputs(base, clus, T, false) != VBHEM_OK) return 0;
+  return vbhem_fused_trials_workspace_bytes(base, clus, 1, T);
+}
+
+size_t vbhem_fused_trials_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus,
+                                          int R, int T) {
+  if (check_inputs(base, clus, T, false) != VBHEM_OK || R < 1 || clus->K % R != 0) return 0;
   FusedWs w;
-  return carve_fused(nullptr, base, clus, T, w);
+  return carve_fused(nullptr, base, clus, T, w, R);
 }
 
 int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
                       const double *tildeN_dev, const double *logOmega_dev, double *stats_dev,
                       double *hatZ_dev, double *LL_elbo_dev, void *workspace_dev,
                       size_t workspace_bytes, void *stream) {
+  return vbhem_estep_fused_trials(base, clus, 1, T, tildeN_dev, logOmega_dev, stats_dev, hatZ_dev,
+                                  LL_elbo_dev, workspace_dev, workspace_bytes, stream);
+}
+
+int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *clus, int R, int T,
+                             const double *tildeN_dev, const double *logOmega_dev,
+                             double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
+                             void *workspace_dev, size_t workspace_bytes, void *stream) {
   int rc = check_inputs(base, clus, T);
   if (rc != VBHEM_OK) return rc;
+  if (R < 1 || clus->K % R != 0)
+    return fail(VBHEM_ERR_ARG, "trials: K must be a positive multiple of R");
+  if (R > 1 && clus->K > 256)
+    return fail(VBHEM_ERR_UNSUPPORTED, "trials: at most 256 clusters in total (R * K_trial)");
   if (!logOmega_dev || !stats_dev ||
       (base->N > 0 && (!tildeN_dev || !hatZ_dev || !LL_elbo_dev)))
     return fail(VBHEM_ERR_ARG, "null fused argument");
   FusedWs w;
-  const size_t need = carve_fused(nullptr, base, clus, T, w);
+  const size_t need = carve_fused(nullptr, base, clus, T, w, R);
   if (!workspace_dev || workspace_bytes < need)
     return fail(VBHEM_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
-  carve_fused(workspace_dev, base, clus, T, w);
+  carve_fused(workspace_dev, base, clus, T, w, R);
   hipStream_t st = static_cast<hipStream_t>(stream);
 
   // statistics kernels' geometry
@@ -553,6 +571,8 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   sa.K = K; sa.S = S; sa.SB = SB; sa.d = d; sa.covmode = base->covmode;
   sa.NU = (int)vbhem_stats_nu(d, base->covmode);
   sa.slab_len = w.slab_len;
+  sa.KT = K / R;
+  sa.SL = w.slab_len / R;
   sa.centres = base->centres; sa.covars = base->covars; sa.LL = LL_elbo_dev;
   sa.nu1 = w.nu1; sa.xi = w.xi; sa.tnu = w.tnu; sa.tildeN = tildeN_dev; sa.logOmega = logOmega_dev;
   sa.Z = w.Z; sa.hatZ = hatZ_dev; sa.slabs = w.slabs;
@@ -568,6 +588,9 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
   size_t sl_lds = 0;
   const bool gated = g_fused_mode == VBHEM_FUSED_GATED && ctx.split.ok &&
                      vbhem::plan_stats_list(sa, sl_lds);
+  if (R > 1 && !gated)
+    return fail(VBHEM_ERR_UNSUPPORTED,
+                "trials need the gated schedule (split-kernel shapes: S <= 16, Sb <= S)");
   sa.gate_cnt = gated ? w.gate_cnt : nullptr;
   sa.list = w.list; sa.list_tot = w.list_tot; sa.list_cap = w.group;
   // chunks of >= kChunkMinBases bases; the first group has the most, and in the

@@ -96,6 +96,8 @@ struct StatsArgs {
   int list_cap;
   int PB;          // pairs per batch of stats_list_kernel
   int assign;      // gated schedule, first group: write the slab entries instead of adding
+  int KT, SL;      // batched trials: clusters per trial (K = R * KT) and the per-trial
+                   // statistics length; slab = R sections of SL (KT = K, SL = slab_len: one)
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).

@@ -147,6 +147,118 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
 }
 
 // ---------------------------------------------------------------------------
+// resp_trials_kernel: resp_kernel for R = K / KT independent EM trials batched
+// as one cluster set (trial r = clusters [r KT, (r+1) KT)).  hat_Z(i, .) is
+// normalised within each trial (step_fc.m:275-281 per trial); Nj, Lt1, Lt7 go
+// to trial r's section [r SL, (r+1) SL) of the slab.  K <= 256: a lane holds
+// the clusters gl + s G, s < kRespSlots; per-trial sums are masked lane sums in
+// a fixed order (deterministic).
+// ---------------------------------------------------------------------------
+constexpr int kRespSlots = 4;
+
+__global__ __launch_bounds__(kRespThreads) void resp_trials_kernel(const StatsArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kRespThreads / 64;
+  const int K = p.K, KT = p.KT, R = K / KT, SL = p.SL, S = p.S;
+  int G = 1;
+  while (G < K && G < 64) G <<= 1;
+  const int BPW = 64 / G;
+  const int sub = lane / G, gl = lane - sub * G;
+  double *accNj = lds;                        // [NW*BPW][K]
+  double *accLt = accNj + NW * BPW * K;       // [NW][R][2]
+  int *gcnt = reinterpret_cast<int *>(accLt + 2 * NW * R);  // [K]
+  for (int x = tid; x < NW * BPW * K + 2 * NW * R; x += kRespThreads) accNj[x] = 0.0;
+  for (int x = tid; x < K; x += kRespThreads) gcnt[x] = 0;
+  __syncthreads();
+  int tr[kRespSlots];  // trial of this lane's slot s (-1: no cluster)
+#pragma unroll
+  for (int s = 0; s < kRespSlots; ++s) {
+    const int j = gl + s * G;
+    tr[s] = j < K ? j / KT : -1;
+  }
+  int b0, b1;
+  chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
+  double l1[kRespSlots], l7[kRespSlots];
+#pragma unroll
+  for (int s = 0; s < kRespSlots; ++s) l1[s] = l7[s] = 0.0;
+  for (int i = b0 + wave * BPW + sub; i - sub < b1; i += NW * BPW) {
+#pragma clang fp contract(off)
+    const bool iv = i < b1;
+    const int ii = iv ? i : b0;
+    const double tn = p.tildeN[ii];
+    const double *LL = p.LL + (size_t)ii * K;
+    double lz[kRespSlots], lse[kRespSlots];
+#pragma unroll
+    for (int s = 0; s < kRespSlots; ++s) {
+      const int j = tr[s] >= 0 ? gl + s * G : 0;
+      lz[s] = tr[s] >= 0 ? tn * (p.logOmega[j] + LL[j]) : -INFINITY;
+      lse[s] = 0.0;
+    }
+    for (int r = 0; r < R; ++r) {
+      double mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < kRespSlots; ++s) mx = tr[s] == r ? fmax(mx, lz[s]) : mx;
+      mx = group_max(mx, G);
+      double sm = 0.0;
+#pragma unroll
+      for (int s = 0; s < kRespSlots; ++s) sm += tr[s] == r ? exp(lz[s] - mx) : 0.0;
+      sm = group_sum(sm, G);
+      const double l = mx + log(sm);
+#pragma unroll
+      for (int s = 0; s < kRespSlots; ++s) lse[s] = tr[s] == r ? l : lse[s];
+    }
+    if (iv) {
+#pragma unroll
+      for (int s = 0; s < kRespSlots; ++s) {
+        if (tr[s] < 0) continue;
+        const int j = gl + s * G;
+        const double hz = exp(lz[s] - lse[s]) + 1e-50;
+        const double Z = hz * tn;
+        p.hatZ[(size_t)i * K + j] = hz;
+        p.Z[(size_t)(i - p.i_buf0) * K + j] = Z;
+        accNj[(wave * BPW + sub) * K + j] += Z;
+        if (Z > kGateZ) atomicAdd(&gcnt[j], 1);
+        l1[s] += Z * LL[j];
+        l7[s] += hz * log(hz);
+      }
+    }
+  }
+  for (int r = 0; r < R; ++r) {
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int s = 0; s < kRespSlots; ++s) {
+      a += tr[s] == r ? l1[s] : 0.0;
+      b += tr[s] == r ? l7[s] : 0.0;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+      accLt[(wave * R + r) * 2] = a;
+      accLt[(wave * R + r) * 2 + 1] = b;
+    }
+  }
+  __syncthreads();
+  double *slab = p.slabs + (size_t)blockIdx.x * p.slab_len;
+  for (int j = tid; j < K; j += kRespThreads) {
+    double s = 0.0;
+    for (int w = 0; w < NW * BPW; ++w) s += accNj[w * K + j];
+    const int r = j / KT;
+    double &dst = slab[(size_t)r * SL + (j - r * KT)];
+    dst = p.assign ? s : dst + s;
+  }
+  for (int x = tid; x < 2 * R; x += kRespThreads) {
+    const int r = x >> 1, q = x & 1;
+    double s = 0.0;
+    for (int w = 0; w < NW; ++w) s += accLt[(w * R + r) * 2 + q];
+    double &dst = slab[(size_t)r * SL + KT + (size_t)KT * S + (size_t)KT * S * S + q];
+    dst = p.assign ? s : dst + s;
+  }
+  if (p.gate_cnt)
+    for (int j = tid; j < K; j += kRespThreads) p.gate_cnt[(size_t)blockIdx.x * K + j] = gcnt[j];
+}
+
+// ---------------------------------------------------------------------------
 // gate_list_kernel: the gated pairs as per-cluster lists of bases, ascending i
 // (list[j][n], n < list_tot[j]).  Block = the resp_kernel chunk: its offset in
 // cluster j's list is the gate count of the chunks before it; inside the chunk
@@ -263,6 +375,9 @@ __global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs 
   const int *lst = p.list + (size_t)j * p.list_cap;
   const float invNU = 1.0f / (float)NU, invOU = 1.0f / (float)OU, invUN = 1.0f / (float)(SB * NU);
   double *slab = p.slabs + (size_t)c * p.slab_len;
+  // trial section of cluster j (R = K / KT trials; one section when KT = K)
+  const int KT = p.KT, tr = j / KT, jt = j - tr * KT;
+  double *tsl = slab + (size_t)tr * p.SL;
   for (int o0 = 0; o0 < NO; o0 += PER * kSlThreads) {
     double acc[PER];
 #pragma unroll
@@ -323,12 +438,12 @@ __global__ __launch_bounds__(kSlThreads) void stats_list_kernel(const StatsArgs 
       const int o = o0 + tid + e * kSlThreads;
       double *dst = nullptr;
       if (o < S) {
-        dst = slab + K + (size_t)j * S + o;
+        dst = tsl + KT + (size_t)jt * S + o;
       } else if (o < S + S * S) {
-        dst = slab + K + (size_t)K * S + (size_t)j * S * S + (o - S);
+        dst = tsl + KT + (size_t)KT * S + (size_t)jt * S * S + (o - S);
       } else if (o < NO) {
         const int oo = o - S - S * S;
-        dst = slab + K + (size_t)K * S + (size_t)K * S * S + 2 + (size_t)j * S * NU + oo;
+        dst = tsl + KT + (size_t)KT * S + (size_t)KT * S * S + 2 + (size_t)jt * S * NU + oo;
       }
       if (dst) *dst = p.assign ? acc[e] : *dst + acc[e];
     }
@@ -655,6 +770,14 @@ static hipError_t launch_stats_t(const StatsArgs &a, int nchunk, int ngroups, si
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
   int G = 1;
   while (G < a.K && G < 64) G <<= 1;
+  if (a.KT != a.K) {  // batched trials
+    if (a.K > kRespSlots * 64 || a.KT < 1 || a.K % a.KT != 0) return hipErrorInvalidValue;
+    const int R = a.K / a.KT;
+    const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2 * R)) * sizeof(double) +
+                       (size_t)a.K * sizeof(int);
+    hipLaunchKernelGGL(resp_trials_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
+    return hipGetLastError();
+  }
   const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2)) * sizeof(double) +
                      (size_t)a.K * sizeof(int);
   hipLaunchKernelGGL(resp_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);

@@ -95,3 +95,95 @@ def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
         res.point = host.convert_to_point(post, covmode)
         res.label = torch.argmax(res.hatZ, dim=1)
     return res
+
+
+def _stack_constants(all_consts: List[dict]) -> dict:
+    """Trial-major concatenation of per-trial cluster constants (R x K -> R*K)."""
+    return {k: np.concatenate([np.asarray(c[k]) for c in all_consts], axis=0)
+            for k in ("logA", "logPi", "m", "P", "c")}
+
+
+@dataclasses.dataclass
+class TrialsResult:
+    results: List[EMResult]         # one per trial (vbhem_h3m_c.m: h3m_news)
+    LLall: np.ndarray               # [R] final lower bound per trial (LLall)
+    best: int                       # argmax LLall (vbhem_h3m_c.m:167-170)
+
+
+def vbhem_h3m_c_trials(posts: List[Posterior], engine: EStepEngine, opt: dict, *,
+                       total_N: Optional[int] = None,
+                       allreduce: Optional[Callable[[torch.Tensor], None]] = None,
+                       max_iter: Optional[int] = None) -> TrialsResult:
+    """R EM trials from their own initial posteriors (vbhem_h3m_c.m:28-67,
+    `parfor it = 1:numits`), run in lockstep with one batched E-step launch per
+    iteration (vbhem_estep_fused_trials).  Every trial follows
+    :func:`vbhem_h3m_c_step_fc` exactly; a trial that has stopped keeps its
+    final state (its clusters still ride along in the launch, their outputs
+    unused).  The best trial is the one with the largest final bound."""
+    R = len(posts)
+    if engine.trials != R:
+        raise ValueError("engine.trials must equal len(posts)")
+    covmode = engine.base.covmode
+    K, S, d = posts[0].m.shape
+    total_N = engine.N if total_N is None else int(total_N)
+    tN = tilde_n(engine, opt["Nv"], total_N)
+    maxIter = opt["max_iter"] if max_iter is None else max_iter
+    minDiff = opt["minDiff"]
+    SL = host.stats_len(K, S, d, covmode)
+    post = [p.copy() for p in posts]
+    lastL = [-np.finfo(float).max] * R
+    it = [0] * R
+    LogLs: List[List[float]] = [[] for _ in range(R)]
+    syn: List[Optional[dict]] = [None] * R
+    stable = [True] * R
+    L = [-np.inf] * R
+    Nj = [np.zeros(K) for _ in range(R)]
+    done = [False] * R
+    hatZ: List[Optional[torch.Tensor]] = [None] * R
+    Lel: List[Optional[torch.Tensor]] = [None] * R
+    consts = [host.cluster_constants(p, covmode) for p in post]
+    logOm = [host.log_omega_tilde(p.alpha) for p in post]
+    while not all(done):
+        engine.set_clusters(_stack_constants(consts))
+        engine.set_log_omega(np.concatenate(logOm))
+        stats = engine.fused(tN)
+        if allreduce is not None:
+            allreduce(stats)
+        vec = stats.cpu().numpy()
+        for r in range(R):
+            if done[r]:
+                continue
+            st = host.unpack_stats(vec[r * SL:(r + 1) * SL], K, S, d, covmode)
+            Nj[r] = st["Nj"] + 1e-50
+            Lr = host.lower_bound(st["Lt1"], st["Lt7"], Nj[r], logOm[r], post[r], consts[r], opt,
+                                  covmode)
+            stop = (it[r] > 1 and abs((Lr - lastL[r]) / lastL[r]) <= minDiff) or it[r] == maxIter
+            if np.isnan(Lr):  # step_fc.m:338-374
+                L[r] = -np.inf
+                stable[r] = False
+                stop = True
+            else:
+                L[r] = Lr
+                syn[r] = host.finish_statistics(st, covmode)
+                post[r] = host.mstep(syn[r], Nj[r], opt, covmode, post[r].W0mode)
+                it[r] += 1
+                LogLs[r].append(Lr)
+                lastL[r] = Lr
+            if stop:
+                done[r] = True
+                cols = slice(r * K, (r + 1) * K)
+                hatZ[r] = engine.hatZ[:, cols].clone()
+                Lel[r] = engine.LL[:, cols].clone()
+            else:
+                consts[r] = host.cluster_constants(post[r], covmode)
+                logOm[r] = host.log_omega_tilde(post[r].alpha)
+    results = []
+    for r in range(R):
+        res = EMResult(post=post[r], LogLs=LogLs[r], LL=L[r], iters=it[r], stable=stable[r],
+                       hatZ=hatZ[r], L_elbo=Lel[r], Nj=Nj[r], syn=syn[r])
+        if stable[r]:
+            res.point = host.convert_to_point(post[r], covmode)
+            res.label = torch.argmax(res.hatZ, dim=1)
+        results.append(res)
+    LLall = np.array([x.LL for x in results])
+    return TrialsResult(results=results, LLall=LLall, best=int(np.argmax(LLall)))

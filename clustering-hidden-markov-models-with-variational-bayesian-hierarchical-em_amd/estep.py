@@ -22,7 +22,9 @@ F64 = torch.float64
 
 
 class EStepEngine:
-    def __init__(self, base: BaseSet, K: int, S: int, T: int, device=None):
+    def __init__(self, base: BaseSet, K: int, S: int, T: int, device=None, trials: int = 1):
+        """K clusters in total; with ``trials`` = R > 1 they are R independent EM
+        trials of K / R clusters each, trial-major (vbhem_estep_fused_trials)."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -48,7 +50,11 @@ class EStepEngine:
                                _capi.ptr(bb.A), _capi.ptr(bb.centres), _capi.ptr(bb.covars))
         self._ct = _capi.ClusterT(K, S, _capi.ptr(self.c_logA), _capi.ptr(self.c_logPi),
                                   _capi.ptr(self.c_m), _capi.ptr(self.c_P), _capi.ptr(self.c_c))
-        self.stats_len = int(self.lib.vbhem_stats_len(K, S, d, bb.covmode))
+        self.trials = int(trials)
+        if self.trials < 1 or K % self.trials:
+            raise ValueError("K must be a positive multiple of trials")
+        self.stats_len = self.trials * int(self.lib.vbhem_stats_len(K // self.trials, S, d,
+                                                                       bb.covmode))
         self.stats = torch.zeros((self.stats_len,), dtype=F64, device=dv)
         self.hatZ = torch.zeros((N, K), dtype=F64, device=dv)
         self.LL = torch.zeros((N, K), dtype=F64, device=dv)
@@ -121,14 +127,23 @@ class EStepEngine:
         Returns the packed statistics vector (device, [stats_len]); hat_Z and
         L_elbo are left in ``self.hatZ`` / ``self.LL``."""
         if self._ws_fused is None:
-            nb = int(self.lib.vbhem_fused_workspace_bytes(ctypes.byref(self._bt),
-                                                          ctypes.byref(self._ct), self.T))
+            nb = int(self.lib.vbhem_fused_trials_workspace_bytes(
+                ctypes.byref(self._bt), ctypes.byref(self._ct), self.trials, self.T))
             self._ws_fused = torch.empty((max(nb, 1),), dtype=torch.uint8, device=self.device)
-        rc = self.lib.vbhem_estep_fused(
-            ctypes.byref(self._bt), ctypes.byref(self._ct), self.T, _capi.ptr(tildeN),
-            _capi.ptr(self.logOmega), _capi.ptr(self.stats), _capi.ptr(self.hatZ),
-            _capi.ptr(self.LL), _capi.ptr(self._ws_fused), self._ws_fused.numel(), self._stream())
-        _capi.check(rc, "vbhem_estep_fused")
+        if self.trials == 1:
+            rc = self.lib.vbhem_estep_fused(
+                ctypes.byref(self._bt), ctypes.byref(self._ct), self.T, _capi.ptr(tildeN),
+                _capi.ptr(self.logOmega), _capi.ptr(self.stats), _capi.ptr(self.hatZ),
+                _capi.ptr(self.LL), _capi.ptr(self._ws_fused), self._ws_fused.numel(),
+                self._stream())
+            _capi.check(rc, "vbhem_estep_fused")
+        else:
+            rc = self.lib.vbhem_estep_fused_trials(
+                ctypes.byref(self._bt), ctypes.byref(self._ct), self.trials, self.T,
+                _capi.ptr(tildeN), _capi.ptr(self.logOmega), _capi.ptr(self.stats),
+                _capi.ptr(self.hatZ), _capi.ptr(self.LL), _capi.ptr(self._ws_fused),
+                self._ws_fused.numel(), self._stream())
+            _capi.check(rc, "vbhem_estep_fused_trials")
         return self.stats
 
     def fallback_count(self) -> int:

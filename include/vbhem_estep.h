@@ -131,6 +131,21 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
                       double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
                       void *workspace_dev, size_t workspace_bytes, void *stream);
 
+/* R independent EM trials (vbhem_h3m_c.m:28-67, `parfor it = 1:numits`, each from its
+ * own initialisation) batched as one launch over the same base set: `clus` holds
+ * R * KT clusters, trial-major (trial r = clusters [r KT, (r+1) KT)).  hat_Z is
+ * normalised within each trial; stats_dev holds R consecutive vectors of
+ * vbhem_stats_len(KT, S, d, covmode), each laid out as above for its trial;
+ * logOmega_dev [R*KT] is each trial's psi(alpha) - psi(sum alpha); hatZ_dev /
+ * LL_elbo_dev are [N][R*KT].  R = 1 is vbhem_estep_fused.  Needs the gated schedule
+ * (S <= 16, Sb <= S) and R * KT <= 256; else VBHEM_ERR_UNSUPPORTED. */
+size_t vbhem_fused_trials_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus,
+                                          int R, int T);
+int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *clus, int R, int T,
+                             const double *tildeN_dev, const double *logOmega_dev,
+                             double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
+                             void *workspace_dev, size_t workspace_bytes, void *stream);
+
 /* Fused E-step schedule (process-wide; default VBHEM_FUSED_GATED, or set the
  * environment variable VBHEM_FUSED_DENSE=1).  Both give the same outputs:
  *   VBHEM_FUSED_GATED  backward sweep + log-likelihood for every pair, then the
