@@ -45,6 +45,16 @@ class EmOptT(ctypes.Structure):  # include/vbhem_em.h vbhem_em_opt_t
                 ("Nv", ctypes.c_double), ("max_iter", _c_int), ("minDiff", ctypes.c_double)]
 
 
+class SeqsT(ctypes.Structure):  # include/vbhmm_fb.h vbhmm_seqs_t
+    _fields_ = [("N", _c_int), ("dim", _c_int), ("maxT", _c_int), ("offsets", _vp), ("x", _vp)]
+
+
+class HmmParamsT(ctypes.Structure):  # include/vbhmm_fb.h vbhmm_params_t
+    _fields_ = [("K", _c_int), ("dim", _c_int), ("m", _vp), ("W", _vp), ("v", _vp), ("beta", _vp),
+                ("logLambdaTilde", _vp), ("pz1", _vp), ("A", _vp),
+                ("const_denominator", ctypes.c_double)]
+
+
 ALLREDUCE_FN = ctypes.CFUNCTYPE(_c_int, _vp, _c_size, _vp, _vp)
 
 EXPORTS = {
@@ -86,6 +96,11 @@ EXPORTS = {
                               ctypes.POINTER(PostT), _vp, ctypes.POINTER(_c_int),
                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int), _vp, _vp,
                               _vp, _vp, _c_size, _vp, ALLREDUCE_FN, _vp]),
+    "vbhmm_fb_workspace_bytes": (_c_size, [ctypes.POINTER(SeqsT), _c_int]),
+    "vbhmm_fb": (_c_int, [ctypes.POINTER(SeqsT), ctypes.POINTER(HmmParamsT), _vp, _vp, _vp, _vp, _vp,
+                          _c_size, _vp]),
+    "vbhmm_fb_host": (_c_int, [_c_int, ctypes.POINTER(SeqsT), ctypes.POINTER(HmmParamsT), _vp, _vp,
+                               _vp, _vp]),
     "vbhem_last_error": (ctypes.c_char_p, []),
     "vbhem_version": (ctypes.c_char_p, []),
 }

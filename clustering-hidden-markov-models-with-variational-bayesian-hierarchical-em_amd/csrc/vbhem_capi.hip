@@ -55,6 +55,13 @@ int hip_fail(hipError_t e, const char *where) {
   return fail(VBHEM_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 
+}  // namespace
+
+// shared with the other C-ABI translation units (vbhmm_fb.hip): vbhem_last_error()
+int vbhem::set_error(int code, const std::string &msg) { return fail(code, msg); }
+
+namespace {
+
 constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
 constexpr int kExactThreads = vbhem::kExactBlock;  // fallback kernel threads
@@ -578,8 +585,7 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   sa.Z = w.Z; sa.hatZ = hatZ_dev; sa.slabs = w.slabs;
   size_t slds = 0;
   int ngroups = 1;
-  if (!vbhem::plan_stats(sa, slds, ngroups))
-    return fail(VBHEM_ERR_UNSUPPORTED, "statistics tile does not fit (S or d too large)");
+  const bool dense_ok = vbhem::plan_stats(sa, slds, ngroups);  // dense-schedule statistics
 
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T);
@@ -591,6 +597,8 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   if (R > 1 && !gated)
     return fail(VBHEM_ERR_UNSUPPORTED,
                 "trials need the gated schedule (split-kernel shapes: S <= 16, Sb <= S)");
+  if (!gated && !dense_ok)
+    return fail(VBHEM_ERR_UNSUPPORTED, "statistics tile does not fit (S or d too large)");
   sa.gate_cnt = gated ? w.gate_cnt : nullptr;
   sa.list = w.list; sa.list_tot = w.list_tot; sa.list_cap = w.group;
   // chunks of >= kChunkMinBases bases; the first group has the most, and in the

@@ -6,9 +6,13 @@
 #include <cstddef>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 
 namespace vbhem {
+
+// record `msg` for vbhem_last_error() and return `code` (vbhem_capi.hip)
+int set_error(int code, const std::string &msg);
 
 // Host-side launch helpers: the dynamic-LDS attribute and the occupancy query
 // are per (kernel, block, LDS) facts, so they are asked once and remembered

@@ -72,6 +72,9 @@ def load_c_oracle(build_if_missing: bool = True):
                                       ctypes.c_int, dp, dp, dp, dp, dp, dp,
                                       dp, dp, dp, dp, dp, dp]
     lib.oracle_statistics.restype = None
+    lib.oracle_vbhmm_fb.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, dp,
+                                    dp, dp, dp, dp, dp, ctypes.c_double, dp, dp, dp, dp, dp, dp]
+    lib.oracle_vbhmm_fb.restype = ctypes.c_int
     _LIB = lib
     return lib
 
@@ -686,3 +689,112 @@ def em_step_fc(post: dict, base: dict, opt: dict, estep=None):
                    M=np.array([s["Nj_rho2rho"] for s in syn]),
                    Nrho=np.array([s["Nj_rho"] for s in syn]))
     return out
+
+
+# ---------------------------------------------------------------------------
+# VB-HMM forward-backward (src/hmm/vbhmm_fb.m, vbhmm_fb_mex.c)
+# ---------------------------------------------------------------------------
+def pack_sequences(data, dim: int):
+    """data: list of [T_n x dim] arrays (vbhmm_fb.m `data{n}`, one row per
+    observation) -> (offsets [N+1] int32, x [sum T][dim] fp64, maxT)."""
+    lens = [int(np.asarray(a).reshape(-1, dim).shape[0]) for a in data]
+    offsets = np.zeros(len(data) + 1, dtype=np.int32)
+    offsets[1:] = np.cumsum(lens)
+    x = (np.concatenate([np.asarray(a, dtype=np.float64).reshape(-1, dim) for a in data], axis=0)
+         if offsets[-1] > 0 else np.zeros((0, dim)))
+    return offsets, np.ascontiguousarray(x), max(lens) if lens else 0
+
+
+def vbhmm_prelude(varpar: dict):
+    """vbhmm_fb.m:54-93 (usegroups = 0) and :121-122: logLambdaTilde [K],
+    logATilde [K][K] (row format), logPiTilde [K], const_denominator, and the
+    MEX inputs t_pz1 = exp(logPiTilde), t_tpztzt1 = exp(logATilde).
+    varpar: v [K], W [K][dim][dim], epsilon [K][K], alpha [K], m [K][dim], beta [K]."""
+    from scipy.special import digamma
+    v = np.asarray(varpar["v"], dtype=np.float64)
+    W = np.asarray(varpar["W"], dtype=np.float64)
+    K, dim = np.asarray(varpar["m"]).shape
+    const = dim * np.log(2.0)
+    lLT = np.zeros(K)
+    for k in range(K):
+        t1 = digamma(0.5 * (v[k] + 1.0) - 0.5 * np.arange(1, dim + 1))
+        lLT[k] = t1.sum() + const + np.log(np.linalg.det(W[k]))
+    eps = np.asarray(varpar["epsilon"], dtype=np.float64)
+    logA = digamma(eps) - digamma(eps.sum(axis=1, keepdims=True))
+    alpha = np.asarray(varpar["alpha"], dtype=np.float64)
+    logPi = digamma(alpha) - digamma(alpha.sum())
+    return dict(logLambdaTilde=lLT, logATilde=logA, logPiTilde=logPi,
+                const_denominator=dim * np.log(2 * np.pi) / 2.0,
+                pz1=np.exp(logPi), A=np.exp(logA))
+
+
+def c_vbhmm_fb(data, varpar: dict, pre: dict = None):
+    """vbhmm_fb_mex outputs from the C restatement: logrho [maxT][N][K],
+    gamma [maxT][N][K], xi_sum [N][K][K] ([n][from][to]), phi_norm [N]."""
+    lib = load_c_oracle()
+    m = _c64(varpar["m"])
+    K, dim = m.shape
+    pre = vbhmm_prelude(varpar) if pre is None else pre
+    offsets, x, maxT = pack_sequences(data, dim)
+    N = len(data)
+    out = dict(logrho=np.zeros((maxT, N, K)), gamma=np.zeros((maxT, N, K)),
+               xi_sum=np.zeros((N, K, K)), phi_norm=np.zeros(N))
+    rc = lib.oracle_vbhmm_fb(
+        N, K, dim, maxT, offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(x), _dp(m),
+        _dp(_c64(varpar["W"])), _dp(_c64(varpar["v"])), _dp(_c64(varpar["beta"])),
+        _dp(_c64(pre["logLambdaTilde"])), float(pre["const_denominator"]), _dp(_c64(pre["pz1"])),
+        _dp(_c64(pre["A"])), _dp(out["logrho"]), _dp(out["gamma"]), _dp(out["xi_sum"]),
+        _dp(out["phi_norm"]))
+    if rc != 0:
+        raise ValueError(f"oracle_vbhmm_fb failed rc={rc}")
+    return out
+
+
+def twin_vbhmm_fb(data, varpar: dict, pre: dict = None):
+    """numpy restatement of the MATLAB path vbhmm_fb.m:227-379 (vectorised the way
+    the .m file is, independent of the C restatement's loops); same outputs."""
+    m = np.asarray(varpar["m"], dtype=np.float64)
+    W = np.asarray(varpar["W"], dtype=np.float64)
+    v = np.asarray(varpar["v"], dtype=np.float64)
+    beta = np.asarray(varpar["beta"], dtype=np.float64)
+    K, dim = m.shape
+    pre = vbhmm_prelude(varpar) if pre is None else pre
+    N = len(data)
+    maxT = max([np.asarray(a).reshape(-1, dim).shape[0] for a in data] + [0])
+    logrho_S = np.zeros((maxT, N, K))
+    gamma_all = np.zeros((maxT, N, K))
+    xi_sum = np.zeros((N, K, K))
+    phi = np.zeros(N)
+    pz1, A = pre["pz1"], pre["A"]
+    for n in range(N):
+        tdata = np.asarray(data[n], dtype=np.float64).reshape(-1, dim).T   # [dim x T]
+        tT = tdata.shape[1]
+        delta = np.zeros((K, tT))
+        for k in range(K):
+            diff = tdata - m[k][:, None]
+            mterm = ((W[k] @ diff) * diff).sum(axis=0)
+            delta[k] = dim / beta[k] + v[k] * mterm
+        logrho = 0.5 * pre["logLambdaTilde"][:, None] - 0.5 * delta - pre["const_denominator"]
+        logrho_S[:tT, n, :] = logrho.T
+        fb = logrho.T                                   # [T x K]
+        mx = fb.max(axis=1) if tT else np.zeros(0)
+        px = np.exp(fb - mx[:, None])
+        if tT >= 1:
+            al = np.zeros((tT, K)); c = np.zeros(tT); be = np.zeros((tT, K)); g = np.zeros((K, tT))
+            Dl = pz1 * px[0]
+            c[0] = Dl.sum(); al[0] = Dl / c[0]
+            for i in range(1, tT):
+                Dl = (al[i - 1] @ A) * px[i]
+                c[i] = Dl.sum(); al[i] = Dl / c[i]
+            be[tT - 1] = 1.0
+            g[:, tT - 1] = al[tT - 1] * be[tT - 1]
+            sx = np.zeros((K, K))
+            for i in range(tT - 2, -1, -1):
+                bpi = be[i + 1] * px[i + 1]
+                be[i] = (bpi @ A.T) / c[i + 1]
+                g[:, i] = al[i] * be[i]
+                sx += (A * np.outer(al[i], bpi)) / c[i + 1]
+            gamma_all[:tT, n, :] = g.T
+            xi_sum[n] = sx
+            phi[n] = np.log(c).sum() + mx.sum()
+    return dict(logrho=logrho_S, gamma=gamma_all, xi_sum=xi_sum, phi_norm=phi)

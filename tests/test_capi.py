@@ -18,7 +18,7 @@ def declared_functions():
                   for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
-    return sorted(set(re.findall(r"\b((?:vbhem|vhem)_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b((?:vbhem|vhem|vbhmm)_[a-z0-9_]+)\s*\(", src)))
 
 
 def header_constants():
