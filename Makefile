@@ -24,12 +24,12 @@ oracle:
 	$(MAKE) -C oracle liboracle.so
 
 # test-only: a MATLAB mx/mex API double and the MEX gateway built against it
-mex: tests/mxshim/libmxshim.so $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so $(LIBDIR)/hem_hmm_bwd_fwd_mex.so
+mex: tests/mxshim/libmxshim.so $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so $(LIBDIR)/hem_hmm_bwd_fwd_mex.so $(LIBDIR)/vbhmm_fb_mex.so
 
 tests/mxshim/libmxshim.so: tests/mxshim/mxshim.c tests/mxshim/mex.h
 	gcc -O2 -fPIC -shared -Itests/mxshim -o $@ $<
 
-$(LIBDIR)/%_mex.so: integration/%_mex.c integration/h3m_mex_common.h include/vbhem_estep.h $(LIBDIR)/libvbhem_estep.so tests/mxshim/mex.h
+$(LIBDIR)/%_mex.so: integration/%_mex.c integration/h3m_mex_common.h include/vbhem_estep.h include/vbhmm_fb.h $(LIBDIR)/libvbhem_estep.so tests/mxshim/mex.h
 	gcc -O2 -fPIC -shared -Iinclude -Itests/mxshim -Iintegration -o $@ $< -L$(LIBDIR) -lvbhem_estep -lm -Wl,-rpath,'$$ORIGIN'
 
 # test-only: the restricted-domain exp/log/rcp of vbhem_math.h, host and device

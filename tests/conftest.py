@@ -26,6 +26,7 @@ PKG_DIR = pkgload.PKG_DIR
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libvbhem_estep.so")
 GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "vbhem_hmm_bwd_fwd_mex.so")
 HEM_GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "hem_hmm_bwd_fwd_mex.so")
+FB_GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "vbhmm_fb_mex.so")
 MXSHIM_PATH = os.path.join(ROOT, "tests", "mxshim", "libmxshim.so")
 MATHCHECK_PATH = os.path.join(ROOT, "tests", "mathcheck", "libmathcheck.so")
 GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
@@ -102,6 +103,16 @@ def hem_gateway():
         _make("mex")
     shim = ctypes.CDLL(MXSHIM_PATH, mode=ctypes.RTLD_GLOBAL)
     gw = ctypes.CDLL(HEM_GATEWAY_PATH, mode=ctypes.RTLD_GLOBAL)
+    return gw, shim
+
+
+@pytest.fixture(scope="session")
+def fb_gateway():
+    """(mexFunction of the vbhmm_fb_mex gateway, mxshim)."""
+    if not (os.path.exists(FB_GATEWAY_PATH) and os.path.exists(MXSHIM_PATH)):
+        _make("mex")
+    shim = ctypes.CDLL(MXSHIM_PATH, mode=ctypes.RTLD_GLOBAL)
+    gw = ctypes.CDLL(FB_GATEWAY_PATH, mode=ctypes.RTLD_GLOBAL)
     return gw, shim
 
 
