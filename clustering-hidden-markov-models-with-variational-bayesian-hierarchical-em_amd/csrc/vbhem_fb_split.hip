@@ -32,6 +32,13 @@
 #include "vbhem_log_table.h"
 #include "vbhem_math.h"
 
+// waves per SIMD the backward-only mode is compiled for (register budget 512 / W):
+// 4 where the 128-VGPR budget costs at most a few spills outside the step loop
+// (S = 8: 138 -> 128 VGPRs, 10 spilled, -3 % kernel time at C4), else 3
+#ifndef VBHEM_BWD_WAVES
+#define VBHEM_BWD_WAVES(S) (((S) <= 4 || ((S) >= 7 && (S) <= 10)) ? 4 : 3)
+#endif
+
 namespace vbhem {
 
 namespace {
@@ -180,7 +187,7 @@ __device__ __forceinline__ void load_row(double (&dst)[SH], const double *row, i
 // List mode: the gated pairs of every cluster cut into PPB-pair work items,
 // contiguous item ranges per block (cluster constants restaged when j changes).
 template <int S, int LPC, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kFbBackward ? 3 : 2)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kFbBackward ? VBHEM_BWD_WAVES(S) : 2)))
 void fb_split_kernel(const SplitArgs p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using LY = SplitLayout<S, LPC>;
