@@ -23,7 +23,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cmath>
 
 #include "vbhem_internal.h"
@@ -313,122 +312,6 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_raw_kernel(EmissionArg
   }
 }
 
-// emission_chunk_kernel (d > 8 or odd d, KD <= 160: e.g. C5, d = 16 full, KD = 152):
-// W' (up to 160 x K*S doubles) does not fit LDS whole, so each block stages one
-// 64-row slice of it (rows r0 .. r0+63, all k) and its waves walk 16-column tiles;
-// block b takes row slice b % nrc, so the nrc blocks that share a column range
-// run side by side and read the same covariances from L2.  Per tile each lane
-// builds its whole B operand U[4t + l/16][l mod 16], t < KQ, once into registers
-// (from L1/L2: the covariance rows of 16 consecutive columns are contiguous), then
-// 4 row tiles x KQ k-steps of v_mfma_f64_16x16x4f64 with W' read from LDS.
-// ---------------------------------------------------------------------------
-constexpr int kEmChunkRows = 64;
-constexpr int kEmChunkMaxKQ = 40;
-constexpr int kEmChunkPart = 10;
-constexpr int kEmChunkThreads = 256;
-
-__global__ __launch_bounds__(kEmChunkThreads) __attribute__((amdgpu_waves_per_eu(2)))
-void emission_chunk_kernel(EmissionArgs p) {
-  extern __shared__ double lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NW = kEmChunkThreads / 64;
-  const int d = p.d, SB = p.SB, KS = p.K * p.S, KSP = p.ksp, KDP = p.kdp, KQ = KDP / 4;
-  const bool full = p.covmode == kCovFull;
-  const int NPF = full ? d * (d + 1) / 2 : d;
-  const int dd = full ? d * d : d;
-  const int ncols = (p.i_end - p.i_begin) * SB;
-  const int nctile = (ncols + 15) / 16;
-  const int nrc = KSP / kEmChunkRows, rc = blockIdx.x % nrc, r0 = rc * kEmChunkRows;
-  const int cslice = blockIdx.x / nrc, nslice = gridDim.x / nrc;
-  double *Wl = lds;                            // [KDP][64]
-  double *bl = Wl + (size_t)KDP * kEmChunkRows;  // [64]
-  double *zsh = bl + kEmChunkRows;             // [d]
-  int *tab = reinterpret_cast<int *>(zsh + d);  // [KDP] operand descriptors
-  for (int x = tid; x < KDP * kEmChunkRows; x += kEmChunkThreads) {
-    const int e = x / kEmChunkRows, r = x - e * kEmChunkRows;
-    Wl[x] = p.W[(size_t)e * KSP + r0 + r];
-  }
-  for (int x = tid; x < kEmChunkRows; x += kEmChunkThreads) bl[x] = p.bias[r0 + x];
-  for (int a = tid; a < d; a += kEmChunkThreads) zsh[a] = p.shift[a];
-  for (int e = tid; e < KDP; e += kEmChunkThreads) {
-    // u = C[oA] + C[oB] + f mu'_a mu'_b + g mu'_a  (oA / oB = -1: no term)
-    int a = 0, b = 0, oA = -1, oB = -1, f = 0, g = 0;
-    if (e < NPF) {
-      if (full) {
-        packed_ab(e, d, a, b);
-        oA = a * d + b;
-        if (a != b) { oB = b * d + a; f = 2; } else { f = 1; }
-      } else {
-        a = b = e; oA = a; f = 1;
-      }
-    } else if (e < NPF + d) {
-      a = b = e - NPF; g = 1;
-    }
-    tab[e] = (oA + 1) | ((oB + 1) << 9) | (a << 18) | (b << 23) | (f << 28) | (g << 30);
-  }
-  __syncthreads();
-  const int kl = lane >> 4, cl = lane & 15;
-  const size_t ldE = (size_t)p.e_ld;
-  for (int ct = cslice * NW + wave; ct < nctile; ct += nslice * NW) {
-    const int c0 = ct * 16;
-    const bool cv = cl < min(16, ncols - c0);
-    const size_t gcol = (size_t)p.i_begin * SB + c0 + (cv ? cl : 0);
-    const double *Cg = p.covars + gcol * dd;
-    const double *Mg = p.centres + gcol * d;
-    double4_t acc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) acc[q][v] = bl[q * 16 + kl + 4 * v];
-    const double *Wr = Wl + kl * kEmChunkRows + cl;
-    // the k-steps in parts of kEmChunkPart: a part's B operand built into registers,
-    // then its MFMAs (a bounded live range: 2 waves per SIMD)
-#pragma unroll
-    for (int h = 0; h < kEmChunkMaxKQ / kEmChunkPart; ++h) {
-      if (h * kEmChunkPart < KQ) {
-        double ub[kEmChunkPart];
-#pragma unroll
-        for (int tt = 0; tt < kEmChunkPart; ++tt) {
-          const int t = h * kEmChunkPart + tt;
-          ub[tt] = 0.0;
-          if (t < KQ) {
-            const int tb = tab[4 * t + kl];
-            const int oA = (tb & 511) - 1, oB = ((tb >> 9) & 511) - 1;
-            const int a = (tb >> 18) & 31, b = (tb >> 23) & 31;
-            const double f = (double)((tb >> 28) & 3), g = (double)((tb >> 30) & 1);
-            const double ma = Mg[a] - zsh[a], mb = Mg[b] - zsh[b];
-            const double cA = Cg[oA < 0 ? 0 : oA], cB = Cg[oB < 0 ? 0 : oB];
-            const double u = (oA < 0 ? 0.0 : cA) + (oB < 0 ? 0.0 : cB) + fma(f * ma, mb, g * ma);
-            ub[tt] = cv ? u : 0.0;
-          }
-        }
-#pragma unroll
-        for (int tt = 0; tt < kEmChunkPart; ++tt) {
-          const int t = h * kEmChunkPart + tt;
-          if (t < KQ) {
-            double w[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = Wr[4 * t * kEmChunkRows + q * 16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(w[q], ub[tt], acc[q], 0, 0, 0);
-          }
-        }
-      }
-    }
-    if (cv) {
-      double *Ec = p.E + (size_t)(p.i_begin - p.i_buf0) * SB + c0 + cl;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int row = r0 + q * 16 + kl + 4 * v;
-          if (row < KS) Ec[(size_t)row * ldE] = p.smooth != 1.0 ? acc[q][v] / p.smooth : acc[q][v];
-        }
-    }
-  }
-}
-
 // emission_gen_kernel<WL> (d > 8): operand B formed per k-step from the column's
 // covariances and means read through L1/L2.
 template <bool WL>
@@ -531,7 +414,6 @@ bool plan_emission(EmissionArgs &a, size_t &lds) {
   a.ksp = emission_ksp(a.K * a.S);
   const int dd = full ? d * d : d;
   a.wfull = (dd <= 64 && d <= 8 && dd % 2 == 0 && d % 2 == 0);  // RAW: tile staged in LDS
-  a.chunk = false;
   // 8 waves per block with W' in LDS when it fits one block per CU, else 4 waves
   // reading W' through L1/L2
   const size_t wbytes = (size_t)a.kdp * a.ksp * sizeof(double);
@@ -541,12 +423,6 @@ bool plan_emission(EmissionArgs &a, size_t &lds) {
     a.wlds = head + wbytes + 8 * slot <= 160 * 1024;
     a.nwave = a.wlds ? 8 : 4;
     lds = head + (a.wlds ? wbytes : 0) + (size_t)a.nwave * slot;
-  } else if (a.kdp <= 4 * kEmChunkMaxKQ && std::getenv("VBHEM_EMISSION_CHUNK") &&
-             std::atoi(std::getenv("VBHEM_EMISSION_CHUNK")) != 0) {  // experimental (opt-in)
-    a.chunk = true;  // emission_chunk_kernel: a 64-row slice of W' per block
-    a.nwave = kEmChunkThreads / 64;
-    lds = ((size_t)a.kdp * kEmChunkRows + kEmChunkRows + d) * sizeof(double) +
-          (size_t)a.kdp * sizeof(int);
   } else {
     const size_t head = ((size_t)(a.KD + 1) / 2 + 1) * sizeof(double);
     a.wlds = head + wbytes <= 160 * 1024;
@@ -600,18 +476,6 @@ hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
       case 11: return launch_raw_kq<11>(a, lds, st);
       default: return hipErrorInvalidValue;
     }
-  }
-  if (a.chunk) {
-    auto *fn = &emission_chunk_kernel;
-    hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
-    if (e != hipSuccess) return e;
-    const int nrc = a.ksp / kEmChunkRows;
-    const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), kEmChunkThreads, lds);
-    const int nctile = (ncols + 15) / 16;
-    // every resident block, in whole groups of the nrc row slices
-    const int slices = std::max(1, std::min((nctile + 3) / 4, device_cus() * per_cu / nrc));
-    hipLaunchKernelGGL(fn, dim3((unsigned)(slices * nrc)), dim3(kEmChunkThreads), lds, st, a);
-    return hipGetLastError();
   }
   return a.wlds ? launch_emission_fn(&emission_gen_kernel<true>, a, lds, st)
                 : launch_emission_fn(&emission_gen_kernel<false>, a, lds, st);

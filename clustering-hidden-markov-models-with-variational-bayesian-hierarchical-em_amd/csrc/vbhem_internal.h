@@ -136,7 +136,6 @@ struct EmissionArgs {
   int SB, d, covmode, K, S, KD, CB;
   int kdp, ksp;  // padded W' dims: [kdp][ksp], bias' [ksp]
   bool wfull;  // column tiles staged in LDS (d <= 8); else read through L1/L2
-  bool chunk;  // emission_chunk_kernel (no RAW path, KD <= 160): 64-row W' slices in LDS
   bool wlds;   // W staged in LDS (8-wave blocks); else read through L1/L2 (4-wave blocks)
   int nwave;
   int i_begin, i_end, i_buf0;
