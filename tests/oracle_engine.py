@@ -25,11 +25,14 @@ def pack_stats(Nj, N1, M, Lt1, Lt7, Nr, Y, SC, covmode):
 
 
 class OracleEngine:
-    def __init__(self, base, K, S, T, nthreads=2):
+    def __init__(self, base, K, S, T, nthreads=2, trials=1):
+        """K clusters in total; trials = R > 1: R consecutive groups of K / R
+        (the layout of vbhem_estep_fused_trials)."""
         self.base = base                       # vbhem_amd.BaseSet on the CPU
         self._np = base.numpy()
         self.K, self.S, self.T = K, S, T
         self.nthreads = nthreads
+        self.trials = trials
         self.consts = None
         self.logOmega = None
         self.hatZ = torch.zeros((base.N, K), dtype=torch.float64)
@@ -50,12 +53,20 @@ class OracleEngine:
         self.calls += 1
         tN = tildeN.cpu().numpy() if torch.is_tensor(tildeN) else np.asarray(tildeN)
         cov = self.base.covmode
-        pairs = vo.c_estep_pairs(self._np, self.consts, self.T, nthreads=self.nthreads)
-        hz, Z = vo.c_responsibilities(pairs["LL_elbo"], tN, self.logOmega)
-        st = vo.c_statistics(Z, pairs, cov)
-        Lt1 = float((Z * pairs["LL_elbo"]).sum())
-        Lt7 = float((hz * np.log(hz)).sum())
-        self.hatZ = torch.from_numpy(hz)
-        self.LL = torch.from_numpy(pairs["LL_elbo"])
-        return torch.from_numpy(pack_stats(st["Nj"], st["N1"], st["M"], Lt1, Lt7, st["Nr"],
-                                           st["Y"], st["SC"], cov))
+        KT = self.K // self.trials
+        vecs, hzs, lls = [], [], []
+        for r in range(self.trials):
+            sl = slice(r * KT, (r + 1) * KT)
+            consts = {k: v[sl] for k, v in self.consts.items()}
+            pairs = vo.c_estep_pairs(self._np, consts, self.T, nthreads=self.nthreads)
+            hz, Z = vo.c_responsibilities(pairs["LL_elbo"], tN, self.logOmega[sl])
+            st = vo.c_statistics(Z, pairs, cov)
+            Lt1 = float((Z * pairs["LL_elbo"]).sum())
+            Lt7 = float((hz * np.log(hz)).sum())
+            hzs.append(hz)
+            lls.append(pairs["LL_elbo"])
+            vecs.append(pack_stats(st["Nj"], st["N1"], st["M"], Lt1, Lt7, st["Nr"], st["Y"],
+                                   st["SC"], cov))
+        self.hatZ = torch.from_numpy(np.concatenate(hzs, axis=1))
+        self.LL = torch.from_numpy(np.concatenate(lls, axis=1))
+        return torch.from_numpy(np.concatenate(vecs))

@@ -117,3 +117,28 @@ def test_em_trials_match_separate_runs(vb):
         assert np.allclose(a.post.m, b.post.m, rtol=1e-9, atol=1e-12)
         assert rel_err(a.hatZ.cpu().numpy(), b.hatZ.cpu().numpy()) < 1e-8
     assert tr.best == int(np.argmax([s.LL for s in singles]))
+
+
+def test_em_trials_host_logic_cpu(vb):
+    """vbhem_h3m_c_trials on the oracle stand-in engine (CPU): every trial follows
+    vbhem_h3m_c_step_fc exactly (iterations, bounds, posteriors, labels), a trial
+    that stops early keeps its own last E-step, and the best trial is argmax LL."""
+    from oracle_engine import OracleEngine
+    from vbhem_amd import em
+    N, K, S, Sb, d, cov, T, R = 24, 3, 3, 3, 2, 1, 6, 3
+    cs = make_case(N, K, S, Sb, d, cov, seed=5, tau=T)
+    posts = _trial_posts(cs, R, 5)
+    opt = dict(cs["opt"], max_iter=15, minDiff=1e-5)
+    bs = vb.BaseSet.from_numpy(cs["base"])
+    tr = em.vbhem_h3m_c_trials(posts, OracleEngine(bs, R * K, S, T, nthreads=1, trials=R), opt)
+    iters = []
+    for r in range(R):
+        one = em.vbhem_h3m_c_step_fc(posts[r], OracleEngine(bs, K, S, T, nthreads=1), opt)
+        a = tr.results[r]
+        assert a.iters == one.iters
+        np.testing.assert_array_equal(a.LogLs, one.LogLs)
+        np.testing.assert_array_equal(a.post.m, one.post.m)
+        np.testing.assert_array_equal(a.hatZ.numpy(), one.hatZ.numpy())
+        np.testing.assert_array_equal(a.label.numpy(), one.label.numpy())
+        iters.append(one.iters)
+    assert tr.best == int(np.argmax(tr.LLall))
