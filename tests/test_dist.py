@@ -70,3 +70,56 @@ def test_gloo_two_ranks_match_single_process(tmp_path, name):
     hz = np.concatenate([r0["hatZ"], r1["hatZ"]])
     np.testing.assert_allclose(hz, single["hatZ"], rtol=1e-9, atol=1e-300)
     assert int(r0["hi"]) == int(r1["lo"])
+
+
+def _run_trials(N, world, rank, outdir, port):
+    import torch.distributed as dist
+
+    import pkgload
+    from oracle_engine import OracleEngine
+
+    vb = pkgload.load()
+    from vbhem_amd.dist import make_allreduce, shard_range
+    from vbhem_amd.em import vbhem_h3m_c_trials
+
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    base, P, opt = vb.synth_workload("C2", N=N)
+    posts = [P.copy()]
+    for r in (1, 2):
+        Q = P.copy()
+        rng = np.random.default_rng(r)
+        Q.m = Q.m + rng.normal(0.0, 0.5, Q.m.shape)
+        posts.append(Q)
+    lo, hi = shard_range(N, rank, world)
+    eng = OracleEngine(base.shard(lo, hi), 3 * P.K, P.S, opt["tau"], nthreads=1, trials=3)
+    tr = vbhem_h3m_c_trials(posts, eng, dict(opt, max_iter=6), total_N=N,
+                            allreduce=make_allreduce())
+    np.savez(os.path.join(outdir, f"t{rank}_w{world}.npz"), LLall=tr.LLall, best=tr.best,
+             m=np.stack([r.post.m for r in tr.results]),
+             LogLs=np.stack([np.pad(r.LogLs, (0, 7 - len(r.LogLs))) for r in tr.results]))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _trials_worker(rank, N, world, outdir, port):
+    _run_trials(N, world, rank, outdir, port)
+
+
+@pytest.mark.slow
+def test_gloo_two_ranks_batched_trials(tmp_path):
+    """Batched trials (one statistics vector of R sections, one all-reduce per
+    iteration) on 2 gloo ranks vs one process."""
+    N = 30
+    _run_trials(N, 1, 0, str(tmp_path), 0)
+    port = _free_port()
+    mp.spawn(_trials_worker, args=(N, 2, str(tmp_path), port), nprocs=2, join=True)
+    single = np.load(tmp_path / "t0_w1.npz")
+    r0, r1 = np.load(tmp_path / "t0_w2.npz"), np.load(tmp_path / "t1_w2.npz")
+    for k in ("LLall", "m", "LogLs"):
+        np.testing.assert_array_equal(r0[k], r1[k])
+        np.testing.assert_allclose(r0[k], single[k], rtol=1e-10, err_msg=k)
+    assert int(r0["best"]) == int(single["best"])
