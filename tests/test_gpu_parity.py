@@ -60,14 +60,23 @@ def fused_mode(request):
     _capi.set_fused_mode(prev)
 
 
+@pytest.fixture(params=[("gated", 100.0), ("dense", 100.0), ("gated", 1e-9)],
+                ids=["gated-Nv100", "dense-Nv100", "gated-allgated"])
+def mode_tscale(request):
+    """(schedule, tscale): the all-gated edge case targets the gated schedule only."""
+    from vbhem_amd import _capi
+    mode, tscale = request.param
+    prev = _capi.set_fused_mode(_capi.FUSED_GATED if mode == "gated" else _capi.FUSED_DENSE)
+    yield tscale
+    _capi.set_fused_mode(prev)
+
+
 @pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
-@pytest.mark.parametrize("tscale", [100.0, 1e-9], ids=["Nv100", "allgated"])
-def test_fused_matches_oracle(vb, vo, shape, fused_mode, tscale):
+def test_fused_matches_oracle(vb, vo, shape, mode_tscale):
     """tscale = Nv: 100 (the configs' virtual samples: Z mostly one-hot, the gate
     drops most pairs) and 1e-9 (every Z < 1e-8: no pair passes the gate)."""
     name, N, K, S, Sb, d, cov, T, ragged = shape
-    if tscale != 100.0 and fused_mode == "dense":
-        pytest.skip("gate-edge case targets the gated schedule")
+    tscale = mode_tscale
     cs = make_case(N, K, S, Sb, d, cov, seed=seed_of(name) + 1, ragged=ragged, tau=T)
     base, consts = cs["base"], cs["consts"]
     pairs = vo.c_estep_pairs(base, consts, T, nthreads=4)
