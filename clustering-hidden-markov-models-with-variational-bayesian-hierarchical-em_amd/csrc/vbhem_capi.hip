@@ -24,20 +24,36 @@ namespace {
 thread_local std::string g_err;
 
 // Optional kernel timing (bench/profiling): hipEvents recorded on the launch
-// stream around each fb_pairs_kernel / stats_kernel launch; read back (and
-// synchronised) only by vbhem_timing_read.  Off by default (graph capture).
+// stream around each kernel launch; read back (and synchronised) only by
+// vbhem_timing_read*.  Off by default.  Per host thread (thread_local), like the
+// schedule below: the library keeps no state shared between threads, so several
+// host threads may drive it at once (the reference MEX is re-entrant).  Never
+// recorded into a stream that is being captured into a graph: a captured event
+// would be destroyed by the next vbhem_timing_read while the graph still
+// records into it on every replay.
 struct TimingState {
   bool on = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em, gf;
   std::vector<long long> fb_pairs;
 };
-TimingState g_timing;
+thread_local TimingState g_timing;
 
-// fused schedule (vbhem_set_fused_mode; VBHEM_FUSED_DENSE=1 in the environment)
-int g_fused_mode = [] {
+// fused schedule of this host thread (vbhem_set_fused_mode; VBHEM_FUSED_DENSE=1
+// in the environment sets every thread's default)
+int default_fused_mode() {
   const char *ev = std::getenv("VBHEM_FUSED_DENSE");
   return (ev && std::atoi(ev) != 0) ? VBHEM_FUSED_DENSE : VBHEM_FUSED_GATED;
-}();
+}
+thread_local int g_fused_mode = default_fused_mode();
+
+// timing is recorded for this launch: enabled on this thread and the stream
+// is not capturing
+bool timing_on(hipStream_t st) {
+  if (!g_timing.on) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
+  return cs == hipStreamCaptureStatusNone;
+}
 
 hipEvent_t timing_event(hipStream_t st) {
   hipEvent_t ev = nullptr;
@@ -64,7 +80,7 @@ namespace {
 
 constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
-constexpr int kExactThreads = vbhem::kExactBlock;  // fallback kernel threads
+constexpr int kExactThreads = vbhem::kExactBlock * vbhem::kExactBlocks;  // fallback threads
 constexpr int kChunkMinBases = 32;                 // fused epilogue: bases per chunk, at least
 constexpr size_t kGroupBudget = (size_t)8 << 30;  // per-pair buffers per group (fused)
 constexpr int kMaxSlabs = 512;    // statistics chunks (= resp/stats blocks per group)
@@ -240,7 +256,7 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
                    PairsWs &w) {
   Carver cv(ws);
   const size_t np = (size_t)b->N * c->K;
-  w.flags = cv.take<int>(2 + np);
+  w.flags = cv.take<int>(vbhem::kFlagHead + np);
   w.scratch = cv.take<double>(exact_stride(c->S, b->SB, T) * kExactThreads);
   w.tnu = need_tnu ? cv.take<double>(np * c->S * b->SB) : nullptr;
   w.E = cv.take<double>(np * c->S * b->SB);
@@ -275,7 +291,7 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   if (const char *ev = std::getenv("VBHEM_NSLAB")) maxslab = std::max(1, std::min(8192, std::atoi(ev)));
   w.nslab = std::min<int>(w.group, maxslab);
   w.slab_len = R * (int)vbhem_stats_len(K / R, S, b->d, b->covmode);
-  w.flags = cv.take<int>(2 + g * K);
+  w.flags = cv.take<int>(vbhem::kFlagHead + g * K);
   w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   w.nu1 = cv.take<double>(g * K * S);
   w.xi = cv.take<double>(g * K * S * S);
@@ -366,16 +382,16 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   ca.E = Ebuf; ca.e_ld = e_ld;
   ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
   ca.LL = nullptr; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
-  ca.flag_count = flags; ca.flag_list = flags + 2;
+  ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
   ca.list = list; ca.list_tot = list_tot; ca.list_cap = list_cap;
-  hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
+  hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
   hipError_t e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_list), c.split.lds_list, st);
   if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
-  if (g_timing.on) g_timing.gf.emplace_back(ev0, timing_event(st));
+  if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin; a.i_end = i_end; a.i_buf0 = i_buf0;
   a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
-  a.flag_count = flags; a.flag_list = flags + 2;
+  a.flag_count = flags; a.flag_list = flags + vbhem::kFlagHead;
   e = vbhem::launch_fb_exact(a, scratch, exact_stride(a.S, a.SB, a.T), kExactThreads, st);
   if (e != hipSuccess) return hip_fail(e, "fb_exact_kernel");
   return VBHEM_OK;
@@ -394,7 +410,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   a.i_buf0 = i_buf0;
   a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
   a.flag_count = flags;
-  a.flag_list = flags + 2;
+  a.flag_list = flags + vbhem::kFlagHead;
   hipError_t e = hipSuccess;
   if (!c.split.ok) {  // split path: zeroed by emission_prep_kernel, reset by fb_exact_kernel
     e = hipMemsetAsync(flags, 0, sizeof(int), st);
@@ -403,12 +419,12 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   if (c.split.ok) {
     vbhem::EmissionArgs ea = c.em;
     ea.i_begin = i_begin; ea.i_end = i_end; ea.i_buf0 = i_buf0; ea.E = Ebuf; ea.e_ld = e_ld;
-    hipEvent_t em0 = g_timing.on ? timing_event(st) : nullptr;
+    hipEvent_t em0 = timing_on(st) ? timing_event(st) : nullptr;
     e = vbhem::launch_emission(ea, c.em_lds, st);
     if (e != hipSuccess) return hip_fail(e, "emission_kernel");
-    if (g_timing.on) g_timing.em.emplace_back(em0, timing_event(st));
+    if (em0) g_timing.em.emplace_back(em0, timing_event(st));
   }
-  hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
+  hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
   if (c.split.ok) {
     const SplitPlan &sp = mode == vbhem::kFbBackward ? c.bwd : c.split;
     vbhem::SplitArgs ca = sp.a;
@@ -416,7 +432,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     ca.E = Ebuf; ca.e_ld = e_ld;
     ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
     ca.LL = LL; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
-    ca.flag_count = flags; ca.flag_list = flags + 2;
+    ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
     const unsigned ntile = (unsigned)((i_end - i_begin + sp.ppb - 1) / sp.ppb);
     unsigned grid = ntile * (unsigned)ca.K;
     if (mode == vbhem::kFbBackward) {  // persistent: NB blocks per cluster (x8 when possible)
@@ -432,7 +448,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     e = vbhem::launch_fb(a, grid, c.plan.block, c.plan.lds, st);
     if (e != hipSuccess) return hip_fail(e, "fb_pairs_kernel");
   }
-  if (g_timing.on) {
+  if (ev0) {
     g_timing.fb.emplace_back(ev0, timing_event(st));
     g_timing.fb_pairs.push_back((long long)(i_end - i_begin) * a.K);
   }
@@ -490,10 +506,10 @@ int estep_pairs_impl(const vbhem_base_t *base, const vbhem_cluster_t *clus, int 
   rc = prepare_fb(ctx, base, clus, T, smooth);
   if (rc != VBHEM_OK) return rc;
   if (!ctx.split.ok) {
-    hipError_t e0 = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
+    hipError_t e0 = hipMemsetAsync(w.flags, 0, vbhem::kFlagHead * sizeof(int), st);
     if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
   }
-  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, 2);
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, vbhem::kFlagHead);
   if (rc != VBHEM_OK) return rc;
   rc = run_fb(ctx, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.E,
               (long long)base->N * base->SB, w.flags,
@@ -611,11 +627,12 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(slabs)");
   }
   if (!ctx.split.ok) {
-    e = hipMemsetAsync(w.flags, 0, 2 * sizeof(int), st);
+    e = hipMemsetAsync(w.flags, 0, vbhem::kFlagHead * sizeof(int), st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
   }
   if (gated) ctx.bwd.a.Atg = w.Atg;
-  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, 2, gated ? w.Atg : nullptr,
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, vbhem::kFlagHead,
+                         gated ? w.Atg : nullptr,
                          clus->logA);
   if (rc != VBHEM_OK) return rc;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
@@ -627,24 +644,24 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     sa.assign = gated && g0 == 0;
     const int nchunk = std::max(1, chunks(g1 - g0));
-    hipEvent_t ev0 = g_timing.on ? timing_event(st) : nullptr;
+    hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
     e = vbhem::launch_resp(sa, nchunk, st);
     if (e != hipSuccess) return hip_fail(e, "resp_kernel");
     if (gated) {
       e = vbhem::launch_gate_list(sa, nchunk, st);
       if (e != hipSuccess) return hip_fail(e, "gate_list_kernel");
-      if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
+      if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
       rc = run_fb_list(ctx, g0, g1, g0, w.nu1, w.xi, w.tnu, w.E, e_ld, w.list, w.list_tot,
                        w.group, w.flags, w.scratch, LL_elbo_dev, st);
       if (rc != VBHEM_OK) return rc;
-      ev0 = g_timing.on ? timing_event(st) : nullptr;
+      ev0 = timing_on(st) ? timing_event(st) : nullptr;
       e = vbhem::launch_stats_list(sa, nchunk, sl_lds, st);
       if (e != hipSuccess) return hip_fail(e, "stats_list_kernel");
     } else {
       e = vbhem::launch_stats(sa, nchunk, ngroups, slds, st);
       if (e != hipSuccess) return hip_fail(e, "stats_kernel");
     }
-    if (g_timing.on) g_timing.stats.emplace_back(ev0, timing_event(st));
+    if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
   e = vbhem::launch_stats_final(w.slabs, nslab_used, w.slab_len, stats_dev, st);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");

@@ -69,20 +69,33 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
     p.Atg[(size_t)r * p.S + tid] = exp_nonpos(la[tid] - mx);
   }
   // z: coordinate a = tid % d, the rows q = part, part + NP, ... summed by thread
-  // (a, part), then the NP parts of each coordinate in order (d <= 64)
+  // (a, part), then the NP parts of each coordinate in order (d <= 64).  Only
+  // finite means count: a diverged cluster (NaN constants, e.g. one trial of a
+  // batched launch) must not poison the shift, and so every other cluster's E.
   const int NP = kPrepThreads / d, part = tid / d, a0 = tid - part * d;
   if (part < NP) {
-    double s = 0.0;
-    for (int q = part; q < KS; q += NP) s += p.m[(size_t)q * d + a0];
+    double s = 0.0, n = 0.0;
+    for (int q = part; q < KS; q += NP) {
+      const double v = p.m[(size_t)q * d + a0];
+      if (isfinite(v)) {
+        s += v;
+        n += 1.0;
+      }
+    }
     zp[tid] = s;
+    pm[tid] = n;
   }
   __syncthreads();
   for (int a = tid; a < d; a += kPrepThreads) {
-    double s = 0.0;
-    for (int q = 0; q < NP; ++q) s += zp[q * d + a];
-    zs[a] = s / (double)KS;
+    double s = 0.0, n = 0.0;
+    for (int q = 0; q < NP; ++q) {
+      s += zp[q * d + a];
+      n += pm[q * d + a];
+    }
+    zs[a] = n > 0.0 ? s / n : 0.0;
     if (r == 0) p.shift[a] = zs[a];
   }
+  __syncthreads();  // pm is reused below
   __syncthreads();
   // W' = -W/2 and bias' = -bias/2 (exact scalings), so E = bias' + sum W' U;
   // rows r >= K*S and k-rows e >= KD are the zero padding of the [kdp][ksp] layout

@@ -566,13 +566,26 @@ void fb_split_kernel(const SplitArgs p) {
         }
       }
     }
-    // fallback flags (one per pair)
-    if (bad && active) F[q] = 1;
+    // fallback flags (one per pair).  !(Z >= kZMinS) also catches NaN; a pair whose
+    // inputs are not finite (a diverged cluster) is not sent to the exact fallback,
+    // its L_elbo is NaN (the table-driven log need not propagate NaN by itself)
+    if (bad && active) {
+      bool nf = false;
+#pragma unroll
+      for (int k = 0; k < SH; ++k) nf |= (r0 + k < S) && !isfinite(E[k]);
+      for (int x = 0; x < S; ++x) nf |= isnan(amax[x]) || isnan(lpi[x]);
+      atomicOr(&F[q], kFlagBad | (nf ? kFlagNonFinite : 0));
+    }
     pair_sync<kWaveLocal>();
-    if (active && w == 0 && F[q]) {
-      const int slot = atomicAdd(pa.flag_count, 1);
-      atomicAdd(pa.flag_count + 1, 1);
-      pa.flag_list[slot] = (int)pair;
+    if (active && w == 0) {
+      const int f = F[q];
+      if (f == kFlagBad) {
+        const int slot = atomicAdd(pa.flag_count, 1);
+        atomicAdd(pa.flag_count + 1, 1);
+        pa.flag_list[slot] = (int)pair;
+      } else if ((f & kFlagNonFinite) && MODE != kFbList) {
+        pa.LL[pair] = __builtin_nan("");
+      }
     }
   };
 

@@ -14,25 +14,34 @@ namespace vbhem {
 // record `msg` for vbhem_last_error() and return `code` (vbhem_capi.hip)
 int set_error(int code, const std::string &msg);
 
-// Host-side launch helpers: the dynamic-LDS attribute and the occupancy query
-// are per (kernel, block, LDS) facts, so they are asked once and remembered
-// (every fused E-step launches the same kernels with the same geometry).
+// Host-side launch helpers: the dynamic-LDS attribute, the occupancy query and
+// the CU count are per (device, kernel, block, LDS) facts, so they are asked
+// once per device and remembered (every fused E-step launches the same kernels
+// with the same geometry).  Keyed by the caller's current device: a process that
+// drives several GPUs gets each device's own answers.
+inline int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  return dev;
+}
 inline hipError_t set_dyn_lds(const void *fn, size_t lds) {
   static std::mutex mu;
-  static std::map<const void *, size_t> done;  // largest LDS size already allowed
+  static std::map<std::pair<int, const void *>, size_t> done;  // largest LDS already allowed
+  const auto key = std::make_pair(current_device(), fn);
   std::lock_guard<std::mutex> g(mu);
-  auto it = done.find(fn);
+  auto it = done.find(key);
   if (it != done.end() && it->second >= lds) return hipSuccess;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e == hipSuccess) done[fn] = lds;
+  if (e == hipSuccess) done[key] = lds;
   return e;
 }
 inline int resident_per_cu(const void *fn, int threads, size_t lds) {
   static std::mutex mu;
-  static std::map<std::tuple<const void *, int, size_t>, int> memo;
+  static std::map<std::tuple<int, const void *, int, size_t>, int> memo;
+  const auto key = std::make_tuple(current_device(), fn, threads, lds);
   {
     std::lock_guard<std::mutex> g(mu);
-    auto it = memo.find(std::make_tuple(fn, threads, lds));
+    auto it = memo.find(key);
     if (it != memo.end()) return it->second;
   }
   int n = 0;
@@ -40,20 +49,24 @@ inline int resident_per_cu(const void *fn, int threads, size_t lds) {
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, lds) != hipSuccess || n < 1)
     return 1;  // not remembered: ask again next time
   std::lock_guard<std::mutex> g(mu);
-  memo[std::make_tuple(fn, threads, lds)] = n;
+  memo[key] = n;
   return n;
 }
 inline int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      cus = n;
-    else
-      return 256;
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  const int dev = current_device();
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cus.find(dev);
+    if (it != cus.end()) return it->second;
   }
-  return cus;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+    return 256;  // not remembered
+  std::lock_guard<std::mutex> g(mu);
+  cus[dev] = n;
+  return n;
 }
 
 constexpr int kCovDiag = 0;
@@ -185,7 +198,19 @@ hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream
 int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mode
 
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
-constexpr int kExactBlock = 256;  // fb_exact_kernel: one block of this many threads
+// Fallback bookkeeping in the workspace's int array `flags`:
+//   [0] pairs flagged by the current pass (consumed and reset by fb_exact_kernel)
+//   [1] pairs flagged over the whole call (vbhem_last_fallback_count)
+//   [2] fb_exact_kernel blocks finished (the last one resets [0] and [2])
+//   [kFlagHead ...] the flagged pair indices
+// A pair is flagged only when its factorised normaliser underflowed with finite
+// inputs; pairs whose cluster constants or emissions are not finite (a diverged
+// EM trial) are not flagged: their L_elbo is written as NaN, as the reference's
+// arithmetic would produce, and they cost the fallback nothing.
+constexpr int kFlagHead = 3;
+constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
+constexpr int kExactBlock = 256;   // fb_exact_kernel: threads per block
+constexpr int kExactBlocks = 8;    // fb_exact_kernel: blocks (grid-stride over the list)
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
                            hipStream_t st);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t st);

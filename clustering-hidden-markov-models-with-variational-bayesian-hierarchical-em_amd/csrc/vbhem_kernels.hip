@@ -349,10 +349,14 @@ __global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
       const int ro = o / S, so = o - ro * S;
       p.xi[lp * S * S + o] = Atj[ro * AS + so] * H[o];
     }
-    if (bad) pflag[q] = 1;
+    if (bad) {  // underflow, or non-finite inputs (NaN propagates through exp/log here)
+      bool nf = !isfinite(E);
+      for (int s = 0; s < S; ++s) nf |= isnan(Atj[a * AS + s]) || isnan(amaxj[s]);
+      atomicOr(&pflag[q], kFlagBad | (nf ? kFlagNonFinite : 0));
+    }
   }
   __syncthreads();
-  if (active && e == 0 && pflag[q]) {
+  if (active && e == 0 && pflag[q] == kFlagBad) {
     const int slot = atomicAdd(p.flag_count, 1);
     atomicAdd(p.flag_count + 1, 1);
     p.flag_list[slot] = (int)pair;
@@ -361,15 +365,18 @@ __global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
 
 // ---------------------------------------------------------------------------
 // fb_exact_kernel: reference-order recursion for flagged pairs (one thread per
-// pair, Theta in global scratch).  Mirrors mex.c:715-1298 step by step.  One
-// block: it consumes the pass's flag counter and resets it to zero on exit, so
-// the next pass needs no memset of its own (flag_count[1] keeps the total).
+// pair, grid-stride over the list; Theta in global scratch).  Mirrors
+// mex.c:715-1298 step by step.  kExactBlocks blocks consume the pass's flag
+// counter; the last block to finish resets it (and the blocks-done counter) to
+// zero, so the next pass needs no memset of its own (flag_count[1] keeps the
+// total).  Every block reads the count before it signals completion, so the
+// reset can never race a read.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kExactBlock) void fb_exact_kernel(const FbArgs p, double *scratch,
                                                       size_t scratch_stride) {
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int nt = gridDim.x * blockDim.x;
-  const int cnt = *p.flag_count;
+  const int cnt = __atomic_load_n(p.flag_count, __ATOMIC_RELAXED);
   const int S = p.S, SB = p.SB, d = p.d, T = p.T;
   double *w = scratch + (size_t)gt * scratch_stride;
   double *E = w, *L = E + S * SB, *Ln = L + S * SB, *lt = Ln + S * SB, *nu = lt + S * SB,
@@ -476,8 +483,14 @@ __global__ __launch_bounds__(kExactBlock) void fb_exact_kernel(const FbArgs p, d
     }
     for (int k = 0; k < S * SB; ++k) p.tnu[lp * S * SB + k] = tn[k];
   }
-  __syncthreads();  // every thread has read the count
-  if (threadIdx.x == 0) *p.flag_count = 0;
+  __syncthreads();  // every thread of this block has read the count
+  if (threadIdx.x == 0) {
+    const int done = atomicAdd(p.flag_count + 2, 1);
+    if (done == (int)gridDim.x - 1) {  // last block: everyone has read the count
+      atomicExch(p.flag_count, 0);
+      atomicExch(p.flag_count + 2, 0);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -551,8 +564,10 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
                            hipStream_t st) {
-  if (nthreads != kExactBlock) return hipErrorInvalidValue;  // single self-resetting block
-  hipLaunchKernelGGL(fb_exact_kernel, dim3(1), dim3(kExactBlock), 0, st, a, scratch, stride);
+  // the scratch holds kExactBlocks * kExactBlock thread slots (vbhem_capi.hip)
+  if (nthreads != kExactBlock * kExactBlocks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fb_exact_kernel, dim3(kExactBlocks), dim3(kExactBlock), 0, st, a, scratch,
+                     stride);
   return hipGetLastError();
 }
 

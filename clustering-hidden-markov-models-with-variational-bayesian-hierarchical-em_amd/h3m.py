@@ -246,7 +246,8 @@ def _digamma(x: torch.Tensor) -> torch.Tensor:
 
 def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
                    device="cpu", exprmt1: bool = False, ragged: bool = False,
-                   n_total: Optional[int] = None, i_offset: int = 0) -> BaseSet:
+                   n_total: Optional[int] = None, i_offset: int = 0,
+                   face: bool = False) -> BaseSet:
     """Synthetic h3m_b built directly in packed form (use_post=1 semantics).
 
     Ground truth: K HMMs, base i is a noisy copy of GT g = i mod K: means
@@ -255,6 +256,9 @@ def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
     alpha = 1+25*pi, epsilon = 1+250*A, beta = 1+250/Sb, then the
     hmms_to_h3m_hem(use_post=1) transform.  exprmt1=True uses the two GT HMMs
     of Synthetic_experiment/exprmt1_sampledata.m:20-43 instead (Sb=d=2).
+    face=True draws eye-fixation-scale emissions (demo/vbdemo_face.m: screen
+    pixels): GT means [256, 192, 150, ...][:d] + U[-60, 60]^d, per-base mean
+    noise N(0, 5^2), covariances 900 (L L'/d + 0.5 I) (about 30 px spread).
     ragged=True draws per-base state counts in [1, Sb] (zero-padded).
     Generated on ``device``; ``n_total``/``i_offset`` place this block of N
     bases inside a larger set (omega = 1/n_total, GT index (i_offset+i) mod K)."""
@@ -280,6 +284,10 @@ def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
             gt_cov = Lm @ Lm.transpose(-1, -2) / d + 0.5 * torch.eye(d, dtype=dt)
         else:
             gt_cov = 0.5 + torch.rand((G, Sb, d), generator=gcpu, dtype=dt)
+        if face:
+            centre = torch.tensor(([256.0, 192.0, 150.0] + [128.0] * d)[:d], dtype=dt)
+            gt_mu = centre + (gt_mu / 5.0 - 0.5) * 120.0
+            gt_cov = 900.0 * gt_cov
     gt_prior, gt_A, gt_mu, gt_cov = (x.to(device) for x in (gt_prior, gt_A, gt_mu, gt_cov))
     gi = (torch.arange(N, device=device) + int(i_offset)) % G
     alpha = 1.0 + 25.0 * gt_prior[gi]
@@ -287,7 +295,8 @@ def synth_base_set(N: int, K: int, Sb: int, d: int, covmode: int, seed: int,
     beta = 1.0 + 250.0 / Sb
     prior = torch.exp(_digamma(alpha) - _digamma(alpha.sum(-1, keepdim=True)))
     A = torch.exp(_digamma(eps) - _digamma(eps.sum(-1, keepdim=True)))
-    centres = gt_mu[gi] + 0.1 * torch.randn((N, Sb, d), generator=g, dtype=dt, device=device)
+    noise = 5.0 if face else 0.1
+    centres = gt_mu[gi] + noise * torch.randn((N, Sb, d), generator=g, dtype=dt, device=device)
     covars = ((beta + 1.0) / beta) * gt_cov[gi]
     nstates = torch.full((N,), Sb, dtype=torch.int32, device=device)
     if ragged and Sb > 1:

@@ -22,6 +22,14 @@
  *   - Functions return VBHEM_OK (0) or a negative status; vbhem_last_error()
  *     gives a message.  Nothing synchronises the stream except the *_host
  *     convenience entry point.
+ *   - Re-entrant: the library keeps no state shared between host threads (the
+ *     error message, the fused schedule and the timing records are per thread;
+ *     the launch-attribute caches are per device and locked).  Each concurrent
+ *     call needs its own workspace.
+ *   - The device-pointer entry points enqueue kernels and memsets only (no
+ *     allocation, no host synchronisation, no per-call host state in device
+ *     memory), so a call may be captured into a HIP graph and replayed; the
+ *     workspace's fallback counters reset themselves on the device.
  */
 #ifndef VBHEM_ESTEP_H
 #define VBHEM_ESTEP_H
@@ -146,8 +154,8 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
                              double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
                              void *workspace_dev, size_t workspace_bytes, void *stream);
 
-/* Fused E-step schedule (process-wide; default VBHEM_FUSED_GATED, or set the
- * environment variable VBHEM_FUSED_DENSE=1).  Both give the same outputs:
+/* Fused E-step schedule of the calling host thread (default VBHEM_FUSED_GATED,
+ * or VBHEM_FUSED_DENSE=1 in the environment).  Both give the same outputs:
  *   VBHEM_FUSED_GATED  backward sweep + log-likelihood for every pair, then the
  *                      forward sweep and statistics only for the pairs the gate
  *                      Z > 1e-8 of vbhem_compute_Statistics.m:35 keeps (the
@@ -163,9 +171,10 @@ int vbhem_set_fused_mode(int mode);
  * log-sum-exp fell below its safe range.  Synchronises `stream`. */
 int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
 
-/* Kernel timing for benchmarking/profiling (not for graph capture): while
- * enabled, hipEvents are recorded on the launch stream around every
- * fb_pairs_kernel and stats_kernel launch of this process.  vbhem_timing_read
+/* Kernel timing for benchmarking/profiling, per host thread: while enabled,
+ * hipEvents are recorded on the launch stream around every fb / stats kernel
+ * launch of this thread (never into a stream that is capturing a graph: such
+ * launches are simply not timed).  vbhem_timing_read
  * synchronises on them, returns the summed elapsed milliseconds, the launch
  * counts and the number of (i,j) pairs the fb launches covered, and resets. */
 int vbhem_timing_enable(int on);

@@ -21,13 +21,16 @@ def post_dict(post) -> dict:
 
 
 def make_case(N=6, K=3, S=3, Sb=3, d=2, covmode=1, seed=0, ragged=False, perturb=True,
-              tau=10, exprmt1=False, **opt_over):
+              tau=10, exprmt1=False, face=False, Nv=100, **opt_over):
     """Returns dict(base=numpy base dict, post=posterior dict, consts=E-step constants
     (oracle prelude), opt=options, T=tau, bs=BaseSet, P=Posterior)."""
     bs = vb.synth_base_set(N, K, Sb, d, covmode, seed=1000 + seed, device="cpu",
-                           exprmt1=exprmt1, ragged=ragged)
+                           exprmt1=exprmt1, ragged=ragged, face=face)
     v0 = max(5.0, d + 1.0)
-    opt = vb.default_options(K, S, d, tau=tau, Nv=100, covmode=covmode, v0=v0, **opt_over)
+    if face:  # demo/vbdemo_face.m:49-61 hyperparameters (m0 defaults to [256, 192])
+        opt_over = dict(dict(W0=0.001, v0=10.0), **opt_over)
+        v0 = opt_over.pop("v0")
+    opt = vb.default_options(K, S, d, tau=tau, Nv=Nv, covmode=covmode, v0=v0, **opt_over)
     rb, rg, om = vb.baseem_draws(bs, K, S, seed=77 + seed)
     P = vb.baseem_init(bs, opt, rb, rg, om)
     if perturb:
@@ -38,7 +41,7 @@ def make_case(N=6, K=3, S=3, Sb=3, d=2, covmode=1, seed=0, ragged=False, perturb
         P.v = P.v + rng.uniform(0.0, 3.0, P.v.shape)
         sc = rng.uniform(0.7, 1.3, P.v.shape)
         P.W = P.W * (sc[..., None, None] if covmode == 1 else sc[..., None])
-        P.m = P.m + rng.normal(0.0, 0.3, P.m.shape)
+        P.m = P.m + rng.normal(0.0, 8.0 if face else 0.3, P.m.shape)
         P.alpha = P.alpha * rng.uniform(0.5, 1.5, P.alpha.shape)
     base = bs.numpy()
     post = post_dict(P)

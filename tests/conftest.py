@@ -139,9 +139,53 @@ def mathcheck():
 
 
 def rel_err(a, b, floor=1e-300):
+    """Normwise: max|a - b| / max|b| (an extra check; the parity gates use elem_err)."""
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     if a.size == 0:
         return 0.0
     scale = max(np.abs(b).max(), floor)
     return float(np.abs(a - b).max() / scale)
+
+
+# BASELINE.md: hat_Z entries below 1e-8 are compared in absolute terms (Nv = 100
+# makes hat_Z nearly one-hot); everything else element by element.
+ZHAT_ABS_FLOOR = 1e-8
+
+
+def elem_err(a, b, floor_abs=0.0, floor_rel=0.0):
+    """Elementwise relative error  max_i |a_i - b_i| / max(|b_i|, floor),
+    floor = max(floor_abs, floor_rel * max|b|): every entry at or above the floor
+    is held to the relative bound on its own, entries below it to rtol * floor
+    absolutely.  NaN in either operand counts as an infinite error unless both
+    are NaN at the same place."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    if a.size == 0:
+        return 0.0
+    both_nan = np.isnan(a) & np.isnan(b)
+    if (np.isnan(a) ^ np.isnan(b)).any():
+        return float("inf")
+    floor = max(floor_abs, floor_rel * float(np.abs(np.where(both_nan, 0.0, b)).max()), 1e-300)
+    d = np.where(both_nan, 0.0, np.abs(a - b))
+    return float((d / np.maximum(np.abs(np.where(both_nan, 1.0, b)), floor)).max())
+
+
+def hatz_err(a, b):
+    """hat_Z parity metric (elementwise, absolute below ZHAT_ABS_FLOOR)."""
+    return elem_err(a, b, floor_abs=ZHAT_ABS_FLOOR)
+
+
+def post_err(a, b):
+    """Posterior parity metric (north-star 1e-5): elementwise relative, with an
+    absolute floor of 1e-8 of the array's largest entry (entries that are zero up
+    to cancellation, e.g. a mean coordinate at the origin)."""
+    return elem_err(a, b, floor_rel=1e-8)
+
+
+def stat_err(a, b):
+    """Statistics parity metric for the tight (1e-9 .. 1e-10) bounds: elementwise
+    relative with a floor of 1e-5 of the largest entry.  Sums whose terms cancel
+    (first moments of means near the origin) are only determined to ~1e-16 of
+    the sum of |terms|, so entries far below the largest are held absolutely."""
+    return elem_err(a, b, floor_rel=1e-5)

@@ -8,8 +8,10 @@
 * full-size (C4, N = 100,000) size-independent properties: determinism, shard
   additivity, normalisation and mass rules, and a sampled oracle comparison.
 
-Tolerances: per-pair outputs RTOL_PAIRS = 1e-10 (normwise relative);
-statistics 1e-9; hat_Z / ELBO the north-star 1e-5 (conftest.py).
+Tolerances (elementwise unless noted; conftest.elem_err / hatz_err / post_err):
+per-pair outputs RTOL_PAIRS = 1e-10 (normwise, and elementwise with a 1e-8
+relative floor); statistics 1e-9; hat_Z / posteriors / ELBO the north-star
+1e-5 (hat_Z entries below 1e-8 absolutely).
 """
 import ctypes
 import zlib
@@ -19,7 +21,7 @@ import pytest
 import torch
 
 from cases import SHAPES, make_case
-from conftest import RTOL_NORTH_STAR, RTOL_PAIRS, rel_err
+from conftest import RTOL_NORTH_STAR, RTOL_PAIRS, elem_err, hatz_err, post_err, rel_err, stat_err
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -47,8 +49,11 @@ def test_pairs_match_oracle(vb, vo, shape):
     got = eng.pairs(want_tnu=True)
     torch.cuda.synchronize()
     for k in PAIR_KEYS + ("sum_t_nu",):
-        e = rel_err(got[k].cpu().numpy(), ref[k])
+        g = got[k].cpu().numpy()
+        e = rel_err(g, ref[k])
         assert e < RTOL_PAIRS, (name, k, e)
+        e = stat_err(g, ref[k])
+        assert e < 1e-8, (name, k, e)
 
 
 @pytest.fixture(params=["gated", "dense"])
@@ -88,13 +93,13 @@ def test_fused_matches_oracle(vb, vo, shape, mode_tscale):
     vec = eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy()
     got = vb.host.unpack_stats(vec, K, S, d, cov)
     for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
-        assert rel_err(got[k], st[k]) < 1e-9, (name, k, rel_err(got[k], st[k]))
+        assert stat_err(got[k], st[k]) < 1e-9, (name, k, stat_err(got[k], st[k]))
     Lt1 = float((Z * pairs["LL_elbo"]).sum())
     Lt7 = float((hz * np.log(hz)).sum())
     assert abs(got["Lt1"] - Lt1) <= 1e-10 * abs(Lt1)
     assert abs(got["Lt7"] - Lt7) <= 1e-9 * abs(Lt7) + 1e-9
-    assert rel_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
-    assert rel_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+    assert hatz_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
 def test_fused_multigroup(vb, vo, fused_mode, monkeypatch):
@@ -113,9 +118,9 @@ def test_fused_multigroup(vb, vo, fused_mode, monkeypatch):
     eng.set_log_omega(logOmega)
     got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, cov)
     for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
-        assert rel_err(got[k], st[k]) < 1e-9, k
-    assert rel_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
-    assert rel_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+        assert stat_err(got[k], st[k]) < 1e-9, k
+    assert hatz_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
 def adversarial_case(cov=1, S=4, Sb=4, d=3, N=4, K=3, T=6):
@@ -160,7 +165,7 @@ def test_exact_fallback_fused(vb, vo, fused_mode):
     got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
     assert eng.fallback_count() > 0
     for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
-        assert rel_err(got[k], st[k]) < 1e-9, k
+        assert stat_err(got[k], st[k]) < 1e-9, k
 
 
 def test_host_pointer_entry_point(vb, vo, capi_lib):
@@ -303,7 +308,7 @@ def test_c4_sampled_oracle(vb, vo, c4_full):
     sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == base.N else v)
            for k, v in base.shard(0, base.N).numpy().items()}
     ref = vo.c_estep_pairs(sub, consts, c4_full["opt"]["tau"], nthreads=8)
-    assert rel_err(LL[idx], ref["LL_elbo"]) < RTOL_PAIRS
+    assert elem_err(LL[idx], ref["LL_elbo"]) < RTOL_PAIRS
 
 
 def test_c4_em_iterations_vs_oracle_sample(vb, vo):
@@ -318,8 +323,8 @@ def test_c4_em_iterations_vs_oracle_sample(vb, vo):
     ref = vo.em_step_fc(post_dict(P), base.numpy(), opt)
     np.testing.assert_allclose(res.LogLs, ref["LogLs"], rtol=RTOL_NORTH_STAR)
     for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
-        assert rel_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, k
-    assert rel_err(res.hatZ.cpu().numpy(), ref["hat_Z"]) < RTOL_NORTH_STAR
+        assert post_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, k
+    assert hatz_err(res.hatZ.cpu().numpy(), ref["hat_Z"]) < RTOL_NORTH_STAR
 
 
 # ----------------------------------------------------------------------------

@@ -1,0 +1,141 @@
+"""Parity at the scales the synthetic grids and the demo actually run at.
+
+* face scale (demo/vbdemo_face.m:49-61): means around [256, 192] px with ~30 px
+  spread, W0 = 0.001, v0 = 10, Nv = 10, tau = 5, d = 2 full, S in {1, 2, 3},
+  ragged base HMMs.  This pins the shifted, expanded quadratic form of the
+  emission GEMM where |mu| is large next to the spread
+  (hard part 3): per-pair outputs, the fused E-step and an EM
+  run against the oracle;
+* C3 at its full size (N = 10,000, K = 8, S = 5, d = 2 diag): every pair's
+  L_elbo, hat_Z and the statistics against the oracle;
+* a C5 slice (N = 1,000 of the 10^6 bases, K = 32, S = 12, d = 16 full): the
+  MFMA emission path for d > 8 at more than one MFMA tile, against the oracle.
+
+Tolerances are elementwise (conftest.elem_err / hatz_err / stat_err / post_err).
+"""
+import numpy as np
+import pytest
+import torch
+
+from cases import make_case, post_dict
+from conftest import RTOL_NORTH_STAR, RTOL_PAIRS, elem_err, hatz_err, post_err, stat_err
+
+DEV = "cuda:0"
+PAIR_KEYS = ("LL_elbo", "sum_nu_1", "sum_xi", "emit_pr", "emit_mu", "emit_Mu")
+
+
+def face_case(S, seed, N=80, K=4):
+    return make_case(N, K, S, 3, 2, 1, seed=seed, ragged=True, tau=5, face=True, Nv=10)
+
+
+def _engine(vb, base, consts, T, K=None, S=None):
+    from vbhem_amd.estep import EStepEngine
+    K0, S0 = consts["logPi"].shape
+    eng = EStepEngine(vb.BaseSet.from_numpy(base) if isinstance(base, dict) else base, K0, S0, T,
+                      device=DEV)
+    eng.set_clusters(consts)
+    return eng
+
+
+def test_face_scale_oracle_twin(vo):
+    """CPU: the two oracle restatements agree at face scale as well."""
+    for S in (1, 2, 3):
+        cs = face_case(S, seed=70 + S, N=12)
+        c = vo.c_estep_pairs(cs["base"], cs["consts"], cs["T"], want_tnu=True)
+        t = vo.twin_estep_pairs(cs["base"], cs["post"], cs["consts"], cs["T"])
+        for k in PAIR_KEYS:
+            assert stat_err(c[k], t[k]) < 1e-10, (S, k, stat_err(c[k], t[k]))
+        # the quadratic form is large: |E| reaches hundreds of nats here
+        assert np.abs(c["LL_elbo"]).max() > 10.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 2, 3])
+def test_face_scale_pairs(vb, vo, S):
+    cs = face_case(S, seed=60 + S)
+    ref = vo.c_estep_pairs(cs["base"], cs["consts"], cs["T"], nthreads=4, want_tnu=True)
+    got = _engine(vb, cs["base"], cs["consts"], cs["T"]).pairs(want_tnu=True)
+    torch.cuda.synchronize()
+    for k in PAIR_KEYS + ("sum_t_nu",):
+        g = got[k].cpu().numpy()
+        assert stat_err(g, ref[k]) < 1e-8, (S, k, stat_err(g, ref[k]))
+    assert elem_err(got["LL_elbo"].cpu().numpy(), ref["LL_elbo"]) < RTOL_PAIRS
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 2, 3])
+def test_face_scale_fused(vb, vo, S):
+    cs = face_case(S, seed=80 + S, N=120)
+    base, consts, T = cs["base"], cs["consts"], cs["T"]
+    N = base["prior"].shape[0]
+    pairs = vo.c_estep_pairs(base, consts, T, nthreads=4)
+    tN = 10.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, pairs, 1)
+    eng = _engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    vec = eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy()
+    K = consts["logPi"].shape[0]
+    got = vb.host.unpack_stats(vec, K, S, 2, 1)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, (S, k, stat_err(got[k], st[k]))
+    assert hatz_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 2, 3])
+def test_face_scale_em_vs_oracle(vb, vo, S):
+    """EM from the same initial posterior (6 iterations) on the GPU and in the oracle."""
+    from vbhem_amd.em import vbhem_h3m_c_step_fc
+    from vbhem_amd.estep import EStepEngine
+    cs = face_case(S, seed=90 + S, N=60, K=3)
+    opt = dict(cs["opt"], max_iter=6)
+    eng = EStepEngine(cs["bs"], 3, S, cs["T"], device=DEV)
+    res = vbhem_h3m_c_step_fc(cs["P"], eng, opt)
+    ref = vo.em_step_fc(post_dict(cs["P"]), cs["base"], opt)
+    assert res.iters == ref["iters"]
+    np.testing.assert_allclose(res.LogLs, ref["LogLs"], rtol=RTOL_NORTH_STAR)
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert post_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, (S, k)
+    assert hatz_err(res.hatZ.cpu().numpy(), ref["hat_Z"]) < RTOL_NORTH_STAR
+
+
+def _fused_vs_oracle(vb, vo, name, N=None, nthreads=8):
+    from vbhem_amd.em import tilde_n
+    from vbhem_amd.estep import EStepEngine
+    base, P, opt = vb.synth_workload(name, N=N)
+    cov = base.covmode
+    consts = vb.host.cluster_constants(P, cov)
+    logOm = vb.host.log_omega_tilde(P.alpha)
+    eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+    eng.set_clusters(consts)
+    eng.set_log_omega(logOm)
+    tN = tilde_n(eng, opt["Nv"], base.N)
+    vec = eng.fused(tN).cpu().numpy()
+    bnp = base.numpy()
+    pairs = vo.c_estep_pairs(bnp, consts, opt["tau"], nthreads=nthreads)
+    tNn = tN.cpu().numpy()
+    hz, Z = vo.c_responsibilities(pairs["LL_elbo"], tNn, logOm)
+    st = vo.c_statistics(Z, pairs, cov)
+    got = vb.host.unpack_stats(vec, P.K, P.S, base.d, cov)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, (name, k, stat_err(got[k], st[k]))
+    assert hatz_err(eng.hatZ.cpu().numpy(), hz) < RTOL_NORTH_STAR
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+    assert eng.fallback_count() == 0
+    return hz
+
+
+@pytest.mark.gpu
+def test_c3_full_size_vs_oracle(vb, vo):
+    """C3 at N = 10,000 (80,000 pairs), every pair checked."""
+    hz = _fused_vs_oracle(vb, vo, "C3")
+    assert hz.shape == (10_000, 8)
+
+
+@pytest.mark.gpu
+def test_c5_slice_vs_oracle(vb, vo):
+    """C5 shapes (K = 32, S = Sb = 12, d = 16 full) on 1,000 bases = 32,000 pairs."""
+    hz = _fused_vs_oracle(vb, vo, "C5", N=1000, nthreads=16)
+    assert hz.shape == (1000, 32)

@@ -1,0 +1,152 @@
+"""Robustness of the C-ABI library beyond plain parity:
+
+* graph capture (GPU): a fused E-step captured into a HIP graph and replayed
+  reproduces the eager result bit for bit, also after the cluster constants
+  change between replays and when the exact fallback runs inside the graph
+  (its counters reset themselves on the device); timing enabled during the
+  capture records nothing into the graph;
+* a diverged trial (NaN cluster constants) inside a batched-trials launch
+  leaves the other trials untouched, is not sent to the exact fallback, and
+  yields NaN log-likelihoods (the EM loop then ends that trial as unstable,
+  vbhem_h3m_c_step_fc.m:338-374);
+* the fused schedule is per host thread (CPU, no device call).
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from cases import make_case
+from conftest import rel_err
+
+DEV = "cuda:0"
+
+
+def _engine(vb, cs, trials=1, consts=None):
+    from vbhem_amd.estep import EStepEngine
+    c = cs["consts"] if consts is None else consts
+    K, S = c["logPi"].shape
+    eng = EStepEngine(vb.BaseSet.from_numpy(cs["base"]), K, S, cs["T"], device=DEV, trials=trials)
+    eng.set_clusters(c)
+    return eng
+
+
+def _tn(cs, Nv=100.0):
+    N = cs["base"]["prior"].shape[0]
+    return torch.as_tensor(Nv * N * cs["base"]["omega"], device=DEV)
+
+
+def _capture(eng, tN, time_it):
+    from vbhem_amd import _capi
+    s = torch.cuda.Stream(device=DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        eng.fused(tN)  # warm-up on the side stream: workspace allocated outside the capture
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    _capi.timing_enable(time_it)
+    try:
+        with torch.cuda.graph(g):
+            eng.fused(tN)
+    finally:
+        _capi.timing_enable(False)
+    t = _capi.timing_read()  # drains (destroys) whatever was recorded
+    assert t["fb_launches"] == 0 and t["stats_launches"] == 0 and t["em_launches"] == 0
+    return g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("time_it", [False, True], ids=["plain", "timing-on"])
+def test_fused_graph_replay(vb, time_it):
+    cs = make_case(600, 16, 8, 8, 8, 1, seed=31, tau=10)
+    eng = _engine(vb, cs)
+    from vbhem_amd import host
+    logOm = host.log_omega_tilde(cs["P"].alpha)
+    eng.set_log_omega(logOm)
+    tN = _tn(cs)
+    ref = eng.fused(tN).clone()
+    ref_hz, ref_ll = eng.hatZ.clone(), eng.LL.clone()
+    g = _capture(eng, tN, time_it)
+    for _ in range(2):
+        eng.stats.zero_()
+        eng.hatZ.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(eng.stats, ref) and torch.equal(eng.hatZ, ref_hz)
+        assert torch.equal(eng.LL, ref_ll)
+    # new cluster constants in the same buffers: the replay picks them up
+    P2 = cs["P"].copy()
+    P2.m = P2.m + 0.25
+    c2 = host.cluster_constants(P2, 1)
+    eng.set_clusters(c2)
+    g.replay()
+    torch.cuda.synchronize()
+    got = eng.stats.clone()
+    eager = eng.fused(tN).clone()
+    assert torch.equal(got, eager)
+    assert not torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_graph_replay_with_exact_fallback(vb, vo):
+    from test_gpu_parity import adversarial_case
+    cs, consts = adversarial_case(1)
+    eng = _engine(vb, cs, consts=consts)
+    from vbhem_amd import host
+    eng.set_log_omega(host.log_omega_tilde(cs["P"].alpha))
+    tN = _tn(cs)
+    ref = eng.fused(tN).clone()
+    assert eng.fallback_count() > 0
+    g = _capture(eng, tN, False)
+    for _ in range(3):
+        eng.stats.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(eng.stats, ref)
+        assert eng.fallback_count() > 0
+
+
+@pytest.mark.gpu
+def test_nan_trial_is_isolated(vb):
+    """Trial 1 of 2 carries NaN cluster constants: trial 0's outputs equal its own
+    single-trial launch, nothing takes the exact fallback, trial 1's L_elbo is NaN."""
+    from vbhem_amd import host
+    cs = make_case(300, 4, 5, 5, 3, 1, seed=41, tau=8)
+    c0 = cs["consts"]
+    c1 = {k: np.full_like(np.asarray(v), np.nan) for k, v in c0.items()}
+    both = {k: np.concatenate([np.asarray(c0[k]), c1[k]]) for k in c0}
+    K = c0["logPi"].shape[0]
+    logOm = host.log_omega_tilde(cs["P"].alpha)
+    tN = _tn(cs)
+    e1 = _engine(vb, cs)
+    e1.set_log_omega(logOm)
+    ref = e1.fused(tN).cpu().numpy()
+    ref_ll = e1.LL.cpu().numpy()
+    e2 = _engine(vb, cs, trials=2, consts=both)
+    e2.set_log_omega(np.concatenate([logOm, np.full(K, np.nan)]))
+    vec = e2.fused(tN).cpu().numpy()
+    assert e2.fallback_count() == 0
+    SL = vec.size // 2
+    assert rel_err(vec[:SL], ref) < 1e-12
+    ll = e2.LL.cpu().numpy()
+    assert rel_err(ll[:, :K], ref_ll) < 1e-13
+    assert np.isnan(ll[:, K:]).all()
+
+
+def test_fused_mode_is_per_thread(capi_lib):
+    from vbhem_amd import _capi
+    prev_main = _capi.set_fused_mode(_capi.FUSED_GATED)
+    seen = {}
+
+    def worker():
+        seen["prev"] = _capi.set_fused_mode(_capi.FUSED_DENSE)   # this thread's default
+        seen["now"] = _capi.set_fused_mode(_capi.FUSED_DENSE)
+
+    th = threading.Thread(target=worker)
+    th.start()
+    th.join()
+    assert seen == {"prev": _capi.FUSED_GATED, "now": _capi.FUSED_DENSE}
+    # the main thread's schedule is untouched by the worker
+    assert _capi.set_fused_mode(prev_main) == _capi.FUSED_GATED
