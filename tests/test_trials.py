@@ -91,7 +91,10 @@ def test_fused_trials_match_separate(vb, shape):
         for k in ("Lt1", "Lt7"):
             assert abs(a[k] - b[k]) <= 1e-12 * abs(b[k]) + 1e-12, (name, r, k)
         cols = slice(r * K, (r + 1) * K)
-        assert hatz_err(eng.hatZ[:, cols].cpu().numpy(), one.hatZ.cpu().numpy()) < 1e-12
+        # elementwise: log_Z = tilde_N (logOmega + L_elbo) ~ 1e4..1e5 carries ~1e-11
+        # absolute rounding from the last-bit L_elbo differences noted below
+        assert rel_err(eng.hatZ[:, cols].cpu().numpy(), one.hatZ.cpu().numpy()) < 1e-12
+        assert hatz_err(eng.hatZ[:, cols].cpu().numpy(), one.hatZ.cpu().numpy()) < 1e-9
         # the emission GEMM shifts every mean by the average of ALL cluster means
         # (R*K of them here): shift-invariant algebra, last-bit differences in E
         assert rel_err(eng.LL[:, cols].cpu().numpy(), one.LL.cpu().numpy()) < 1e-13
