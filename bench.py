@@ -100,6 +100,20 @@ def committed_traffic(config, N, world, want):
     return None, None
 
 
+def host_cpu():
+    """(nproc, CPU model) of the host this process runs on (the GPU box's cores)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count() or 1, model
+
+
 def cpu_baseline(vo, base_np, consts, T, N_total, K, target_s):
     """Time the oracle's C port of mex.c (1 thread) + responsibilities + stats
     on a bounded sample of bases and scale linearly to N_total."""
@@ -131,12 +145,16 @@ def cpu_baseline(vo, base_np, consts, T, N_total, K, target_s):
     hzm, Zm = vo.c_responsibilities(prm["LL_elbo"], tnm, np.log(np.full(K, 1.0 / K)))
     vo.c_statistics(Zm, prm, b["covmode"])
     tm = time.perf_counter() - tm0
+    nproc, model = host_cpu()
     multi = dict(value=1.0 / (tm * N_total / n), unit="E-steps/s", cores=threads, kind="port",
-                 sample=f"the same {n}-base sample, pairs over {threads} OpenMP threads ({tm:.2f} s)")
+                 sample=f"the same {n}-base sample, pairs over {threads} OpenMP threads ({tm:.2f} s)",
+                 host_nproc=nproc, host_cpu=model)
     return dict(value=1.0 / (t * N_total / n), unit="E-steps/s", cores=1, kind="port",
                 sample=(f"oracle/vbhem_oracle.c (C port of the reference mex.c E-step, 1 thread) + "
                         f"responsibilities + statistics on {n} of {N_total} base HMMs x {K} clusters "
-                        f"({t:.1f} s), scaled linearly to N={N_total}"),
+                        f"({t:.1f} s), scaled linearly to N={N_total}; host: {nproc} logical CPUs, "
+                        f"{model}"),
+                host_nproc=nproc, host_cpu=model,
                 seconds=t, n_sample=n, multi=multi), pr, n
 
 
@@ -294,7 +312,7 @@ def main():
                    "parallelism": f"bases sharded over {world} GPU(s), 1 RCCL all-reduce/E-step"},
         "pairs_per_s": N * K * args.steps / dt,
         "roofline": {
-            "bound": "mfma",
+            "bound": "valu",
             "achieved": achieved,
             "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s",
@@ -305,7 +323,8 @@ def main():
             "kernel_ms": fb_launch_ms,
             "flops_per_pair": fpp,
             "pairs_per_launch": pairs_per_launch,
-            "note": ("fp64 compute-bound (VALU + software exp/log); peak = MI355X FP64 dense "
+            "note": ("fp64 VALU-bound (software exp/log + contractions on the vector ALU); "
+                     "peak = MI355X FP64 dense "
                      "78.6 TF/s (vector = matrix rate); flops counted on the reference "
                      "recurrences this kernel runs (" + ("K2 backward + K3 termination, every "
                      "pair" if gated else "K2-K4") + "), excluding exp/log"),
@@ -316,6 +335,12 @@ def main():
             "exp_log_per_pair_reference": [n_exp, n_log],
         },
         "schedule": "gated" if gated else "dense",
+        "metric_definition": ("one E-step = every (base, cluster) pair's backward recursion and "
+                              "L_elbo, hat_Z, the gated statistics (vbhem_compute_Statistics.m:35 "
+                              "keeps pairs with Z > 1e-8; the forward sweep runs for those pairs "
+                              "only, the reference computes it for all and discards the rest), the "
+                              "ELBO partials, the all-reduce and the copy to the host; outputs "
+                              "equal the dense schedule's (dense_schedule.max_rel_diff_vs_gated)"),
         "gated_pairs_frac": n_gated / float(N * K),
         "gated_forward": ({"kernel": f"vbhem::fb_split_kernel<{S}, {lpc}, 2>", "kernel_ms": gf_ms,
                            "pairs_per_launch": n_gated / world,
@@ -335,7 +360,8 @@ def main():
         import vbhem_oracle as vo  # cpu_baseline leg only
         base_np = eng.base.numpy() if hasattr(eng.base, "numpy") else base.numpy()
         cb, pr, n = cpu_baseline(vo, base_np, consts, T, N, K, args.cpu_seconds)
-        res["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        res["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
+                                                  "host_nproc", "host_cpu")}
         res["cpu_baseline_multithread"] = cb["multi"]
         g = eng.LL[:n].cpu().numpy()
         r = pr["LL_elbo"]

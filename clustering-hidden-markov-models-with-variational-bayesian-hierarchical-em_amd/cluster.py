@@ -1,0 +1,139 @@
+"""The clustering API around the device E-step (callers of the hot path).
+
+* :func:`vbhem_h3m_cluster` -- src/vbhem/vbhem_h3m_cluster.m:103-402: input
+  HMMs -> remove empty states (:116-134, vbhmm_remove_empty with thresh 1e-3)
+  -> ``hmms_to_h3m_hem`` (:237) -> for a vector of K, one run per K and the best
+  of LL + gammaln(K+1) (:261-309); for a vector of S, likewise with
+  gammaln(S+1) (:313-354); a single (K, S) runs :func:`vbhem_h3m_c`.
+* :func:`vbhem_h3m_c` -- vbhem_h3m_c.m:28-76, 167-170: ``trials`` EM runs
+  (the reference's ``parfor``) as ONE batched launch per iteration
+  (em.vbhem_h3m_c_trials), the best bound wins; with ``learn_hyps`` the
+  unique trials (uniqueLL, :79-89) are re-optimised by the L-BFGS
+  hyperparameter learner (hyp.vbhem_h3m_c_hyp, :94-137).
+* :func:`unique_ll` -- src/util/uniqueLL.m; :func:`form_groups` --
+  form_outputH3M.m:50-60 (label, groups, group_size).
+
+Initialisation: the reference's default init modes are 'baseem', 'gmmNew'
+and 'wtkmeans' (auto mode); 'gmmNew'/'wtkmeans' need the Statistics Toolbox
+(out of scope).  Every trial here is the 'baseem' restatement
+(vbhemhmm_init.m:58-100) with its draws from a numpy generator seeded by
+seed + trial (vbhem_h3m_c.m:32-38 seeds MATLAB's twister the same way).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+from scipy.special import gammaln
+
+from . import em
+from .estep import EStepEngine
+from .h3m import COV_FULL, BaseSet, baseem_draws, baseem_init, default_options, hmms_to_h3m_hem
+
+
+def unique_ll(LLall: Sequence[float], diffthresh: float) -> List[int]:
+    """uniqueLL.m:43-84: indices of the trials whose bound differs from every
+    bound kept so far by more than diffthresh (relative)."""
+    kept_ll: List[float] = []
+    kept: List[int] = []
+    for it, my_LL in enumerate(LLall):
+        if it == 0:
+            new = True
+        else:
+            pLL = np.abs((np.asarray(kept_ll) - my_LL) / my_LL)
+            new = bool(np.all(pLL > diffthresh))   # MATLAB `if` on a vector: all nonzero
+        if new:
+            kept_ll.append(float(my_LL))
+            kept.append(it)
+    return kept
+
+
+def form_groups(label: np.ndarray, K: int):
+    """form_outputH3M.m:50-60: 0-based label -> groups (indices per cluster) and
+    group_size."""
+    label = np.asarray(label).reshape(-1)
+    groups = [np.flatnonzero(label == j) for j in range(K)]
+    return groups, np.array([g.size for g in groups])
+
+
+def _device_engine(device):
+    dev = torch.device(device)
+    return lambda base, K, S, T, trials=1: EStepEngine(base, K, S, T, device=dev, trials=trials)
+
+
+def vbhem_h3m_c(base: BaseSet, opt: dict, device="cuda", engine_factory=None,
+                hyp_learn: Optional[bool] = None) -> dict:
+    """vbhem_h3m_c.m for one (K, S): batched trials, best bound (and optional
+    hyperparameter learning of the unique trials).  Trials run in launches of at
+    most 256 clusters (vbhem_estep_fused_trials' limit).  ``engine_factory(base,
+    K_total, S, T, trials)`` builds the E-step engine (default: the device one)."""
+    K, S, R = int(opt["K"]), int(opt["S"]), int(opt.get("trials", 100))
+    make = engine_factory or _device_engine(device)
+    posts = []
+    for it in range(1, R + 1):
+        rb, rg, om = baseem_draws(base, K, S, seed=int(opt["seed"]) + it)
+        posts.append(baseem_init(base, opt, rb, rg, om))
+    per = max(1, 256 // K)
+    results, LLs = [], []
+    for r0 in range(0, R, per):
+        chunk = posts[r0:r0 + per]
+        eng = make(base, len(chunk) * K, S, opt["tau"], trials=len(chunk))
+        tr = em.vbhem_h3m_c_trials(chunk, eng, opt)
+        results.extend(tr.results)
+        LLs.extend(tr.LLall.tolist())
+        del eng
+    LLall = np.array(LLs)
+    learn = opt.get("learn_hyps", 0) if hyp_learn is None else hyp_learn
+    hyp_info = None
+    if learn:
+        from . import hyp
+        uniq = unique_ll(LLall, 2 * opt["minDiff"] * 10)
+        one = make(base, K, S, opt["tau"], trials=1)
+        hyp_info = {}
+        for q in uniq:
+            h = hyp.vbhem_h3m_c_hyp(base, opt, results[q].post, one)
+            results[q] = h["result"]
+            LLall[q] = h["result"].LL
+            hyp_info[q] = h
+    best = int(np.argmax(LLall))
+    res = results[best]
+    out = dict(result=res, LL=float(LLall[best]), LLall=LLall, best=best, K=K, S=S,
+               hyp=hyp_info[best] if hyp_info and best in hyp_info else None)
+    if res.label is not None:
+        lab = res.label.cpu().numpy()
+        out["label"] = lab
+        out["groups"], out["group_size"] = form_groups(lab, K)
+    return out
+
+
+def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda",
+                      base: Optional[BaseSet] = None, engine_factory=None) -> dict:
+    """vbhem_h3m_cluster.m:103-402 (initmode 'baseem', full covariance,
+    use_post = 1).  ``hmms``: list of VB-HMM dicts (vbhmm_em output) or None;
+    ``base``: an already converted h3m_b (skips the conversion)."""
+    Ks = [int(k) for k in np.atleast_1d(K)]
+    Ss = [int(s) for s in np.atleast_1d(S)]
+    if base is None:
+        from .vbhmm_em import vbhmm_remove_empty
+        if opt is None or opt.get("remove_empty", 1):
+            hmms = [vbhmm_remove_empty(h, 1e-3) if h is not None else None for h in hmms]
+        base = hmms_to_h3m_hem(hmms, COV_FULL, use_post=True)
+    if len(Ks) > 1:
+        outs = [vbhem_h3m_cluster(None, k, Ss, dict(opt), device, base, engine_factory) for k in Ks]
+        LLk = np.array([o["LL"] for o in outs]) + gammaln(np.array(Ks) + 1.0)
+        ind = int(np.argmax(LLk))
+        h = dict(outs[ind])
+        h.update(model_LL=LLk, model_k=Ks, model_bestK=Ks[ind], model_all=outs)
+        return h
+    if len(Ss) > 1:
+        outs = [vbhem_h3m_cluster(None, Ks[0], s, dict(opt), device, base, engine_factory)
+                for s in Ss]
+        LLs = np.array([o["LL"] for o in outs]) + gammaln(np.array(Ss) + 1.0)
+        ind = int(np.argmax(LLs))
+        h = dict(outs[ind])
+        h.update(model_LL_S=LLs, model_S=Ss, model_bestS=Ss[ind], model_all_s=outs)
+        return h
+    o = default_options(Ks[0], Ss[0], base.d, **{k: v for k, v in (opt or {}).items()
+                                                  if k not in ("K", "S")})
+    return vbhem_h3m_c(base, o, device, engine_factory)

@@ -35,6 +35,7 @@ class EMResult:
     syn: Optional[dict]             # Syn_STATS of the last M-step (Nj_rho1, Nj_rho2rho, Nj_rho, ...)
     point: Optional[dict] = None    # convert_h3mrtoh3mb point estimates
     label: Optional[torch.Tensor] = None  # argmax_j hat_Z (0-based), form_outputH3M.m:274-275
+    dLL: Optional[dict] = None      # opt['calc_LLderiv']: bound derivatives at the last E-step
 
 
 def tilde_n(engine: EStepEngine, Nv: float, total_N: int) -> torch.Tensor:
@@ -61,6 +62,8 @@ def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
     stable = True
     L = -np.inf
     Nj = np.zeros(K)
+    dLL = None
+    do_deriv = bool(opt.get("calc_LLderiv", 0))
     while True:
         consts = host.cluster_constants(post, covmode)
         logOmega = host.log_omega_tilde(post.alpha)
@@ -81,7 +84,16 @@ def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
             # step_fc.m:338-374: unstable model -> L = -inf, stop before the M-step
             L = -np.inf
             stable = False
+            if do_deriv:  # the gradient is invalidated (:362-368)
+                dLL = {k: np.full_like(np.atleast_1d(v), np.nan)
+                       for k, v in host.lower_bound_derivs(logOmega, post, consts, opt, covmode,
+                                                           opt.get("hyp_clipped")).items()
+                       if k != "raw"}
             break
+        if do_break and do_deriv:
+            # step_fc.m:356-360: derivatives before the last M-step (vbhemh3m_lb.m:202-356)
+            dLL = host.lower_bound_derivs(logOmega, post, consts, opt, covmode,
+                                          opt.get("hyp_clipped"))
         syn = host.finish_statistics(st, covmode)
         post = host.mstep(syn, Nj, opt, covmode, post.W0mode)
         it += 1
@@ -90,7 +102,7 @@ def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
         if do_break:
             break
     res = EMResult(post=post, LogLs=LogLs, LL=L, iters=it, stable=stable, hatZ=engine.hatZ.clone(),
-                   L_elbo=engine.LL.clone(), Nj=Nj, syn=syn)
+                   L_elbo=engine.LL.clone(), Nj=Nj, syn=syn, dLL=dLL)
     if stable:
         res.point = host.convert_to_point(post, covmode)
         res.label = torch.argmax(res.hatZ, dim=1)

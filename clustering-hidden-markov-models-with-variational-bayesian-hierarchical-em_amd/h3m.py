@@ -167,15 +167,23 @@ def default_options(K: int, S: int, d: int, **over) -> dict:
     return opt
 
 
-def clip_hyps(opt: dict) -> dict:
-    """vbhem_clip_hyps.m:20-85."""
+def clip_hyps(opt: dict, with_flags: bool = False):
+    """vbhem_clip_hyps.m:20-85: clip each hyperparameter into [hyps_min, hyps_max].
+    with_flags: also return the clipped flags (+1 at the max, -1 at the min), which
+    vbhemh3m_lb.m:326-343 uses to zero derivatives pointing out of range."""
     out = dict(opt)
+    flags = {}
     for name in ("alpha0", "eta0", "epsilon0", "v0", "lambda0", "W0"):
         val = np.array(opt[name], dtype=float, ndmin=1)
-        val = np.where(val >= opt["hyps_max"][name], opt["hyps_max"][name], val)
-        val = np.where(val <= opt["hyps_min"][name], opt["hyps_min"][name], val)
+        fl = np.zeros(val.size)
+        hi, lo = opt["hyps_max"][name], opt["hyps_min"][name]
+        fl[val >= hi] = 1.0
+        val = np.where(val >= hi, hi, val)
+        fl[val <= lo] = -1.0
+        val = np.where(val <= lo, lo, val)
         out[name] = val if np.ndim(opt[name]) else float(val[0])
-    return out
+        flags[name] = fl
+    return (out, flags) if with_flags else out
 
 
 def baseem_init(base: BaseSet, opt: dict, randomb: np.ndarray, randomg: np.ndarray,

@@ -191,6 +191,64 @@ def lower_bound(Lt1: float, Lt7: float, Nj: np.ndarray, logOmega: np.ndarray, po
     return float(Lt1 + Lt2 + Lt3 + Lt4 + Lt5 + Lt6 - Lt7 - Lt8 - Lt9 - Lt10)
 
 
+def lower_bound_derivs(logOmega: np.ndarray, post: Posterior, consts: dict, opt: dict,
+                       covmode: int, clipped: dict = None) -> dict:
+    """vbhemh3m_lb.m:202-345: derivatives of the lower bound with respect to the
+    hyperparameters (posterior held fixed), zeroed where a clipped hyperparameter
+    would move further out of range (:326-343), then taken with respect to the
+    transformed hyperparameters the optimiser works in (:345-356).
+
+    W0 diag ('diag' W0mode): the reference's branch refers to undefined K*S and
+    covmode and would error; here it uses Kr*Sr and the
+    run's covariance mode, the evident intent."""
+    K, S = post.K, opt["S"]
+    d = len(opt["m0"])
+    a0, e0, ep0, l0, v0 = opt["alpha0"], opt["eta0"], opt["epsilon0"], opt["lambda0"], opt["v0"]
+    m0 = np.asarray(opt["m0"], dtype=float)
+    W0 = np.asarray(opt["W0"], dtype=float)
+    W0inv = np.linalg.inv(_W0(opt, d))
+    iid = W0.size == 1
+    logdetW0inv = d * np.log(W0inv[0, 0]) if iid else np.log(np.diag(W0inv)).sum()
+    q = np.arange(1, d + 1)
+    lLT = consts["logLambdaTilde"]
+    v, lam = post.v, post.lam
+    Wf = post.W if covmode == COV_FULL else post.W[..., :, None] * np.eye(d)
+    diff = post.m - m0
+    mWm = np.einsum("ksa,ksab,ksb->ks", diff, Wf, diff)
+    dLt = {}
+    dLt["alpha0"] = np.atleast_1d(K * digamma(K * a0) - K * digamma(a0) + logOmega.sum())
+    dLt["eta0"] = np.atleast_1d(K * (S * digamma(S * e0) - S * digamma(e0)) + consts["logPi"].sum())
+    dLt["epsilon0"] = np.atleast_1d(K * S * (S * digamma(S * ep0) - S * digamma(ep0))
+                                    + consts["logA"].sum())
+    d_logB0_v0 = 0.5 * logdetW0inv - (d / 2) * np.log(2) - 0.5 * digamma(0.5 * (v0 + 1 - q)).sum()
+    dLt["v0"] = np.atleast_1d(K * S * d_logB0_v0 + 0.5 * lLT.sum())
+    dLt["lambda0"] = np.atleast_1d((0.5 * (d / l0 - d / lam - v * mWm)).sum())
+    if iid:
+        myW0inv = W0inv[0, 0]
+        myW0 = 1.0 / myW0inv
+        trW = np.trace(Wf, axis1=-2, axis2=-1)
+        d_tr = -v * myW0inv ** 2 * trW
+        dLt["W0"] = np.atleast_1d(K * S * (-0.5 * v0 * d * myW0inv) - 0.5 * d_tr.sum())
+    else:
+        myW0inv = np.diag(W0inv)
+        myW0 = 1.0 / myW0inv
+        dgW = np.diagonal(Wf, axis1=-2, axis2=-1)                        # [K][S][d]
+        d_tr = -v[..., None] * myW0inv ** 2 * dgW
+        dLt["W0"] = K * S * (-0.5 * v0 * myW0inv) - 0.5 * d_tr.sum(axis=(0, 1))
+    dLt["m0"] = (l0 * v[..., None] * np.einsum("ksab,ksb->ksa", Wf, post.m - m0)).sum(axis=(0, 1))
+    if clipped is not None:
+        for name, fl in clipped.items():
+            g = dLt[name]
+            g[(fl == 1) & (g > 0)] = 0.0
+            g[(fl == -1) & (g < 0)] = 0.0
+    return dict(d_logalpha0=dLt["alpha0"] * a0, d_logeta0=dLt["eta0"] * e0,
+                d_logepsilon0=dLt["epsilon0"] * ep0, d_logv0D1=dLt["v0"] * (v0 - d + 1),
+                d_sqrtv0D1=dLt["v0"] * 2 * np.sqrt(v0 - d + 1),
+                d_loglambda0=dLt["lambda0"] * l0, d_sqrtlambda0=dLt["lambda0"] * 2 * np.sqrt(l0),
+                d_sqrtW0inv=dLt["W0"] * (myW0 ** 1.5) * (-2.0), d_logW0=dLt["W0"] * myW0,
+                d_m0=dLt["m0"], raw=dLt)
+
+
 def convert_to_point(post: Posterior, covmode: int) -> dict:
     """convert_h3mrtoh3mb.m:9-79: prior, A, centres, covars, omega point estimates."""
     K, S, d = post.m.shape

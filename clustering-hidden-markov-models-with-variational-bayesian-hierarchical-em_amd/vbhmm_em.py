@@ -1,0 +1,365 @@
+"""VB-HMM learning of the base HMMs (config C1).
+
+The upstream stage that produces the HMMs VBHEM clusters:
+``vbhmm_learn_batch`` -> ``vbhmm_learn`` -> ``vbhmm_em`` -> ``vbhmm_fb`` ->
+``vbhmm_fb_mex`` (src/hmm/).  The forward-backward runs on the GPU through the
+C-ABI (:func:`vbhmm.vbhmm_fb`, one lane per sequence); the per-iteration
+statistics, lower bound and M-step are O(K^2 + K dim^2 + total fixations) host
+work, restated here from:
+
+* vbhmm_em.m:112-414  the EM loop (E-step :133-246, bound :251-275, convergence
+  and NaN handling :277-349, M-step :352-408) and the output model :426-491;
+* vbhmm_em_lb.m:74-257  the lower bound (no hyperparameter derivatives);
+* vbhmm_init.m:122-204  the initial posterior from a GMM; :27-43 the K = 1 and
+  N <= K special cases of the 'random' mode;
+* vbhmm_clip_hyps.m:20-85, vbhmm_learn.m:252-310 (defaults), :440-480 (random
+  trials, best LL), :367-405 (model selection over K with +gammaln(K+1));
+* vbhmm_learn_batch.m (one vbhmm_learn per subject);
+* vbhmm_remove_empty.m (states with N < thresh removed, as vbhem_h3m_cluster.m:116-134).
+
+The 'random' initialisation fits a GMM with MATLAB's ``gmdistribution.fit``
+(Statistics Toolbox, 'Start' 'randSample', TolFun 1e-5; vbhmm_init.m:59-60),
+which is not part of the reference.  :func:`gmm_fit_randsample` restates that
+published algorithm (random data rows as means, uniform weights, diagonal
+covariances of the data variances, EM until the relative log-likelihood change
+is below 1e-5); MATLAB's random stream cannot be reproduced, so the draws come
+from a seeded numpy generator and parity tests inject the same GMM into both
+sides.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+from scipy.special import digamma, gammaln
+
+from . import vbhmm
+
+
+# ----------------------------------------------------------------------------
+# options
+# ----------------------------------------------------------------------------
+def vbhmm_default_options(dim: int, **over) -> dict:
+    """vbhmm_learn.m:252-310 (the fields the EM loop reads)."""
+    defmu = {2: [256.0, 192.0], 3: [256.0, 192.0, 150.0]}.get(dim, [0.0] * dim)
+    opt = dict(alpha0=0.1, mu0=defmu, W0=0.005, beta0=1.0, v0=5.0, epsilon0=0.1,
+               initmode="random", numtrials=50, maxIter=100, minDiff=1e-5, seed=None,
+               fix_clusters=0, fix_cov=None, verbose=0)
+    opt["hyps_max"] = dict(alpha0=1.0686e13, epsilon0=1.0686e13, v0=1e4, beta0=1.0686e13,
+                           W0=1.0686e13)
+    opt["hyps_min"] = dict(alpha0=1.0686e-13, epsilon0=1.0686e-13, v0=2.0612e-09 + dim - 1,
+                           beta0=1.0686e-13, W0=1.0686e-13)
+    opt.update(over)
+    opt["mu0"] = np.asarray(opt["mu0"], dtype=np.float64).reshape(-1)
+    if opt["v0"] <= dim - 1:
+        raise ValueError("v0 not large enough...should be > D-1")  # vbhmm_learn.m:319-321
+    return opt
+
+
+def vbhmm_clip_hyps(opt: dict):
+    """vbhmm_clip_hyps.m:20-85: clip each hyperparameter into [min, max];
+    returns (clipped options, clipped flags: +1 at max, -1 at min)."""
+    out = dict(opt)
+    clipped = {}
+    for name in ("alpha0", "epsilon0", "v0", "beta0", "W0"):
+        val = np.array(opt[name], dtype=np.float64, ndmin=1)
+        flag = np.zeros(val.size)
+        hi, lo = opt["hyps_max"][name], opt["hyps_min"][name]
+        flag[val >= hi] = +1
+        val = np.where(val >= hi, hi, val)
+        flag[val <= lo] = -1
+        val = np.where(val <= lo, lo, val)
+        out[name] = val if np.ndim(opt[name]) else float(val[0])
+        clipped[name] = flag
+    return out, clipped
+
+
+# ----------------------------------------------------------------------------
+# initialisation
+# ----------------------------------------------------------------------------
+def gmm_fit_randsample(X: np.ndarray, K: int, rng: np.random.Generator, tolfun: float = 1e-5,
+                       max_iter: int = 100, reg: float = 0.0) -> dict:
+    """Stand-in for MATLAB gmdistribution.fit(X, K, 'Start', 'randSample',
+    'Options', struct('TolFun', 1e-5)) (vbhmm_init.m:59-60): K random rows of X
+    as means, uniform proportions, every covariance diag(var(X)); full-covariance
+    EM until |dLL| <= TolFun * |LL|.  Returns dict(prior [K], mean [K][dim],
+    cov [K][dim][dim])."""
+    N, dim = X.shape
+    mu = X[rng.choice(N, K, replace=False)].copy()
+    var = X.var(axis=0, ddof=1) if N > 1 else np.ones(dim)
+    cov = np.repeat(np.diag(var)[None], K, axis=0)
+    pi = np.full(K, 1.0 / K)
+    last = -np.inf
+    for _ in range(max_iter):
+        logp = np.zeros((N, K))
+        for k in range(K):
+            L = np.linalg.cholesky(cov[k] + reg * np.eye(dim))
+            z = np.linalg.solve(L, (X - mu[k]).T)
+            logp[:, k] = (np.log(pi[k]) - 0.5 * (z * z).sum(0) - np.log(np.diag(L)).sum()
+                          - 0.5 * dim * np.log(2 * np.pi))
+        mx = logp.max(1, keepdims=True)
+        lse = mx[:, 0] + np.log(np.exp(logp - mx).sum(1))
+        ll = lse.sum()
+        post = np.exp(logp - lse[:, None])
+        nk = post.sum(0) + 1e-300
+        pi = nk / N
+        mu = (post.T @ X) / nk[:, None]
+        for k in range(K):
+            d = X - mu[k]
+            cov[k] = (d * post[:, k:k + 1]).T @ d / nk[k] + reg * np.eye(dim)
+            cov[k] = 0.5 * (cov[k] + cov[k].T)
+        if abs(ll - last) <= tolfun * abs(ll):
+            break
+        last = ll
+    return dict(prior=pi, mean=mu, cov=cov)
+
+
+def random_gmm(data: Sequence[np.ndarray], K: int, rng: np.random.Generator) -> dict:
+    """The 'random' initmode's GMM (vbhmm_init.m:27-91): one Gaussian for K = 1,
+    the data points themselves when N <= K, else a GMM fit."""
+    X = np.concatenate([np.asarray(a, dtype=np.float64) for a in data], axis=0)
+    N, dim = X.shape
+    if K == 1:
+        return dict(prior=np.ones(1), mean=X.mean(0, keepdims=True),
+                    cov=np.cov(X.T, ddof=1).reshape(1, dim, dim))
+    if N <= K:
+        tmp = np.concatenate([np.ones(N), 1e-6 * np.ones(K - N)])
+        mean = np.concatenate([X, np.zeros((K - N, dim))])
+        v = X.var(axis=0, ddof=1) if N > 1 else np.ones(dim)
+        return dict(prior=tmp / tmp.sum(), mean=mean,
+                    cov=np.repeat((np.mean(v) * np.eye(dim))[None], K, axis=0))
+    try:
+        return gmm_fit_randsample(X, K, rng)
+    except np.linalg.LinAlgError:  # ill-conditioned: regularised fit (vbhmm_init.m:63-70)
+        return gmm_fit_randsample(X, K, rng, reg=1e-10)
+
+
+def vbhmm_init(data: Sequence[np.ndarray], K: int, opt: dict, gmm: dict) -> dict:
+    """vbhmm_init.m:122-204: the initial variational posterior from a GMM
+    (prior [K], mean [K][dim], cov [K][dim][dim])."""
+    X = np.concatenate([np.asarray(a, dtype=np.float64) for a in data], axis=0)
+    N, dim = X.shape
+    if len(opt["mu0"]) != dim:
+        raise ValueError(f"vbopt.mu0 should have dimension D={dim}")
+    W0 = np.asarray(opt["W0"], dtype=np.float64)
+    W0m = float(W0) * np.eye(dim) if W0.size == 1 else np.diag(W0.reshape(-1))
+    W0inv = np.linalg.inv(W0m)
+    beta0, v0, m0 = float(opt["beta0"]), float(opt["v0"]), opt["mu0"]
+    Nk = N * np.asarray(gmm["prior"], dtype=np.float64).reshape(-1)
+    Nk2 = np.full(K, N / K)
+    xbar = np.asarray(gmm["mean"], dtype=np.float64).reshape(K, dim)
+    S = np.asarray(gmm["cov"], dtype=np.float64).reshape(K, dim, dim)
+    alpha = opt["alpha0"] + Nk2
+    epsilon = np.repeat((opt["epsilon0"] + Nk2)[None, :], K, axis=0)
+    beta = beta0 + Nk
+    v = v0 + Nk + 1
+    m = (beta0 * m0[None, :] + Nk[:, None] * xbar) / beta[:, None]
+    W = np.zeros((K, dim, dim))
+    for k in range(K):
+        mult1 = beta0 * Nk[k] / (beta0 + Nk[k])
+        diff3 = xbar[k] - m0
+        W[k] = np.linalg.inv(W0inv + Nk[k] * S[k] + mult1 * np.outer(diff3, diff3))
+    return dict(alpha=alpha, epsilon=epsilon, beta=beta, v=v, m=m, W=W, W0inv=W0inv,
+                W0mode="iid" if W0.size == 1 else "diag")
+
+
+# ----------------------------------------------------------------------------
+# lower bound (vbhmm_em_lb.m, no derivatives)
+# ----------------------------------------------------------------------------
+def vbhmm_em_lb(st: dict, opt: dict, vp: dict, fb: dict) -> float:
+    """vbhmm_em_lb.m:74-257 (usegroups = 0)."""
+    dim, K = st["dim"], st["K"]
+    alpha0, epsilon0, beta0, v0 = opt["alpha0"], opt["epsilon0"], opt["beta0"], opt["v0"]
+    m0, W0inv = opt["mu0"], st["W0inv"]
+    v, W, eps, alpha, m, beta = vp["v"], vp["W"], vp["epsilon"], vp["alpha"], vp["m"], vp["beta"]
+    lLT, lPi, lA = fb["logLambdaTilde"], fb["logPiTilde"], fb["logATilde"]
+    logdetW0inv = (dim * np.log(W0inv[0, 0]) if st["W0mode"] == "iid"
+                   else np.log(np.diag(W0inv)).sum())
+    q = np.arange(1, dim + 1)
+    logCalpha0 = gammaln(K * alpha0) - K * gammaln(alpha0)
+    logCepsilon0 = np.full(K, gammaln(K * epsilon0) - K * gammaln(epsilon0))
+    logB0 = ((v0 / 2) * logdetW0inv - (v0 * dim / 2) * np.log(2) - (dim * (dim - 1) / 4) * np.log(np.pi)
+             - gammaln(0.5 * (v0 + 1 - q)).sum())
+    logCalpha = gammaln(alpha.sum()) - gammaln(alpha).sum()
+    logCeps = gammaln(eps.sum(1)) - gammaln(eps).sum(1)
+    H = 0.0
+    trSW = np.zeros(K)
+    xWx = np.zeros(K)
+    mWm = np.zeros(K)
+    trW0W = np.zeros(K)
+    for k in range(K):
+        logBk = (-(v[k] / 2) * np.log(np.linalg.det(W[k])) - (v[k] * dim / 2) * np.log(2)
+                 - (dim * (dim - 1) / 4) * np.log(np.pi) - gammaln(0.5 * (v[k] + 1 - q)).sum())
+        H = H - logBk - 0.5 * (v[k] - dim - 1) * lLT[k] + 0.5 * v[k] * dim
+        trSW[k] = np.trace(st["t1_S"][k] @ W[k])
+        dx = st["xbar"][k] - m[k]
+        xWx[k] = dx @ W[k] @ dx
+        dm = m[k] - m0
+        mWm[k] = dm @ W[k] @ dm
+        trW0W[k] = np.trace(W0inv @ W[k])
+    Nk = st["Nk"]
+    Lt1 = 0.5 * (Nk * (lLT - dim / beta - v * trSW - v * xWx - dim * np.log(2 * np.pi))).sum()
+    gamma1 = fb["gamma_all"][:, :, 0]
+    Lt2a = (gamma1 * lPi[:, None]).sum()
+    Lt2b = (st["M"] * lA).sum()
+    Lt2 = Lt2a + Lt2b
+    Lt3 = logCalpha0 + (alpha0 - 1) * lPi.sum()
+    Lt4 = (logCepsilon0 + (epsilon0 - 1) * lA.sum(1)).sum()
+    Lt51 = 0.5 * (dim * np.log(beta0 / (2 * np.pi)) + lLT - dim * beta0 / beta - beta0 * v * mWm).sum()
+    Lt52 = K * logB0 + 0.5 * (v0 - dim - 1) * lLT.sum() - 0.5 * (v * trW0W).sum()
+    Lt5 = Lt51 + Lt52
+    Lt63 = (fb["gamma_all"] * fb["logrho_Saved"]).sum()
+    Lt64 = fb["phi_norm"].sum()
+    Lt6 = Lt2a + Lt2b + Lt63 - Lt64
+    Lt7 = ((alpha - 1) * lPi).sum() + logCalpha + (((eps - 1) * lA).sum(1) + logCeps).sum()
+    Lt8 = 0.5 * (lLT + dim * np.log(beta / (2 * np.pi))).sum() - 0.5 * dim * K - H
+    return float(Lt1 + Lt2 + Lt3 + Lt4 + Lt5 - Lt6 - Lt7 - Lt8)
+
+
+# ----------------------------------------------------------------------------
+# EM
+# ----------------------------------------------------------------------------
+def vbhmm_em(data: Sequence[np.ndarray], K: int, opt: dict, gmm: Optional[dict] = None,
+             rng: Optional[np.random.Generator] = None, device="cuda",
+             batch: Optional["vbhmm.SequenceBatch"] = None) -> dict:
+    """vbhmm_em.m:1-491 (usegroups = 0, no derivatives): EM from the posterior
+    vbhmm_init builds out of ``gmm`` (or a 'random' GMM drawn with ``rng``).
+    Returns the output HMM (prior, trans, pdf, LL, gamma, M, N1, N, varpar)
+    plus the bound trajectory ``LLs``."""
+    data = [np.asarray(a, dtype=np.float64).reshape(-1, len(opt["mu0"])) for a in data]
+    opt, clipped = vbhmm_clip_hyps(opt)
+    if gmm is None:
+        gmm = random_gmm(data, K, rng if rng is not None else np.random.default_rng(0))
+    mix = vbhmm_init(data, K, opt, gmm)
+    dim = len(opt["mu0"])
+    lens = np.array([a.shape[0] for a in data])
+    N, maxT = len(data), int(lens.max())
+    X = np.concatenate(data, axis=0)
+    n_idx = np.repeat(np.arange(N), lens)
+    t_idx = np.concatenate([np.arange(n) for n in lens])
+    sb = batch if batch is not None else vbhmm.SequenceBatch(data, dim, device)
+    alpha, eps, beta, v, m, W = (mix[k].copy() for k in ("alpha", "epsilon", "beta", "v", "m", "W"))
+    alpha0, eps0, beta0, v0, m0 = opt["alpha0"], opt["epsilon0"], opt["beta0"], opt["v0"], opt["mu0"]
+    W0inv = mix["W0inv"]
+    L = lastL = -np.finfo(float).max
+    LLs: List[float] = []
+    C = np.zeros((K, dim, dim))
+    unstable = False
+    for it in range(1, int(opt["maxIter"]) + 1):
+        vp = dict(v=v, W=W, epsilon=eps, alpha=alpha, m=m, beta=beta)
+        fb = vbhmm.vbhmm_fb(data, vp, batch=sb)                      # GPU (vbhmm_fb_mex.c)
+        g_all = fb["gamma_all"]                                       # [K, N, maxT]
+        Nk1 = g_all[:, :, 0].sum(1) + 1e-50
+        Nk = g_all.sum(axis=(1, 2)) + 1e-50
+        M = fb["xi_sum"].sum(2)
+        G = g_all[:, n_idx, t_idx]                                    # gamma_block [K, totalT]
+        xbar = (G @ X) / Nk[:, None]
+        t1_S = np.zeros((K, dim, dim))
+        for k in range(K):
+            d1 = X - xbar[k]
+            t1_S[k] = (d1 * G[k][:, None]).T @ d1 / Nk[k]
+        if it > 1:
+            lastL = L
+        st = dict(dim=dim, K=K, N=N, W0inv=W0inv, W0mode=mix["W0mode"], t1_S=t1_S, xbar=xbar,
+                  Nk=Nk, M=M)
+        L = vbhmm_em_lb(st, opt, vp, fb)
+        do_break = False
+        if it > 1 and abs((L - lastL) / lastL) <= opt["minDiff"]:
+            do_break = True
+        if it == opt["maxIter"]:
+            do_break = True
+        if np.isnan(L):  # vbhmm_em.m:314-330
+            do_break, unstable, L = True, True, -np.inf
+        LLs.append(L)
+        if do_break and unstable:
+            break
+        # M-step (vbhmm_em.m:352-408)
+        alpha = alpha0 + Nk1
+        eps = eps0 + M
+        if not opt.get("fix_clusters", 0):
+            beta = beta0 + Nk
+            v = v0 + Nk + 1
+            m = (beta0 * m0[None, :] + Nk[:, None] * xbar) / beta[:, None]
+            for k in range(K):
+                if opt.get("fix_cov") is None:
+                    mult1 = beta0 * Nk[k] / (beta0 + Nk[k])
+                    diff3 = xbar[k] - m0
+                    Wk = np.linalg.inv(W0inv + Nk[k] * t1_S[k] + mult1 * np.outer(diff3, diff3))
+                    W[k] = 0.5 * (Wk + Wk.T)
+                else:
+                    W[k] = np.linalg.inv(opt["fix_cov"]) / (v[k] - dim - 1)
+        for k in range(K):
+            Ck = np.linalg.inv(W[k]) / ((v[k] - dim - 1) if v[k] > dim + 1 else v[k])
+            C[k] = 0.5 * (Ck + Ck.T)
+        if do_break:
+            break
+    prior = alpha / alpha.sum()
+    sc = eps.sum(1, keepdims=True)
+    trans = eps / np.where(sc == 0, 1.0, sc)
+    return dict(prior=prior, trans=trans,
+                pdf=[dict(mean=m[k].copy(), cov=C[k].copy()) for k in range(K)],
+                LL=float(L), LLs=np.array(LLs), iters=it, unstable=unstable,
+                gamma=[g_all[:, n, :lens[n]].copy() for n in range(N)], M=M, N1=Nk1, N=Nk,
+                varpar=dict(epsilon=eps, alpha=alpha, beta=beta, v=v, m=m, W=W.copy()),
+                clipped=clipped)
+
+
+def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
+                gmms: Optional[dict] = None) -> dict:
+    """vbhmm_learn.m (initmode 'random', learn_hyps = 0): for each K, numtrials EM
+    runs from random GMMs (seeded by opt['seed'], vbhmm_learn.m:443-451; K = 1
+    needs one), keep the best bound; over several K, select by LL + gammaln(K+1)
+    (:367-405).  ``gmms[K]`` = list of GMMs to inject instead of random draws."""
+    Ks = [int(k) for k in np.atleast_1d(Ks)]
+    dim = len(opt["mu0"])
+    data = [np.asarray(a, dtype=np.float64).reshape(-1, dim) for a in data]
+    sb = vbhmm.SequenceBatch(data, dim, device)
+    out_all = []
+    for K in Ks:
+        rng = np.random.default_rng(opt["seed"])
+        if gmms is not None and K in gmms:
+            inits = list(gmms[K])
+        else:
+            numits = 1 if K == 1 else int(opt["numtrials"])
+            inits = [random_gmm(data, K, rng) for _ in range(numits)]
+        trials = [vbhmm_em(data, K, opt, gmm=g, batch=sb) for g in inits]
+        LLall = np.array([h["LL"] for h in trials])
+        best = trials[int(np.argmax(LLall))]
+        best["trials_LL"] = LLall
+        out_all.append(best)
+    if len(Ks) == 1:
+        return out_all[0]
+    LLk = np.array([h["LL"] for h in out_all]) + gammaln(np.array(Ks) + 1.0)
+    ind = int(np.argmax(LLk))
+    h = dict(out_all[ind])
+    h.update(model_LL=LLk, model_k=Ks, model_bestK=Ks[ind], model_all=out_all, LL=float(LLk[ind]))
+    return h
+
+
+def vbhmm_learn_batch(datas: Sequence[Sequence[np.ndarray]], Ks, opt: dict, device="cuda",
+                      gmms: Optional[list] = None):
+    """vbhmm_learn_batch.m: one vbhmm_learn per subject; returns (hmms, LLs)."""
+    hmms = [vbhmm_learn(d, Ks, opt, device, gmms[i] if gmms is not None else None)
+            for i, d in enumerate(datas)]
+    return hmms, np.array([h["LL"] for h in hmms])
+
+
+def vbhmm_remove_empty(hmm: dict, thresh: float = 1.0) -> dict:
+    """vbhmm_remove_empty.m:32-103 (usegroups = 0): drop states with N < thresh,
+    renormalise gamma, prior and trans from the kept variational parameters."""
+    keep = np.flatnonzero(~(np.asarray(hmm["N"]) < thresh))
+    if keep.size == len(hmm["N"]):
+        return hmm
+    vp = hmm["varpar"]
+    nvp = dict(alpha=vp["alpha"][keep], epsilon=vp["epsilon"][np.ix_(keep, keep)],
+               beta=vp["beta"][keep], v=vp["v"][keep], m=vp["m"][keep], W=vp["W"][keep])
+    out = dict(hmm)
+    out["varpar"] = nvp
+    out["M"] = hmm["M"][np.ix_(keep, keep)]
+    out["N1"] = hmm["N1"][keep]
+    out["N"] = hmm["N"][keep]
+    out["gamma"] = [g[keep] / g[keep].sum(0, keepdims=True) for g in hmm["gamma"]]
+    out["prior"] = nvp["alpha"] / nvp["alpha"].sum()
+    out["trans"] = nvp["epsilon"] / nvp["epsilon"].sum(1, keepdims=True)
+    out["pdf"] = [hmm["pdf"][k] for k in keep]
+    return out

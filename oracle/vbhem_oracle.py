@@ -608,6 +608,75 @@ def lower_bound(hat_Z, Z, Nj, L_elbo, logOmega, post: dict, consts: dict, opt: d
     return Lt1 + Lt2 + Lt3 + Lt4 + Lt5 + Lt6 - Lt7 - Lt8 - Lt9 - Lt10
 
 
+def lower_bound_derivs(logOmega, post: dict, consts: dict, opt: dict, clipped=None):
+    """vbhemh3m_lb.m:202-356 loop by loop (iid or diag W0; the diag branch with
+    Kr*Sr for the reference's undefined K*S)."""
+    from scipy.special import digamma as ps
+    K = post["alpha"].shape[0]
+    S = opt["S"]
+    d = len(opt["m0"])
+    covmode = opt["covmode"]
+    a0, e0, ep0, m0, l0, v0 = (opt["alpha0"], opt["eta0"], opt["epsilon0"], np.asarray(opt["m0"], float),
+                               opt["lambda0"], opt["v0"])
+    W0 = _W0(opt, d)
+    W0inv = np.linalg.inv(W0)
+    iid = np.size(opt["W0"]) == 1
+    logdetW0inv = d * np.log(W0inv[0, 0]) if iid else np.log(np.diag(W0inv)).sum()
+    dLt = {}
+    dLt["alpha0"] = K * ps(K * a0) - K * ps(a0) + np.sum(logOmega)                  # :206-212
+    dLt["eta0"] = K * (S * ps(S * e0) - S * ps(e0)) + np.sum(consts["logPi"])        # :216-222
+    dLt["epsilon0"] = K * S * (S * ps(S * ep0) - S * ps(ep0)) + np.sum(consts["logA"])  # :226-232
+    dB = 0.5 * logdetW0inv - (d / 2) * np.log(2) - 0.5 * sum(ps(0.5 * (v0 + 1 - q)) for q in range(1, d + 1))
+    dLt["v0"] = K * S * dB + 0.5 * np.sum(consts["logLambdaTilde"])                  # :236-237
+    dl = 0.0
+    for j in range(K):                                                                # :240-248
+        for k in range(S):
+            Wk = post["W"][j, k] if covmode == COV_FULL else np.diag(post["W"][j, k])
+            diff = post["m"][j, k] - m0
+            mWm = diff @ Wk @ diff
+            dl += 0.5 * (d / l0 - d / post["lam"][j, k] - post["v"][j, k] * mWm)
+    dLt["lambda0"] = dl
+    if iid:                                                                           # :251-272
+        w0i = W0inv[0, 0]
+        myW0 = 1.0 / w0i
+        acc = 0.0
+        for j in range(K):
+            for k in range(S):
+                W = post["W"][j, k]
+                tr = np.trace(W) if covmode == COV_FULL else np.sum(W)
+                acc += -post["v"][j, k] * w0i ** 2 * tr
+        dLt["W0"] = np.array([K * S * (-0.5 * v0 * d * w0i) - 0.5 * acc])
+    else:                                                                             # :275-298
+        w0i = np.diag(W0inv)
+        myW0 = 1.0 / w0i
+        acc = np.zeros(d)
+        for j in range(K):
+            for k in range(S):
+                W = post["W"][j, k]
+                dg = np.diag(W) if covmode == COV_FULL else W
+                acc += -post["v"][j, k] * w0i ** 2 * dg
+        dLt["W0"] = K * S * (-0.5 * v0 * w0i) - 0.5 * acc
+    tmp = np.zeros(d)
+    for j in range(K):                                                                # :304-314
+        for k in range(S):
+            Wk = post["W"][j, k] if covmode == COV_FULL else np.diag(post["W"][j, k])
+            tmp += l0 * post["v"][j, k] * (Wk @ (post["m"][j, k] - m0))
+    dLt["m0"] = tmp
+    if clipped is not None:                                                           # :321-334
+        for name, fl in clipped.items():
+            g = np.atleast_1d(dLt[name]).astype(float)
+            for i in range(len(fl)):
+                if fl[i] == 1 and g[i] > 0:
+                    g[i] = 0.0
+                if fl[i] == -1 and g[i] < 0:
+                    g[i] = 0.0
+            dLt[name] = g
+    return dict(d_logalpha0=dLt["alpha0"] * a0, d_logeta0=dLt["eta0"] * e0,            # :337-346
+                d_logepsilon0=dLt["epsilon0"] * ep0, d_logv0D1=dLt["v0"] * (v0 - d + 1),
+                d_loglambda0=dLt["lambda0"] * l0, d_sqrtW0inv=dLt["W0"] * (myW0 ** 1.5) * (-2),
+                d_logW0=dLt["W0"] * myW0, d_m0=dLt["m0"])
+
+
 def convert_to_point(post: dict, covmode: int):
     """convert_h3mrtoh3mb.m:9-79 (posterior -> point-estimate HMMs)."""
     K, S, d = post["m"].shape

@@ -1,0 +1,75 @@
+"""The clustering driver (vbhem_amd.cluster: vbhem_h3m_cluster.m, vbhem_h3m_c.m)
+and the hyperparameter learner (vbhem_amd.hyp: vbhem_h3m_c_hyp.m) on the CPU,
+with the oracle stand-in engine (tests/oracle_engine.py) in place of the
+device E-step: model selection over K and S (+gammaln), trials and their best
+bound, groups, and a short L-BFGS hyperparameter run."""
+import numpy as np
+from scipy.special import gammaln
+
+from oracle_engine import OracleEngine
+
+
+def _factory(base, K, S, T, trials=1):
+    return OracleEngine(base, K, S, T, nthreads=2, trials=trials)
+
+
+def _exprmt1(vb, N=16):
+    return vb.synth_base_set(N, 2, 2, 2, vb.COV_FULL, seed=1002, exprmt1=True)
+
+
+OPT = dict(alpha0=1e6, eta0=1.0, epsilon0=1.0, lambda0=1.0, v0=5.0, W0=1.0, m0=[1.5, 1.5],
+           tau=20, Nv=100, seed=1001, trials=3, max_iter=30, minDiff=1e-5, learn_hyps=0)
+
+
+def test_cluster_model_selection(vb):
+    from vbhem_amd import cluster, em
+    base = _exprmt1(vb)
+    res = cluster.vbhem_h3m_cluster(None, [1, 2], [1, 2], dict(OPT), base=base,
+                                    engine_factory=_factory)
+    # per-K raw bounds (each the best S of its run) + gammaln(K+1) select K
+    raw = np.array([o["LL"] for o in res["model_all"]])
+    np.testing.assert_allclose(res["model_LL"], raw + gammaln(np.array([2.0, 3.0])))
+    assert res["model_bestK"] == [1, 2][int(np.argmax(res["model_LL"]))]
+    for o in res["model_all"]:
+        np.testing.assert_allclose(o["model_LL_S"],
+                                   np.array([x["LL"] for x in o["model_all_s"]]) + gammaln([2.0, 3.0]))
+    assert res["group_size"].sum() == base.N
+    # the chosen model is its best trial: re-run it alone from the same initialisation
+    K, S = res["K"], res["S"]
+    o = vb.default_options(K, S, 2, **{k: v for k, v in OPT.items()})
+    rb, rg, om = vb.baseem_draws(base, K, S, seed=OPT["seed"] + res["best"] + 1)
+    P = vb.baseem_init(base, o, rb, rg, om)
+    one = em.vbhem_h3m_c_step_fc(P, _factory(base, K, S, OPT["tau"]), o)
+    assert one.iters == res["result"].iters
+    np.testing.assert_allclose(one.LogLs, res["result"].LogLs, rtol=1e-12)
+    assert res["LL"] == max(res["LLall"])
+
+
+def test_trials_chunking_matches_one_launch(vb):
+    """Batched trials (one launch for all) equal the same trials run one per launch."""
+    from vbhem_amd import cluster
+    base = _exprmt1(vb, N=10)
+    o = vb.default_options(2, 2, 2, **dict(OPT, trials=4, max_iter=8))
+    a = cluster.vbhem_h3m_c(base, o, engine_factory=_factory)
+    b_results = []
+    for r in range(4):  # one trial per launch
+        oo = dict(o, trials=1, seed=o["seed"] + r)
+        b_results.append(cluster.vbhem_h3m_c(base, oo, engine_factory=_factory)["LL"])
+    np.testing.assert_allclose(a["LLall"], b_results, rtol=1e-12)
+
+
+def test_hyp_learning_cpu(vb):
+    from vbhem_amd import em, hyp
+    base = _exprmt1(vb, N=12)
+    o = vb.default_options(2, 2, 2, **dict(OPT, max_iter=40, minDiff=1e-8, learn_hyps=1))
+    rb, rg, om = vb.baseem_draws(base, 2, 2, seed=7)
+    P = vb.baseem_init(base, o, rb, rg, om)
+    eng = _factory(base, 2, 2, o["tau"])
+    start = em.vbhem_h3m_c_step_fc(P, eng, o)
+    out = hyp.vbhem_h3m_c_hyp(base, o, start.post, eng, length=3)
+    assert out["evaluations"] >= 2 and np.isfinite(out["result"].LL)
+    # the optimiser's recorded objective never increases (it minimises -LL)
+    assert np.all(np.diff(out["fX"]) <= 1e-9 * np.abs(out["fX"][:-1]))
+    # the final run uses the optimised hyperparameters, clipped into range
+    for name in ("alpha0", "eta0", "epsilon0", "lambda0"):
+        assert o["hyps_min"][name] <= out["vbopt"][name] <= o["hyps_max"][name]
