@@ -74,15 +74,25 @@ def vbhem_h3m_c(base: BaseSet, opt: dict, device="cuda", engine_factory=None,
     for it in range(1, R + 1):
         rb, rg, om = baseem_draws(base, K, S, seed=int(opt["seed"]) + it)
         posts.append(baseem_init(base, opt, rb, rg, om))
-    per = max(1, 256 // K)
     results, LLs = [], []
-    for r0 in range(0, R, per):
-        chunk = posts[r0:r0 + per]
-        eng = make(base, len(chunk) * K, S, opt["tau"], trials=len(chunk))
-        tr = em.vbhem_h3m_c_trials(chunk, eng, opt)
-        results.extend(tr.results)
-        LLs.extend(tr.LLall.tolist())
-        del eng
+    if S <= 16 and base.SB <= S:
+        per = max(1, 256 // K)
+        for r0 in range(0, R, per):
+            chunk = posts[r0:r0 + per]
+            eng = make(base, len(chunk) * K, S, opt["tau"], trials=len(chunk))
+            tr = em.vbhem_h3m_c_trials(chunk, eng, opt)
+            results.extend(tr.results)
+            LLs.extend(tr.LLall.tolist())
+            del eng
+    else:
+        # base HMMs with more states than the clusters (or S > 16): the batched-trials
+        # launch needs the column-split kernel (Sb <= S), so the trials run one after
+        # another through the single-trial fused E-step (generic kernel)
+        one = make(base, K, S, opt["tau"], trials=1)
+        for P in posts:
+            r = em.vbhem_h3m_c_step_fc(P, one, opt)
+            results.append(r)
+            LLs.append(r.LL)
     LLall = np.array(LLs)
     learn = opt.get("learn_hyps", 0) if hyp_learn is None else hyp_learn
     hyp_info = None
