@@ -24,7 +24,7 @@ oracle:
 	$(MAKE) -C oracle liboracle.so
 
 # test-only: a MATLAB mx/mex API double and the MEX gateway built against it
-mex: tests/mxshim/libmxshim.so $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so $(LIBDIR)/hem_hmm_bwd_fwd_mex.so $(LIBDIR)/vbhmm_fb_mex.so
+mex: tests/mxshim/libmxshim.so $(LIBDIR)/vbhem_hmm_bwd_fwd_mex.so $(LIBDIR)/hem_hmm_bwd_fwd_mex.so $(LIBDIR)/vbhmm_fb_mex.so $(LIBDIR)/vbhem_estep_fused_mex.so
 
 tests/mxshim/libmxshim.so: tests/mxshim/mxshim.c tests/mxshim/mex.h
 	gcc -O2 -fPIC -shared -Itests/mxshim -o $@ $<

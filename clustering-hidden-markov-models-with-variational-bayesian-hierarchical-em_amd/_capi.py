@@ -78,6 +78,12 @@ EXPORTS = {
     "vbhem_estep_fused_trials": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
                                           _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "vbhem_last_fallback_count": (_c_int, [_vp, _vp]),
+    "vbhem_ctx_create": (_c_int, [_c_int, ctypes.POINTER(BaseT), _c_int, _c_int, _c_int, _c_int,
+                                  ctypes.POINTER(_vp)]),
+    "vbhem_ctx_fused": (_c_int, [_vp, ctypes.POINTER(ClusterT), _vp, _vp, _vp, _vp, _vp]),
+    "vbhem_ctx_destroy": (None, [_vp]),
+    "vbhem_estep_fused_host": (_c_int, [_c_int, ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT),
+                                        _c_int, _vp, _vp, _vp, _vp, _vp]),
     "vbhem_timing_enable": (_c_int, [_c_int]),
     "vbhem_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                    ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double),

@@ -851,3 +851,155 @@ int vhem_estep_pairs_host(int device, const vbhem_base_t *bh, const vbhem_cluste
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Host-array fused E-step: a context with the base set resident on a device.
+// ---------------------------------------------------------------------------
+struct vbhem_ctx {
+  int device = 0, N = 0, SB = 0, d = 0, covmode = 0, K = 0, S = 0, R = 1, T = 1;
+  size_t stats_len = 0, ws_bytes = 0;
+  hipStream_t stream = nullptr;
+  int *nstates = nullptr;
+  double *prior = nullptr, *A = nullptr, *centres = nullptr, *covars = nullptr;
+  double *logA = nullptr, *logPi = nullptr, *m = nullptr, *P = nullptr, *c = nullptr;
+  double *tildeN = nullptr, *logOmega = nullptr, *stats = nullptr, *hatZ = nullptr, *LL = nullptr;
+  void *ws = nullptr;
+};
+
+namespace {
+
+void ctx_free(vbhem_ctx *x) {
+  if (!x) return;
+  int prev = 0;
+  const bool dev_ok = hipGetDevice(&prev) == hipSuccess && hipSetDevice(x->device) == hipSuccess;
+  void *ptrs[] = {x->nstates, x->prior, x->A, x->centres, x->covars, x->logA, x->logPi, x->m,
+                  x->P, x->c, x->tildeN, x->logOmega, x->stats, x->hatZ, x->LL, x->ws};
+  for (void *q : ptrs)
+    if (q) (void)hipFree(q);
+  if (x->stream) (void)hipStreamDestroy(x->stream);
+  if (dev_ok) (void)hipSetDevice(prev);
+  delete x;
+}
+
+template <class T>
+hipError_t dev_alloc(T **p, size_t n) {
+  return hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(1, n) * sizeof(T));
+}
+
+}  // namespace
+
+extern "C" {
+
+int vbhem_ctx_create(int device, const vbhem_base_t *bh, int K, int S, int R, int T,
+                     vbhem_ctx_t **ctx_out) {
+  if (!ctx_out) return fail(VBHEM_ERR_ARG, "null context pointer");
+  *ctx_out = nullptr;
+  vbhem_cluster_t probe{K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int rc = check_inputs(bh, &probe, T, false);
+  if (rc != VBHEM_OK) return rc;
+  if (bh->N > 0 && (!bh->prior || !bh->A || !bh->centres || !bh->covars))
+    return fail(VBHEM_ERR_ARG, "null base array");
+  if (R < 1 || K % R != 0) return fail(VBHEM_ERR_ARG, "trials: K must be a positive multiple of R");
+  vbhem_ctx *x = new vbhem_ctx;
+  x->device = device; x->N = bh->N; x->SB = bh->SB; x->d = bh->d; x->covmode = bh->covmode;
+  x->K = K; x->S = S; x->R = R; x->T = T;
+  x->stats_len = (size_t)R * vbhem_stats_len(K / R, S, bh->d, bh->covmode);
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { ctx_free(x); return hip_fail(e, "hipSetDevice"); }
+  e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
+  const size_t N = bh->N, SB = bh->SB, d = bh->d;
+  const size_t dC = bh->covmode == VBHEM_COV_FULL ? d * d : d;
+  if (e == hipSuccess) e = dev_alloc(&x->nstates, N);
+  if (e == hipSuccess) e = dev_alloc(&x->prior, N * SB);
+  if (e == hipSuccess) e = dev_alloc(&x->A, N * SB * SB);
+  if (e == hipSuccess) e = dev_alloc(&x->centres, N * SB * d);
+  if (e == hipSuccess) e = dev_alloc(&x->covars, N * SB * dC);
+  if (e == hipSuccess) e = dev_alloc(&x->logA, (size_t)K * S * S);
+  if (e == hipSuccess) e = dev_alloc(&x->logPi, (size_t)K * S);
+  if (e == hipSuccess) e = dev_alloc(&x->m, (size_t)K * S * d);
+  if (e == hipSuccess) e = dev_alloc(&x->P, (size_t)K * S * dC);
+  if (e == hipSuccess) e = dev_alloc(&x->c, (size_t)K * S);
+  if (e == hipSuccess) e = dev_alloc(&x->tildeN, N);
+  if (e == hipSuccess) e = dev_alloc(&x->logOmega, (size_t)K);
+  if (e == hipSuccess) e = dev_alloc(&x->stats, x->stats_len);
+  if (e == hipSuccess) e = dev_alloc(&x->hatZ, N * K);
+  if (e == hipSuccess) e = dev_alloc(&x->LL, N * K);
+  if (e != hipSuccess) { ctx_free(x); return hip_fail(e, "vbhem_ctx_create(alloc)"); }
+  if (N > 0) {
+    if (bh->nstates) {
+      e = hipMemcpy(x->nstates, bh->nstates, N * sizeof(int), hipMemcpyHostToDevice);
+    } else {
+      std::vector<int> ns(N, (int)SB);
+      e = hipMemcpy(x->nstates, ns.data(), N * sizeof(int), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess) e = hipMemcpy(x->prior, bh->prior, N * SB * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(x->A, bh->A, N * SB * SB * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(x->centres, bh->centres, N * SB * d * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(x->covars, bh->covars, N * SB * dC * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { ctx_free(x); return hip_fail(e, "vbhem_ctx_create(upload)"); }
+  }
+  vbhem_base_t bd{bh->N, bh->SB, bh->d, bh->covmode, x->nstates, x->prior, x->A, x->centres,
+                  x->covars};
+  vbhem_cluster_t cd{K, S, x->logA, x->logPi, x->m, x->P, x->c};
+  x->ws_bytes = vbhem_fused_trials_workspace_bytes(&bd, &cd, R, T);
+  if (x->ws_bytes == 0) { ctx_free(x); return fail(VBHEM_ERR_ARG, "vbhem_ctx_create: bad sizes"); }
+  e = hipMalloc(&x->ws, x->ws_bytes);
+  if (e != hipSuccess) { ctx_free(x); return hip_fail(e, "vbhem_ctx_create(workspace)"); }
+  *ctx_out = x;
+  return VBHEM_OK;
+}
+
+int vbhem_ctx_fused(vbhem_ctx_t *x, const vbhem_cluster_t *ch, const double *tildeN_host,
+                    const double *logOmega_host, double *stats_host, double *hatZ_host,
+                    double *LL_host) {
+  if (!x || !ch) return fail(VBHEM_ERR_ARG, "null context or cluster descriptor");
+  if (ch->K != x->K || ch->S != x->S)
+    return fail(VBHEM_ERR_ARG, "cluster descriptor K/S differ from the context's");
+  if (!ch->logA || !ch->logPi || !ch->m || !ch->P || !ch->c || !logOmega_host || !stats_host ||
+      (x->N > 0 && !tildeN_host))
+    return fail(VBHEM_ERR_ARG, "null host array");
+  hipError_t e = hipSetDevice(x->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  const size_t K = x->K, S = x->S, d = x->d, N = x->N;
+  const size_t dC = x->covmode == VBHEM_COV_FULL ? d * d : d;
+  hipStream_t st = x->stream;
+  e = hipMemcpyAsync(x->logA, ch->logA, K * S * S * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(x->logPi, ch->logPi, K * S * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(x->m, ch->m, K * S * d * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(x->P, ch->P, K * S * dC * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(x->c, ch->c, K * S * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(x->logOmega, logOmega_host, K * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && N > 0)
+    e = hipMemcpyAsync(x->tildeN, tildeN_host, N * 8, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) return hip_fail(e, "vbhem_ctx_fused(upload)");
+  vbhem_base_t bd{x->N, x->SB, x->d, x->covmode, x->nstates, x->prior, x->A, x->centres,
+                  x->covars};
+  vbhem_cluster_t cd{x->K, x->S, x->logA, x->logPi, x->m, x->P, x->c};
+  int rc = vbhem_estep_fused_trials(&bd, &cd, x->R, x->T, x->tildeN, x->logOmega, x->stats,
+                                    x->hatZ, x->LL, x->ws, x->ws_bytes, st);
+  if (rc != VBHEM_OK) return rc;
+  e = hipMemcpyAsync(stats_host, x->stats, x->stats_len * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && hatZ_host && N > 0)
+    e = hipMemcpyAsync(hatZ_host, x->hatZ, N * K * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && LL_host && N > 0)
+    e = hipMemcpyAsync(LL_host, x->LL, N * K * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "vbhem_ctx_fused(download)");
+  return VBHEM_OK;
+}
+
+void vbhem_ctx_destroy(vbhem_ctx_t *x) { ctx_free(x); }
+
+int vbhem_estep_fused_host(int device, const vbhem_base_t *bh, const vbhem_cluster_t *ch, int T,
+                           const double *tildeN_host, const double *logOmega_host,
+                           double *stats_host, double *hatZ_host, double *LL_host) {
+  if (!ch) return fail(VBHEM_ERR_ARG, "null cluster descriptor");
+  vbhem_ctx_t *x = nullptr;
+  int rc = vbhem_ctx_create(device, bh, ch->K, ch->S, 1, T, &x);
+  if (rc != VBHEM_OK) return rc;
+  rc = vbhem_ctx_fused(x, ch, tildeN_host, logOmega_host, stats_host, hatZ_host, LL_host);
+  vbhem_ctx_destroy(x);
+  return rc;
+}
+
+}  // extern "C"

@@ -154,6 +154,31 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
                              double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
                              void *workspace_dev, size_t workspace_bytes, void *stream);
 
+/* Host-array entry points of the fused E-step (what a MATLAB gateway binds; see
+ * integration/vbhem_estep_fused_mex.c and INTEGRATION.md).
+ *
+ * A context keeps one base set resident on `device` (uploaded once) together
+ * with the workspace and output buffers for K clusters of S states (R batched
+ * trials, K a multiple of R); each vbhem_ctx_fused call uploads only the
+ * cluster constants (tens of KB), runs vbhem_estep_fused_trials and copies
+ * back the packed statistics (and, when the pointers are non-NULL, hat_Z and
+ * L_elbo as [N][K]).  Host arrays in/out, synchronous.  A context is used by
+ * one host thread at a time.
+ *   clus_host: K, S must match the context; tildeN_host [N]; logOmega_host [K];
+ *   stats_host [R * vbhem_stats_len(K/R, S, d, covmode)].
+ * vbhem_estep_fused_host is the one-shot form (create, one call, destroy). */
+typedef struct vbhem_ctx vbhem_ctx_t;
+int vbhem_ctx_create(int device, const vbhem_base_t *base_host, int K, int S, int R, int T,
+                     vbhem_ctx_t **ctx_out);
+int vbhem_ctx_fused(vbhem_ctx_t *ctx, const vbhem_cluster_t *clus_host, const double *tildeN_host,
+                    const double *logOmega_host, double *stats_host, double *hatZ_host,
+                    double *LL_elbo_host);
+void vbhem_ctx_destroy(vbhem_ctx_t *ctx);
+int vbhem_estep_fused_host(int device, const vbhem_base_t *base_host,
+                           const vbhem_cluster_t *clus_host, int T, const double *tildeN_host,
+                           const double *logOmega_host, double *stats_host, double *hatZ_host,
+                           double *LL_elbo_host);
+
 /* Fused E-step schedule of the calling host thread (default VBHEM_FUSED_GATED,
  * or VBHEM_FUSED_DENSE=1 in the environment).  Both give the same outputs:
  *   VBHEM_FUSED_GATED  backward sweep + log-likelihood for every pair, then the

@@ -110,6 +110,83 @@ static inline void pack_bases(buffers_t *bp, const mxArray *h3m_b, int Kb, int S
   *bp = b;
 }
 
+
+/* cluster HMMs (mex.c:433-457): every cluster has S = maxN2 states.  Fills
+ * b->logA, logPi, m, P, c; full covariances take c and P from
+ * logdetCovPlusDdivlamR / invCovR (mex.c:785-830), diagonal ones from the emit
+ * fields (mex.c:718-760). */
+static inline void pack_clusters(buffers_t *bp, const mxArray *h3m_r, int Kr, int S, int d,
+                                 int covmode, const mxArray *logdetR, const mxArray *invCovR) {
+  buffers_t b = *bp;
+  const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
+  b.logA = (double *)mxCalloc((size_t)Kr * S * S, sizeof(double));
+  b.logPi = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
+  b.m = (double *)mxCalloc((size_t)Kr * S * d, sizeof(double));
+  b.P = (double *)mxCalloc((size_t)Kr * S * dd, sizeof(double));
+  b.c = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
+  for (int j = 0; j < Kr; j++) {
+    const mxArray *hr = mxGetCell(h3m_r, j);
+    if (!hr || !mxIsStruct(hr)) {
+      *bp = b;
+      free_buffers(bp);
+      mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d} must be a struct", j + 1);
+    }
+    const mxArray *lA = mxGetField(hr, 0, "logATilde");
+    if (!lA || (int)mxGetM(lA) != S || (int)mxGetN(lA) != S) {
+      *bp = b;
+      free_buffers(bp);
+      mexErrMsgIdAndTxt("vbhem_mex:unsupported",
+                        "h3m_r{%d}.logATilde must be maxN2 x maxN2 (all clusters equal size)", j + 1);
+    }
+    const double *pA = mxGetPr(lA);
+    const double *pPi = field_pr(hr, "logPiTilde", (size_t)S, "h3m_r");
+    for (int r = 0; r < S; r++) {
+      b.logPi[(size_t)j * S + r] = pPi[r];
+      for (int s = 0; s < S; s++) b.logA[((size_t)j * S + r) * S + s] = pA[r + (size_t)s * S];
+    }
+    const mxArray *emit = mxGetField(hr, 0, "emit");
+    const double *ldet = NULL, *icov = NULL;
+    if (covmode == VBHEM_COV_FULL) {
+      const mxArray *lc = mxGetCell(logdetR, j), *ic = mxGetCell(invCovR, j);
+      if (!lc || mxGetNumberOfElements(lc) != (size_t)S || !ic ||
+          mxGetNumberOfElements(ic) != (size_t)S * d * d) {
+        *bp = b;
+      free_buffers(bp);
+        mexErrMsgIdAndTxt("vbhem_mex:invalidinput",
+                          "logdetCovPlusDdivlamR{%d} / invCovR{%d} have wrong sizes", j + 1, j + 1);
+      }
+      ldet = mxGetPr(lc);
+      icov = mxGetPr(ic);
+    }
+    for (int s = 0; s < S; s++) {
+      const mxArray *es = emit ? mxGetCell(emit, s) : NULL;
+      if (!es) {
+        *bp = b;
+      free_buffers(bp);
+        mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d}.emit{%d} missing", j + 1, s + 1);
+      }
+      const double *pm = field_pr(es, "m", (size_t)d, "h3m_r emit");
+      double *dm = b.m + ((size_t)j * S + s) * d;
+      for (int a = 0; a < d; a++) dm[a] = pm[a];
+      double *dP = b.P + ((size_t)j * S + s) * dd;
+      if (covmode == VBHEM_COV_FULL) {
+        b.c[(size_t)j * S + s] = ldet[s];
+        /* invCovR{j}(a,b,s) at a + b*d + s*d*d (column-major) */
+        for (int a = 0; a < d; a++)
+          for (int c2 = 0; c2 < d; c2++)
+            dP[(size_t)a * d + c2] = icov[a + (size_t)c2 * d + (size_t)s * d * d];
+      } else {
+        const double *pW = field_pr(es, "W", (size_t)d, "h3m_r emit");
+        const double v = field_pr(es, "v", 1, "h3m_r emit")[0];
+        b.c[(size_t)j * S + s] = field_pr(es, "logLambdaTildePlusDdivlamda", 1, "h3m_r emit")[0];
+        for (int a = 0; a < d; a++) dP[a] = v * pW[a];
+      }
+    }
+  }
+
+  *bp = b;
+}
+
 /* outputs (mex.c:396-409, 1108-1122, 1312-1345), column-major */
 static inline void scatter_outputs(mxArray *plhs[], const buffers_t *bp, int Kb, int Kr, int S,
                                    int d, int covmode) {

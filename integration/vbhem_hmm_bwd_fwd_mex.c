@@ -68,66 +68,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
   buffers_t b;
   memset(&b, 0, sizeof(b));
-  b.logA = (double *)mxCalloc((size_t)Kr * S * S, sizeof(double));
-  b.logPi = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
-  b.m = (double *)mxCalloc((size_t)Kr * S * d, sizeof(double));
-  b.P = (double *)mxCalloc((size_t)Kr * S * dd, sizeof(double));
-  b.c = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
-  for (int j = 0; j < Kr; j++) {
-    const mxArray *hr = mxGetCell(h3m_r, j);
-    if (!hr || !mxIsStruct(hr)) {
-      free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d} must be a struct", j + 1);
-    }
-    const mxArray *lA = mxGetField(hr, 0, "logATilde");
-    if (!lA || (int)mxGetM(lA) != S || (int)mxGetN(lA) != S) {
-      free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:unsupported",
-                        "h3m_r{%d}.logATilde must be maxN2 x maxN2 (all clusters equal size)", j + 1);
-    }
-    const double *pA = mxGetPr(lA);
-    const double *pPi = field_pr(hr, "logPiTilde", (size_t)S, "h3m_r");
-    for (int r = 0; r < S; r++) {
-      b.logPi[(size_t)j * S + r] = pPi[r];
-      for (int s = 0; s < S; s++) b.logA[((size_t)j * S + r) * S + s] = pA[r + (size_t)s * S];
-    }
-    const mxArray *emit = mxGetField(hr, 0, "emit");
-    const double *ldet = NULL, *icov = NULL;
-    if (covmode == VBHEM_COV_FULL) {
-      const mxArray *lc = mxGetCell(logdetR, j), *ic = mxGetCell(invCovR, j);
-      if (!lc || mxGetNumberOfElements(lc) != (size_t)S || !ic ||
-          mxGetNumberOfElements(ic) != (size_t)S * d * d) {
-        free_buffers(&b);
-        mexErrMsgIdAndTxt("vbhem_mex:invalidinput",
-                          "logdetCovPlusDdivlamR{%d} / invCovR{%d} have wrong sizes", j + 1, j + 1);
-      }
-      ldet = mxGetPr(lc);
-      icov = mxGetPr(ic);
-    }
-    for (int s = 0; s < S; s++) {
-      const mxArray *es = emit ? mxGetCell(emit, s) : NULL;
-      if (!es) {
-        free_buffers(&b);
-        mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d}.emit{%d} missing", j + 1, s + 1);
-      }
-      const double *pm = field_pr(es, "m", (size_t)d, "h3m_r emit");
-      double *dm = b.m + ((size_t)j * S + s) * d;
-      for (int a = 0; a < d; a++) dm[a] = pm[a];
-      double *dP = b.P + ((size_t)j * S + s) * dd;
-      if (covmode == VBHEM_COV_FULL) {
-        b.c[(size_t)j * S + s] = ldet[s];
-        /* invCovR{j}(a,b,s) at a + b*d + s*d*d (column-major) */
-        for (int a = 0; a < d; a++)
-          for (int c2 = 0; c2 < d; c2++)
-            dP[(size_t)a * d + c2] = icov[a + (size_t)c2 * d + (size_t)s * d * d];
-      } else {
-        const double *pW = field_pr(es, "W", (size_t)d, "h3m_r emit");
-        const double v = field_pr(es, "v", 1, "h3m_r emit")[0];
-        b.c[(size_t)j * S + s] = field_pr(es, "logLambdaTildePlusDdivlamda", 1, "h3m_r emit")[0];
-        for (int a = 0; a < d; a++) dP[a] = v * pW[a];
-      }
-    }
-  }
+  pack_clusters(&b, h3m_r, Kr, S, d, covmode, logdetR, invCovR);
 
   pack_bases(&b, h3m_b, Kb, SB, d, covmode);
 

@@ -27,6 +27,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libvbhem_estep.so")
 GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "vbhem_hmm_bwd_fwd_mex.so")
 HEM_GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "hem_hmm_bwd_fwd_mex.so")
 FB_GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "vbhmm_fb_mex.so")
+FUSED_GATEWAY_PATH = os.path.join(PKG_DIR, "lib", "vbhem_estep_fused_mex.so")
 MXSHIM_PATH = os.path.join(ROOT, "tests", "mxshim", "libmxshim.so")
 MATHCHECK_PATH = os.path.join(ROOT, "tests", "mathcheck", "libmathcheck.so")
 GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
@@ -113,6 +114,16 @@ def fb_gateway():
         _make("mex")
     shim = ctypes.CDLL(MXSHIM_PATH, mode=ctypes.RTLD_GLOBAL)
     gw = ctypes.CDLL(FB_GATEWAY_PATH, mode=ctypes.RTLD_GLOBAL)
+    return gw, shim
+
+
+@pytest.fixture(scope="session")
+def fused_gateway():
+    """(mexFunction of the fused E-step gateway, mxshim)."""
+    if not (os.path.exists(FUSED_GATEWAY_PATH) and os.path.exists(MXSHIM_PATH)):
+        _make("mex")
+    shim = ctypes.CDLL(MXSHIM_PATH, mode=ctypes.RTLD_GLOBAL)
+    gw = ctypes.CDLL(FUSED_GATEWAY_PATH, mode=ctypes.RTLD_GLOBAL)
     return gw, shim
 
 

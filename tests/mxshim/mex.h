@@ -46,6 +46,7 @@ void *mxCalloc(size_t n, size_t sz);
 void mxFree(void *p);
 void mexErrMsgIdAndTxt(const char *id, const char *fmt, ...);
 int mexPrintf(const char *fmt, ...);
+int mexAtExit(void (*fn)(void));
 
 /* the gateway entry point MATLAB calls */
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]);

@@ -155,6 +155,17 @@ int mexPrintf(const char *fmt, ...) {
 }
 
 /* ---- test-harness helpers (not part of the MATLAB API) ------------------------- */
+/* MATLAB runs the registered function when the MEX file is cleared; the double
+   runs it from mxshim_clear() */
+static void (*g_atexit)(void) = NULL;
+int mexAtExit(void (*fn)(void)) {
+  g_atexit = fn;
+  return 0;
+}
+void mxshim_clear(void) {
+  if (g_atexit) g_atexit();
+}
+
 typedef void (*mex_fn)(int, mxArray **, int, const mxArray **);
 
 /* Returns 0 on success, 1 if the gateway raised mexErrMsgIdAndTxt. */
