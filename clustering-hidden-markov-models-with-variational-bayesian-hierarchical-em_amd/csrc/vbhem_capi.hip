@@ -313,6 +313,9 @@ struct FbCtx {
   FbPlan plan;      // generic element-per-lane kernel
   SplitPlan split;  // column-per-LPC-lanes kernel (preferred when it applies)
   SplitPlan bwd;    // its backward-only mode (gated schedule), possibly another LPC
+  // the backward-only pass on fb_bwd2_kernel (S <= 8): LDS bytes, pairs per block
+  size_t bwd2_lds = 0;
+  int bwd2_ppb = 0;
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
 };
@@ -346,6 +349,10 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
     a.prior = b->prior; a.A = b->A; a.logA = cl->logA; a.logPi = cl->logPi;
     vbhem::SplitArgs &ab = c.bwd.a;
     ab.prior = b->prior; ab.A = b->A; ab.logA = cl->logA; ab.logPi = cl->logPi;
+    if (c.bwd.ok && cl->S <= vbhem::kBwd2MaxS && !std::getenv("VBHEM_NO_BWD2")) {
+      c.bwd2_lds = vbhem::bwd2_lds(cl->S, 4);
+      c.bwd2_ppb = vbhem::bwd2_ppb(cl->S, 4);
+    }
   }
   return VBHEM_OK;
 }
@@ -435,13 +442,25 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
     const unsigned ntile = (unsigned)((i_end - i_begin + sp.ppb - 1) / sp.ppb);
     unsigned grid = ntile * (unsigned)ca.K;
-    if (mode == vbhem::kFbBackward) {  // persistent: NB blocks per cluster (x8 when possible)
-      unsigned nb = std::max(1u, std::min(ntile, list_grid(ca, sp.lds_bwd) / (unsigned)ca.K));
+    if (mode == vbhem::kFbBackward && c.bwd2_lds) {
+      // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
+      ca.nwb = 4;
+      const unsigned nt2 = (unsigned)((i_end - i_begin + c.bwd2_ppb - 1) / c.bwd2_ppb);
+      const unsigned all = (unsigned)(vbhem::device_cus() *
+                                      std::max(1, vbhem::bwd2_resident_blocks(ca.S, 4, c.bwd2_lds)));
+      unsigned nb = std::max(1u, std::min(nt2, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
-      grid = (unsigned)ca.K * nb;
+      e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, c.bwd2_lds, st);
+      if (e != hipSuccess) return hip_fail(e, "fb_bwd2_kernel");
+    } else {
+      if (mode == vbhem::kFbBackward) {  // persistent: NB blocks per cluster (x8 when possible)
+        unsigned nb = std::max(1u, std::min(ntile, list_grid(ca, sp.lds_bwd) / (unsigned)ca.K));
+        if (nb >= 8) nb = nb / 8 * 8;
+        grid = (unsigned)ca.K * nb;
+      }
+      e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? sp.lds_bwd : sp.lds, st);
+      if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
     }
-    e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? sp.lds_bwd : sp.lds, st);
-    if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
   } else {
     const int nib = (i_end - i_begin + a.BI - 1) / a.BI;
     const dim3 grid((unsigned)nib * (unsigned)a.njb);

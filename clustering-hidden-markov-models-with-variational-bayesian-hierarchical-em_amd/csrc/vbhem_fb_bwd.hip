@@ -1,0 +1,366 @@
+// vbhem_fb_bwd.hip -- the gated schedule's backward-only pass for S <= 8: K2 (the
+// backward recursion, mex.c:915-1015) and K3 (termination, mex.c:1020-1080) for
+// EVERY pair, writing L_elbo; the forward quantities of the gated pairs come from
+// fb_split_kernel's list mode afterwards (vbhem_fb_split.hip).
+//
+// Why a kernel of its own (measured): the backward sweep is
+// fp64-VALU bound with no MFMA to offload to (on gfx950 v_mfma_f64_* and the fp64
+// VALU do not run concurrently: scripts/ubench_valu.hip), and in fb_split_kernel's
+// one-column-per-lane layout a third of the kernel time went to waiting on the
+// scalar loads of the cluster matrix A' (64 doubles do not fit the 102 SGPRs, so
+// every step reloads them; removing those loads alone cut the kernel 2.10 -> 1.44
+// ms).  Here every lane owns TWO base-state columns of its pair, so each scalar
+// A' value feeds two FMAs, each slab read feeds two FMAs, and the lane has twice
+// the independent exp/log chains.
+//
+// Layout.  LPP = ceil(S/2) lanes per pair, PPW = floor(64/LPP) pairs per
+// wavefront (pairs never straddle a wavefront: every exchange is wave-local), one
+// cluster j per block, consecutive bases.  Lane w of a pair owns columns b = w and
+// b = w + LPP (padded columns past SB duplicate column SB-1 with zero base
+// transitions and prior: exact no-ops, as in fb_split_kernel).  In registers per
+// column: Ef[S], Lf[S], arow[S] (Ab row b).  Per step:
+//   M = max_s (Ef + Lf), G = exp(Ef + Lf - M)        (table exp, LDS table)
+//   Z = A' G                                          (A' rows as scalar operands)
+//   sv = M + log Z                                    (table log, LDS table)
+//   Lf = sum_b' Ab[b][b'] sv[.][b']                   (per-pair LDS slab)
+// with the cluster row maxima folded out of the loop: A' = exp(logA - amax),
+// sv_ref = sv + amax, so L_ref = Lf + amax * rowsum(Ab) and E + L_ref = Ef + Lf
+// with Ef = E + amax * rowsum(Ab) (once per pair).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <type_traits>
+
+#include "vbhem_internal.h"
+#include "vbhem_log_table.h"
+#include "vbhem_math.h"
+
+#ifndef VBHEM_BWD2_WAVES
+#define VBHEM_BWD2_WAVES 3
+#endif
+
+namespace vbhem {
+
+namespace {
+
+constexpr double kZMinB = 1e-200;
+alignas(16) __device__ const double kLogTabB[kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
+alignas(16) __device__ const double kExpTabB[kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
+
+// compact LDS tables of exp_tabc_n / log_tabc_n (vbhem_math.h)
+constexpr int kTabExpD = kExpTabEntries;        // 256 doubles
+constexpr int kTabLogD = 2 * kLogTabEntries;    // 256 doubles
+constexpr int kTabD = kTabExpD + kTabLogD;
+
+// acc += bcast(a from lane N of this lane's 16-lane row) * b: v_fmac_f64 with DPP
+// row_newbcast, the one DPP control the fp64 ALU takes
+template <int N>
+__device__ __forceinline__ void dpp_fmac_bcast(double &acc, double a, double b) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(a), "v"(b), "i"(N));
+}
+
+// f(integral_constant<int, I>) for I = B .. E-1, in order
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int S>
+struct Bwd2Layout {
+  static constexpr int LPP = (S + 1) / 2;            // lanes per pair
+  static constexpr int PPW = 64 / LPP;               // pairs per wavefront
+  static constexpr int SP = 2 * LPP;                 // slab columns (padded)
+  static constexpr int XCS = (S + 1) / 2 * 2 + 2;    // slab column stride (even: 16-B rows)
+  static constexpr int XP = SP * XCS + 2;            // per-pair slab (doubles)
+  static constexpr int OFF_CL = kTabD;               // amax [S], lpi [S]
+  static constexpr int OFF_X = (kTabD + 2 * S + 1) / 2 * 2;
+};
+
+}  // namespace
+
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBHEM_BWD2_WAVES)))
+void fb_bwd2_kernel(const SplitArgs p) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using LY = Bwd2Layout<S>;
+  constexpr int LPP = LY::LPP, PPW = LY::PPW;
+  const int tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
+  const int PPB = NW * PPW;
+  const int SB = p.SB, K = p.K, T = p.T;
+  double *etab = lds;                    // [256]
+  double *ltab = lds + kTabExpD;         // [128][2]
+  double *amax = lds + LY::OFF_CL;       // [S]
+  double *lpi = amax + S;                // [S]
+  double *Xall = lds + LY::OFF_X;        // [PPB][XP]
+  int *F = reinterpret_cast<int *>(Xall + (size_t)PPB * LY::XP);  // [PPB]
+
+  for (int x = tid; x < kExpTabEntries; x += NT) etab[x] = kExpTabB[2 * x];
+  for (int x = tid; x < kLogTabEntries; x += NT) {
+    ltab[2 * x] = kLogTabB[4 * x];
+    ltab[2 * x + 1] = kLogTabB[4 * x + 1];
+  }
+  // persistent: NB blocks per cluster; XCD-aware when NB % 8 == 0 (the K blocks
+  // walking the same bases share one XCD's L2, as fb_split_kernel's backward mode)
+  const int bk = blockIdx.x, NB = (int)gridDim.x / K;
+  int j, t0;
+  if (NB % 8 == 0) {
+    const int r = bk / 8;
+    j = r % K;
+    t0 = (r / K) * 8 + bk % 8;
+  } else {
+    j = bk % K;
+    t0 = bk / K;
+  }
+  j = __builtin_amdgcn_readfirstlane(j);
+  if (tid < S) {
+    const double *la = p.logA + ((size_t)j * S + tid) * S;
+    double mx = la[0];
+    for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
+    amax[tid] = mx;
+    lpi[tid] = p.logPi[(size_t)j * S + tid];
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int qw = lane / LPP, w = lane - qw * LPP;
+  const bool valid = qw < PPW;
+  const int q = wave * PPW + (valid ? qw : 0);
+  double *X = Xall + (size_t)q * LY::XP;
+  const int ntile = (p.i_end - p.i_begin + PPB - 1) / PPB;
+  // A' spread over the 16 lanes of every DPP row: entry e = r S + k in register e % 4
+  // of row lane e / 4 (S^2 <= 64)
+  double aq[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int e = 4 * (lane & 15) + x;
+    aq[x] = e < S * S ? p.Atg[(size_t)j * S * S + e] : 0.0;
+  }
+
+  for (int tile = t0; tile < ntile; tile += NB) {
+    const int i = p.i_begin + tile * PPB + q;
+    const bool active = valid && i < p.i_end;
+    const int ic = active ? i : p.i_begin;
+    if (valid && w == 0) F[q] = 0;
+    // ---- per-pair inputs: two columns ----
+    double Ef[2][S], Lf[2][S], arow[2][S], pb[2];
+    bool bv[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int b = w + c * LPP;
+      bv[c] = b < SB;
+      const int bc = bv[c] ? b : SB - 1;
+      const double *Ep = p.E + (size_t)j * S * p.e_ld + (size_t)(ic - p.i_buf0) * SB + bc;
+      const double *Ai = p.A + ((size_t)ic * SB + bc) * SB;
+      double rs = 0.0;
+#pragma unroll
+      for (int be = 0; be < S; ++be) {
+        const double a = Ai[be < SB ? be : SB - 1];
+        arow[c][be] = (bv[c] && be < SB) ? a : 0.0;
+        rs += arow[c][be];
+      }
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const double am = amax[k] * rs;
+        Ef[c][k] = Ep[(size_t)k * p.e_ld] + am;
+        Lf[c][k] = -am;
+      }
+      const double pr = p.prior[(size_t)ic * SB + bc];
+      pb[c] = bv[c] ? pr : 0.0;
+    }
+    bool bad = false;
+
+    // ---- K2: backward recursion, t = T-1 .. 1 ----
+    for (int t = T - 1; t >= 1; --t) {
+      double G[2][S], M[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double v[S], m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          v[k] = Ef[c][k] + Lf[c][k];
+          m = fmax(m, v[k]);
+        }
+        M[c] = m;
+#pragma unroll
+        for (int k = 0; k < S; ++k) v[k] -= m;
+        exp_tabc_n<S>(G[c], v, etab);
+      }
+      double Z[2][S];
+      // Z = A' G with A'[r][k] broadcast from lane (r S + k) / 4 of the lane's DPP row:
+      // no scalar loads, no LDS (sums in k order, as fma chains)
+#pragma unroll
+      for (int r = 0; r < S; ++r) Z[0][r] = Z[1][r] = 0.0;
+      static_for<0, S * S>([&](auto ec) {
+        constexpr int e = decltype(ec)::value, r = e / S, k = e % S;
+        dpp_fmac_bcast<e / 4>(Z[0][r], aq[e & 3], G[0][k]);
+        dpp_fmac_bcast<e / 4>(Z[1][r], aq[e & 3], G[1][k]);
+      });
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double lz[S];
+#pragma unroll
+        for (int k = 0; k < S; ++k) bad |= bv[c] && !(Z[c][k] >= kZMinB);
+        log_tabc_n<S>(lz, Z[c], ltab);
+        double sv[S];
+#pragma unroll
+        for (int k = 0; k < S; ++k) sv[k] = M[c] + lz[k];
+        if (valid) {
+          double *xc = X + (w + c * LPP) * LY::XCS;
+          if constexpr (S % 2 == 0) {
+#pragma unroll
+            for (int k = 0; k < S; k += 2)
+              *reinterpret_cast<double2 *>(xc + k) = make_double2(sv[k], sv[k + 1]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < S; ++k) xc[k] = sv[k];
+          }
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < S; ++k) Lf[0][k] = Lf[1][k] = 0.0;
+#pragma unroll
+      for (int be = 0; be < S; ++be) {
+        const double *xc = X + be * LY::XCS;
+        double xs[S];
+        if constexpr (S % 2 == 0) {
+#pragma unroll
+          for (int k = 0; k < S; k += 2) {
+            const double2 v = *reinterpret_cast<const double2 *>(__builtin_assume_aligned(xc + k, 16));
+            xs[k] = v.x;
+            xs[k + 1] = v.y;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < S; ++k) xs[k] = xc[k];
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          Lf[0][k] = fma(arow[0][be], xs[k], Lf[0][k]);
+          Lf[1][k] = fma(arow[1][be], xs[k], Lf[1][k]);
+        }
+      }
+      wave_sync();
+    }
+
+    // ---- K3: termination, L_elbo(i, j) = sum_b prior_b * log sum_s exp(lpi + E + L) ----
+    double Y[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      double v1[S], ev[S], m1 = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        v1[k] = lpi[k] + Ef[c][k] + Lf[c][k];
+        m1 = fmax(m1, v1[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < S; ++k) v1[k] -= m1;
+      exp_tabc_n<S>(ev, v1, etab);
+      double zs = 0.0;
+#pragma unroll
+      for (int k = 0; k < S; ++k) zs += ev[k];
+      double lzs[1];
+      const double zsa[1] = {zs};
+      log_tabc_n<1>(lzs, zsa, ltab);
+      Y[c] = pb[c] * (m1 + lzs[0]);
+    }
+    if (valid) {
+      X[w * LY::XCS] = Y[0];
+      X[(w + LPP) * LY::XCS] = Y[1];
+    }
+    // fallback flags, as fb_split_kernel: underflow with finite inputs -> exact
+    // kernel; non-finite cluster constants or emissions -> L_elbo NaN
+    if (bad && active) {
+      bool nf = false;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int k = 0; k < S; ++k) nf |= !isfinite(Ef[c][k]);
+      for (int x = 0; x < S; ++x) nf |= isnan(amax[x]) || isnan(lpi[x]);
+      atomicOr(&F[q], kFlagBad | (nf ? kFlagNonFinite : 0));
+    }
+    wave_sync();
+    if (active && w == 0) {
+      const size_t pair = (size_t)ic * K + j;
+      double ll = 0.0;
+      for (int be = 0; be < SB; ++be) ll += X[be * LY::XCS];
+      const int f = F[q];
+      if (f == kFlagBad) {
+        const int slot = atomicAdd(p.flag_count, 1);
+        atomicAdd(p.flag_count + 1, 1);
+        p.flag_list[slot] = (int)pair;
+        p.LL[pair] = ll;
+      } else {
+        p.LL[pair] = (f & kFlagNonFinite) ? __builtin_nan("") : ll;
+      }
+    }
+    wave_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
+size_t bwd2_lds(int S, int nwb) {
+  if (S < 1 || S > kBwd2MaxS) return 0;
+  const int LPP = (S + 1) / 2, PPW = 64 / LPP;
+  const int XCS = (S + 1) / 2 * 2 + 2, XP = 2 * LPP * XCS + 2;
+  const int off_x = (kTabD + 2 * S + 1) / 2 * 2;
+  const int ppb = nwb * PPW;
+  return ((size_t)off_x + (size_t)ppb * XP + (ppb + 1) / 2 + 1) * sizeof(double);
+}
+
+int bwd2_ppb(int S, int nwb) { return nwb * (64 / ((S + 1) / 2)); }
+
+template <int S>
+static const void *bwd2_fn() {
+  return reinterpret_cast<const void *>(&fb_bwd2_kernel<S>);
+}
+
+static const void *bwd2_fn_s(int S) {
+  switch (S) {
+    case 1: return bwd2_fn<1>();
+    case 2: return bwd2_fn<2>();
+    case 3: return bwd2_fn<3>();
+    case 4: return bwd2_fn<4>();
+    case 5: return bwd2_fn<5>();
+    case 6: return bwd2_fn<6>();
+    case 7: return bwd2_fn<7>();
+    case 8: return bwd2_fn<8>();
+    default: return nullptr;
+  }
+}
+
+int bwd2_resident_blocks(int S, int nwb, size_t lds) {
+  const void *fn = bwd2_fn_s(S);
+  return fn ? resident_per_cu(fn, nwb * 64, lds) : 1;
+}
+
+hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+  const void *fn = bwd2_fn_s(a.S);
+  if (!fn || a.SB > a.S || !a.Atg) return hipErrorInvalidValue;
+  hipError_t e = set_dyn_lds(fn, lds);
+  if (e != hipSuccess) return e;
+  switch (a.S) {
+#define VBHEM_B2(s)                                                                         \
+  case s:                                                                                   \
+    hipLaunchKernelGGL(fb_bwd2_kernel<s>, dim3(grid), dim3(a.nwb * 64), lds, st, a); \
+    break;
+    VBHEM_B2(1) VBHEM_B2(2) VBHEM_B2(3) VBHEM_B2(4) VBHEM_B2(5) VBHEM_B2(6) VBHEM_B2(7) VBHEM_B2(8)
+#undef VBHEM_B2
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace vbhem

@@ -359,4 +359,104 @@ __host__ __device__ __forceinline__ double log_tabf(double z, const double *tab)
   return y[0];
 }
 
+// ---- compact-table variants for fb_bwd2_kernel (vbhem_fb_bwd.hip) ----
+// Tables: exp 2^(j/256) hi parts [256] (8-B entries: the exp table's even
+// doubles), log {1/c, log c hi} [128][2] (16-B entries: the log table's first two
+// doubles per row) -- twice the LDS bank spread of the padded rows.
+//   exp_tabc_n: exp_tabf_n with the reduction's rounding by the 1.5*2^52 shift
+//     (n read from the low word: no conversion instruction) and the scaling by 2^k
+//     as an integer add to the exponent field (no ldexp), which needs a normal
+//     result: the argument is clamped at -700 (exp(-700) = 9.9e-305).  <= 2 ulp on
+//     [-700, 0]; x < -700 returns exp(-700).
+//   log_tabc_n: log_tabf_n with the log1p series cut after r^7 (|r| <= 2^-7 in
+//     the two intervals next to 1, 2^-8 elsewhere: the dropped terms are < 2e-18
+//     absolute).  Error <= 2 ulp + 4e-18 absolute; the
+//     absolute part is what the recursion sees (the log is added to the column
+//     maximum and summed into L, whose own rounding is >= 1e-16 for |L| >= 1).
+template <int N>
+__host__ __device__ __forceinline__ void exp_tabc_n(double (&y)[N], const double (&xin)[N],
+                                                    const double *th) {
+  constexpr double kInvLn2N = 369.3299304675746, kLn2NHi = 0x1.62e42ff000000p-9,
+                   kLn2NLo = -0x1.718432a1b0e26p-43, kShift = 0x1.8p52;
+  double r[N], t[N];
+  int k[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double x = fmax(xin[i], -700.0);
+    const double s = fma(x, kInvLn2N, kShift);
+    const double n = s - kShift;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int ni = __double2loint(s);
+#else
+    unsigned long long sb;
+    __builtin_memcpy(&sb, &s, 8);
+    const int ni = (int)(unsigned)sb;
+#endif
+    const double rr = fma(-n, kLn2NHi, x);
+    r[i] = fma(-n, kLn2NLo, rr);
+    k[i] = ni >> 8;
+    t[i] = th[ni & 255];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double q = fma(fma(r[i], 1.0 / 24.0, 1.0 / 6.0), r[i], 0.5);
+    const double p = fma(q, r[i] * r[i], r[i]);
+    const double m = fma(t[i], p, t[i]);
+#if defined(__HIP_DEVICE_COMPILE__)
+    y[i] = __hiloint2double(__double2hiint(m) + (k[i] << 20), __double2loint(m));
+#else
+    unsigned long long mb;
+    __builtin_memcpy(&mb, &m, 8);
+    mb += (unsigned long long)(long long)k[i] << 52;
+    __builtin_memcpy(&y[i], &mb, 8);
+#endif
+  }
+}
+
+template <int N>
+__host__ __device__ __forceinline__ void log_tabc_n(double (&y)[N], const double (&z)[N],
+                                                    const double *tab) {
+  constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+  double zz[N], ic[N], lc[N];
+  int k[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned hi = (unsigned)__double2hiint(z[i]);
+    const int lo = __double2loint(z[i]);
+#else
+    unsigned long long bits;
+    __builtin_memcpy(&bits, &z[i], 8);
+    const unsigned hi = (unsigned)(bits >> 32);
+    const unsigned lo = (unsigned)bits;
+#endif
+    const unsigned t = hi - 0x3fe60000u;
+    const int idx = (int)((t >> 13) & 127u);
+    k[i] = (int)t >> 20;
+#if defined(__HIP_DEVICE_COMPILE__)
+    zz[i] = __hiloint2double((int)(hi - (t & 0xfff00000u)), lo);
+    const double2 e = *reinterpret_cast<const double2 *>(__builtin_assume_aligned(tab + 2 * idx, 16));
+    ic[i] = e.x;
+    lc[i] = e.y;
+#else
+    const unsigned long long zb = ((unsigned long long)(hi - (t & 0xfff00000u)) << 32) | lo;
+    __builtin_memcpy(&zz[i], &zb, 8);
+    ic[i] = tab[2 * idx];
+    lc[i] = tab[2 * idx + 1];
+#endif
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double r = fma(zz[i], ic[i], -1.0);
+    const double w = fma((double)k[i], kLn2, lc[i]);
+    const double r2 = r * r;
+    double q = fma(r, 1.0 / 7.0, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -1.0 / 4.0);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    y[i] = fma(q, r2, r) + w;
+  }
+}
+
 }  // namespace vbhem

@@ -141,11 +141,12 @@ def mathcheck():
     lib.logtab_host.restype = None
     lib.logtab_device.argtypes = [ctypes.c_int, dp, dp, dp]
     lib.logtab_device.restype = ctypes.c_int
-    for name in ("logtabf_host",):
+    for name in ("logtabf_host", "logtabc_host"):
         getattr(lib, name).argtypes = [ctypes.c_int, dp, dp, dp]
         getattr(lib, name).restype = None
-    lib.logtabf_device.argtypes = [ctypes.c_int, dp, dp, dp]
-    lib.logtabf_device.restype = ctypes.c_int
+    for name in ("logtabf_device", "logtabc_device"):
+        getattr(lib, name).argtypes = [ctypes.c_int, dp, dp, dp]
+        getattr(lib, name).restype = ctypes.c_int
     return lib
 
 

@@ -13,7 +13,42 @@ __device__ const double kLogTabDev[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT
 static const double kExpTabHost[vbhem::kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
 __device__ const double kExpTabDev[vbhem::kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
 
+// compact tables of exp_tabc_n / log_tabc_n (as fb_bwd2_kernel stages them)
+struct CompactTabs {
+  double e[vbhem::kExpTabEntries];
+  double l[2 * vbhem::kLogTabEntries];
+};
+static CompactTabs compact_host() {
+  CompactTabs c;
+  for (int j = 0; j < vbhem::kExpTabEntries; ++j) c.e[j] = kExpTabHost[2 * j];
+  for (int j = 0; j < vbhem::kLogTabEntries; ++j) {
+    c.l[2 * j] = kLogTabHost[4 * j];
+    c.l[2 * j + 1] = kLogTabHost[4 * j + 1];
+  }
+  return c;
+}
+
 namespace {
+
+__global__ void logtabc_kernel(int n, const double* __restrict__ x, double* __restrict__ l,
+                               double* __restrict__ e) {
+  __shared__ __attribute__((aligned(16))) double lt[2 * vbhem::kLogTabEntries];
+  __shared__ __attribute__((aligned(16))) double et[vbhem::kExpTabEntries];
+  for (int k = threadIdx.x; k < vbhem::kExpTabEntries; k += blockDim.x) et[k] = kExpTabDev[2 * k];
+  for (int k = threadIdx.x; k < vbhem::kLogTabEntries; k += blockDim.x) {
+    lt[2 * k] = kLogTabDev[4 * k];
+    lt[2 * k + 1] = kLogTabDev[4 * k + 1];
+  }
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    double y[1], z[1] = {x[i]}, m[1] = {-x[i]};
+    vbhem::log_tabc_n<1>(y, z, lt);
+    l[i] = y[0];
+    vbhem::exp_tabc_n<1>(y, m, et);
+    e[i] = y[0];
+  }
+}
 
 __global__ void math_kernel(int n, const double* __restrict__ x, double* __restrict__ e,
                             double* __restrict__ l, double* __restrict__ r) {
@@ -73,6 +108,18 @@ void logtabf_host(int n, const double* x, double* l, double* e) {
   }
 }
 
+// compact-table pair of fb_bwd2_kernel: log at x, exp at -x
+void logtabc_host(int n, const double* x, double* l, double* e) {
+  static const CompactTabs c = compact_host();
+  for (int i = 0; i < n; i++) {
+    double y[1], z[1] = {x[i]}, m[1] = {-x[i]};
+    vbhem::log_tabc_n<1>(y, z, c.l);
+    l[i] = y[0];
+    vbhem::exp_tabc_n<1>(y, m, c.e);
+    e[i] = y[0];
+  }
+}
+
 static int logtab_device_impl(int n, const double* x, double* l, double* e, int fast) {
   double *dx = nullptr, *dl = nullptr, *de = nullptr;
   const size_t bytes = sizeof(double) * (size_t)(n > 0 ? n : 1);
@@ -81,7 +128,8 @@ static int logtab_device_impl(int n, const double* x, double* l, double* e, int 
   if (st == hipSuccess) st = hipMalloc(&de, bytes);
   if (st == hipSuccess) st = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
   if (st == hipSuccess && n > 0) {
-    logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de, fast);
+    if (fast == 2) logtabc_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
+    else logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de, fast);
     st = hipGetLastError();
   }
   if (st == hipSuccess) st = hipMemcpy(l, dl, sizeof(double) * n, hipMemcpyDeviceToHost);
@@ -98,6 +146,10 @@ int logtab_device(int n, const double* x, double* l, double* e) {
 
 int logtabf_device(int n, const double* x, double* l, double* e) {
   return logtab_device_impl(n, x, l, e, 1);
+}
+
+int logtabc_device(int n, const double* x, double* l, double* e) {
+  return logtab_device_impl(n, x, l, e, 2);
 }
 
 // Same on device 0 (host arrays in/out).  Returns 0 or a hipError_t.

@@ -107,3 +107,32 @@ def test_logtabf_host_build(mathcheck):
 @pytest.mark.gpu
 def test_logtabf_device_build(mathcheck):
     assert _check_logtabf(mathcheck.logtabf_device) == 0
+
+
+def _check_logtabc(fn):
+    """Compact-table pair of fb_bwd2_kernel (log_tabc_n / exp_tabc_n): log within
+    2 ulp + 4e-18 absolute (series cut after r^7), exp <= 2 ulp on [-700, 0] and
+    exp(-700) below it (clamped so the exponent add stays normal)."""
+    x = _samples()
+    x = np.concatenate([x, np.random.default_rng(7).uniform(0.99, 1.01, N // 4),
+                        [700.0, 745.0, 800.0, 1e4]])
+    dp = ctypes.POINTER(ctypes.c_double)
+    l, e = np.zeros_like(x), np.zeros_like(x)
+    rc = fn(len(x), x.ctypes.data_as(dp), l.ctypes.data_as(dp), e.ctypes.data_as(dp))
+    pos = x >= 1e-200
+    ref = np.log(x[pos])
+    assert (np.abs(l[pos] - ref) <= 2.0 * np.spacing(np.abs(ref)) + 4e-18).all()
+    assert l[2] == 0.0
+    m = x <= 700
+    assert _ulps(e[m], np.exp(-x[m])).max() <= 2.0
+    assert (e[x >= 700] == e[x == 700.0][0]).all() and e[x == 700.0][0] > 0
+    return rc
+
+
+def test_logtabc_host_build(mathcheck):
+    _check_logtabc(mathcheck.logtabc_host)
+
+
+@pytest.mark.gpu
+def test_logtabc_device_build(mathcheck):
+    assert _check_logtabc(mathcheck.logtabc_device) == 0
