@@ -23,6 +23,10 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 dense (vector and matrix), AMD spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# sustained v_fma_f64 throughput measured on MI355X by scripts/ubench_valu.hip (4 waves
+# per SIMD, 8 independent chains, 40,000 iterations): 2.40 ns per wave-instruction per
+# SIMD = 54.6 TF/s (profiles/r02_ubench_valu.txt)
+ACHIEVABLE_FP64_VALU_TFLOPS = 54.6
 METRIC = ("VBHEM E-steps/sec (whole node), N baseHMMs × K clusters × S states; "
           "ELBO match")
 
@@ -219,7 +223,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     _capi.timing_read()  # drop warmup records
-    _capi.timing_enable(True)
+    # inside the timed region only the fb launches are timed (two HIP events per
+    # E-step on the launch stream: the roofline's kernel); the per-kernel breakdown
+    # comes from a separate instrumented pass below
+    _capi.timing_enable(True, fb_only=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         stats = step()
@@ -234,6 +241,15 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
     tk = _capi.timing_read()
+    # per-kernel breakdown (emission, gated forward, statistics): a few more E-steps
+    # with every launch timed (not part of `value`)
+    bd_steps = max(1, min(args.steps, 5))
+    _capi.timing_enable(True)
+    for _ in range(bd_steps):
+        step()
+    torch.cuda.synchronize()
+    tkb = _capi.timing_read()
+    _capi.timing_enable(False)
     # fraction of pairs the gate Z > 1e-8 keeps (the gated schedule's second pass)
     zk = (eng.hatZ * tN.view(-1, 1)) > 1e-8
     n_gated = int(zk.sum().item())
@@ -288,10 +304,13 @@ def main():
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
     lpc = 1 if S <= 4 else 2 if S <= 8 else 4      # split_lpc (dense / list modes)
     lpc_bwd = 1 if S <= 8 else 2                    # split_lpc_bwd (backward mode)
-    kname = (f"vbhem::fb_split_kernel<{S}, {lpc_bwd if gated else lpc}, {1 if gated else 0}>"
-             if split else "vbhem::fb_pairs_kernel")
+    if gated and S <= 8 and not os.environ.get("VBHEM_NO_BWD2"):
+        kname = f"vbhem::fb_bwd2_kernel<{S}>"
+    else:
+        kname = (f"vbhem::fb_split_kernel<{S}, {lpc_bwd if gated else lpc}, {1 if gated else 0}>"
+                 if split else "vbhem::fb_pairs_kernel")
     traffic, traffic_src = committed_traffic(args.config, N, world, kname)
-    gf_ms = tk["gated_fwd_ms"] / max(1, tk["gated_fwd_launches"])
+    gf_ms = tkb["gated_fwd_ms"] / max(1, tkb["gated_fwd_launches"])
     res = {
         "metric": METRIC,
         "value": args.steps / dt,
@@ -317,6 +336,8 @@ def main():
             "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP64_TFLOPS,
+            "achievable_peak": ACHIEVABLE_FP64_VALU_TFLOPS,
+            "frac_of_achievable": achieved / ACHIEVABLE_FP64_VALU_TFLOPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
             "kernel": kname,
@@ -325,7 +346,9 @@ def main():
             "pairs_per_launch": pairs_per_launch,
             "note": ("fp64 VALU-bound (software exp/log + contractions on the vector ALU); "
                      "peak = MI355X FP64 dense "
-                     "78.6 TF/s (vector = matrix rate); flops counted on the reference "
+                     "78.6 TF/s (vector = matrix rate); achievable_peak = the sustained "
+                     "v_fma_f64 rate measured on this chip by scripts/ubench_valu.hip "
+                     "(4 waves/SIMD, independent chains); flops counted on the reference "
                      "recurrences this kernel runs (" + ("K2 backward + K3 termination, every "
                      "pair" if gated else "K2-K4") + "), excluding exp/log"),
             "hbm": {"algorithmic_bytes_per_launch": bpp * pairs_per_launch,
@@ -349,8 +372,9 @@ def main():
                            / max(gf_ms * 1e-3, 1e-12) / 1e12} if gated else None),
         "dense_schedule": {"value": dense_steps / float(dtd.item()), "unit": "E-steps/s",
                            "steps": dense_steps, "max_rel_diff_vs_gated": dense_rel},
-        "emission_kernel_ms": tk["em_ms"] / max(1, tk["em_launches"]),
-        "stats_kernels_ms_per_step": tk["stats_ms"] / args.steps,
+        "emission_kernel_ms": tkb["em_ms"] / max(1, tkb["em_launches"]),
+        "stats_kernels_ms_per_step": tkb["stats_ms"] / bd_steps,
+        "breakdown_steps": bd_steps,
         "reference_equivalent_tflops_per_s": flops_per_pair(S, Sb, d, T, cov) * N * K * args.steps / dt / 1e12,
         "host_mstep_ms": host_ms,
         "elbo": L,

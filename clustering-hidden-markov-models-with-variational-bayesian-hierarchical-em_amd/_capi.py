@@ -145,8 +145,10 @@ def ptr(t) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
-def timing_enable(on: bool = True) -> None:
-    lib().vbhem_timing_enable(1 if on else 0)
+def timing_enable(on: bool = True, fb_only: bool = False) -> None:
+    """Kernel timing on this thread: every timed launch, or (fb_only) the fb
+    launches alone (two events per E-step)."""
+    lib().vbhem_timing_enable((2 if fb_only else 1) if on else 0)
 
 
 def timing_read() -> dict:

@@ -31,10 +31,19 @@ thread_local std::string g_err;
 // recorded into a stream that is being captured into a graph: a captured event
 // would be destroyed by the next vbhem_timing_read while the graph still
 // records into it on every replay.
+// Levels: 1 every timed launch (fb, emission, statistics, gated forward), 2 the fb
+// launches only -- two events per E-step, so the instrumentation costs the timed
+// region next to nothing (each recorded event is a marker packet the queue
+// processes between kernels; a dozen per step was ~40 us at N = 12,500).  Events
+// are recycled through a per-thread pool (no create/destroy per launch).
 struct TimingState {
-  bool on = false;
+  int level = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em, gf;
   std::vector<long long> fb_pairs;
+  std::vector<hipEvent_t> pool;
+  ~TimingState() {
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+  }
 };
 thread_local TimingState g_timing;
 
@@ -48,8 +57,8 @@ thread_local int g_fused_mode = default_fused_mode();
 
 // timing is recorded for this launch: enabled on this thread and the stream
 // is not capturing
-bool timing_on(hipStream_t st) {
-  if (!g_timing.on) return false;
+bool timing_on(hipStream_t st, bool fb_launch = false) {
+  if (g_timing.level == 0 || (g_timing.level == 2 && !fb_launch)) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
   return cs == hipStreamCaptureStatusNone;
@@ -57,9 +66,17 @@ bool timing_on(hipStream_t st) {
 
 hipEvent_t timing_event(hipStream_t st) {
   hipEvent_t ev = nullptr;
-  if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+  if (!g_timing.pool.empty()) {
+    ev = g_timing.pool.back();
+    g_timing.pool.pop_back();
+  } else if (hipEventCreate(&ev) != hipSuccess) {
+    return nullptr;
+  }
   (void)hipEventRecord(ev, st);
   return ev;
+}
+void timing_recycle(hipEvent_t ev) {
+  if (ev) g_timing.pool.push_back(ev);
 }
 
 int fail(int code, const std::string &msg) {
@@ -431,7 +448,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     if (e != hipSuccess) return hip_fail(e, "emission_kernel");
     if (em0) g_timing.em.emplace_back(em0, timing_event(st));
   }
-  hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
+  hipEvent_t ev0 = timing_on(st, true) ? timing_event(st) : nullptr;
   if (c.split.ok) {
     const SplitPlan &sp = mode == vbhem::kFbBackward ? c.bwd : c.split;
     vbhem::SplitArgs ca = sp.a;
@@ -694,7 +711,7 @@ int vbhem_set_fused_mode(int mode) {
 }
 
 int vbhem_timing_enable(int on) {
-  g_timing.on = on != 0;
+  g_timing.level = (on == 1 || on == 2) ? on : 0;
   return VBHEM_OK;
 }
 
@@ -712,8 +729,8 @@ int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs
         if (e != hipSuccess) rc = hip_fail(e, "vbhem_timing_read");
         acc += ms;
       }
-      if (pr.first) (void)hipEventDestroy(pr.first);
-      if (pr.second) (void)hipEventDestroy(pr.second);
+      timing_recycle(pr.first);
+      timing_recycle(pr.second);
     }
   };
   const long long nf = (long long)g_timing.fb.size(), ns = (long long)g_timing.stats.size();
@@ -744,8 +761,8 @@ static int drain_events(std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, doubl
       if (e != hipSuccess) rc = hip_fail(e, where);
       t += ms;
     }
-    if (pr.first) (void)hipEventDestroy(pr.first);
-    if (pr.second) (void)hipEventDestroy(pr.second);
+    timing_recycle(pr.first);
+    timing_recycle(pr.second);
   }
   v.clear();
   if (ms_out) *ms_out = t;
@@ -769,8 +786,8 @@ int vbhem_timing_read_emission(double *em_ms, long long *em_launches) {
       if (e != hipSuccess) rc = hip_fail(e, "vbhem_timing_read_emission");
       t += ms;
     }
-    if (pr.first) (void)hipEventDestroy(pr.first);
-    if (pr.second) (void)hipEventDestroy(pr.second);
+    timing_recycle(pr.first);
+    timing_recycle(pr.second);
   }
   g_timing.em.clear();
   if (em_ms) *em_ms = t;

@@ -62,6 +62,17 @@ __device__ __forceinline__ void dpp_fmac_bcast(double &acc, double a, double b) 
       : "v"(a), "v"(b), "i"(N));
 }
 
+// max of v[0..N) as a balanced tree (dependency depth log2 N instead of N - 1)
+template <int N, int O = 0>
+__device__ __forceinline__ double tree_max_at(const double *v) {
+  if constexpr (N == 1) return v[O];
+  else return fmax(tree_max_at<N / 2, O>(v), tree_max_at<N - N / 2, O + N / 2>(v));
+}
+template <int N>
+__device__ __forceinline__ double tree_max(const double (&v)[N]) {
+  return tree_max_at<N>(v);
+}
+
 // f(integral_constant<int, I>) for I = B .. E-1, in order
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f) {
@@ -186,12 +197,10 @@ void fb_bwd2_kernel(const SplitArgs p) {
       double G[2][S], M[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        double v[S], m = -INFINITY;
+        double v[S];
 #pragma unroll
-        for (int k = 0; k < S; ++k) {
-          v[k] = Ef[c][k] + Lf[c][k];
-          m = fmax(m, v[k]);
-        }
+        for (int k = 0; k < S; ++k) v[k] = Ef[c][k] + Lf[c][k];
+        const double m = tree_max<S>(v);
         M[c] = m;
 #pragma unroll
         for (int k = 0; k < S; ++k) v[k] -= m;

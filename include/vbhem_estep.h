@@ -197,11 +197,14 @@ int vbhem_set_fused_mode(int mode);
 int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
 
 /* Kernel timing for benchmarking/profiling, per host thread: while enabled,
- * hipEvents are recorded on the launch stream around every fb / stats kernel
- * launch of this thread (never into a stream that is capturing a graph: such
- * launches are simply not timed).  vbhem_timing_read
- * synchronises on them, returns the summed elapsed milliseconds, the launch
- * counts and the number of (i,j) pairs the fb launches covered, and resets. */
+ * hipEvents are recorded on the launch stream around the kernel launches of this
+ * thread (never into a stream that is capturing a graph: such launches are simply
+ * not timed).  on = 1: every fb / emission / stats / gated-forward launch; on = 2:
+ * the fb (backward or dense) launches only -- two events per E-step, for timing
+ * the dominant kernel inside a timed region at negligible cost; 0: off.
+ * vbhem_timing_read synchronises on them, returns the summed elapsed
+ * milliseconds, the launch counts and the number of (i,j) pairs the fb launches
+ * covered, and resets. */
 int vbhem_timing_enable(int on);
 int vbhem_timing_read(double *fb_ms, long long *fb_launches, long long *fb_pairs,
                       double *stats_ms, long long *stats_launches);
