@@ -24,7 +24,8 @@ _c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
 
 class BaseT(ctypes.Structure):
     _fields_ = [("N", _c_int), ("SB", _c_int), ("d", _c_int), ("covmode", _c_int),
-                ("nstates", _vp), ("prior", _vp), ("A", _vp), ("centres", _vp), ("covars", _vp)]
+                ("nstates", _vp), ("prior", _vp), ("A", _vp), ("centres", _vp), ("covars", _vp),
+                ("U", _vp)]
 
 
 class ClusterT(ctypes.Structure):
@@ -58,6 +59,8 @@ class HmmParamsT(ctypes.Structure):  # include/vbhmm_fb.h vbhmm_params_t
 ALLREDUCE_FN = ctypes.CFUNCTYPE(_c_int, _vp, _c_size, _vp, _vp)
 
 EXPORTS = {
+    "vbhem_prepare_base_bytes": (_c_size, [ctypes.POINTER(BaseT)]),
+    "vbhem_prepare_base": (_c_int, [ctypes.POINTER(BaseT), _vp, _c_size, _vp]),
     "vbhem_pairs_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int]),
     "vbhem_estep_pairs": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),

@@ -258,11 +258,19 @@ struct Carver {
   }
 };
 
+// emission_u_kernel applies (k-steps <= kUMaxKq): the per-call operand U is needed
+// unless the caller prepared one (base->U)
+bool u_gemm_ok(const vbhem_base_t *b) {
+  return vbhem::emission_kdp(b->d, b->covmode) / 4 <= vbhem::kUMaxKq && !std::getenv("VBHEM_NO_UGEMM");
+}
+bool need_u_ws(const vbhem_base_t *b) { return !b->U && u_gemm_ok(b); }
+
 struct PairsWs {
   int *flags;  // [0]=count [1]=total [2..] list
   double *scratch;
   double *tnu;
   double *E, *W, *bias, *shift;  // emission GEMM (split path)
+  double *U;                     // the GEMM's base-set operand, built per call (null: prepared)
 };
 
 inline size_t emission_w_doubles(int d, int covmode, int K, int S) {
@@ -280,6 +288,9 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.W = cv.take<double>(emission_w_doubles(b->d, b->covmode, c->K, c->S));
   w.bias = cv.take<double>((size_t)vbhem::emission_ksp(c->K * c->S));
   w.shift = cv.take<double>((size_t)b->d);
+  w.U = need_u_ws(b) ? cv.take<double>(vbhem::u_doubles((long long)b->N * b->SB + 16, b->d,
+                                                         b->covmode))
+                     : nullptr;
   return cv.off + 256;
 }
 
@@ -292,6 +303,7 @@ struct FusedWs {
   double *Atg;                      // gated schedule: [K][S][S] A' for the backward pass
   double *scratch, *nu1, *xi, *tnu, *Z, *slabs;
   double *E, *W, *bias, *shift;
+  double *U;                        // per-call operand of the emission GEMM (null: prepared)
 };
 
 size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, int T, FusedWs &w,
@@ -319,6 +331,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.W = cv.take<double>(emission_w_doubles(b->d, b->covmode, K, S));
   w.bias = cv.take<double>((size_t)vbhem::emission_ksp(K * S));
   w.shift = cv.take<double>((size_t)b->d);
+  w.U = need_u_ws(b) ? cv.take<double>(vbhem::u_doubles((long long)g * SB + 16, b->d, b->covmode))
+                     : nullptr;
   w.gate_cnt = cv.take<int>((size_t)w.nslab * K);
   w.list = cv.take<int>(g * K);
   w.list_tot = cv.take<int>((size_t)K);
@@ -335,6 +349,11 @@ struct FbCtx {
   int bwd2_ppb = 0;
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
+  // emission_u_kernel: on the prepared operand (base->U) or one built per call in u_ws
+  bool use_u = false;
+  size_t em_lds_u = 0;
+  const vbhem_base_t *base = nullptr;
+  double *u_ws = nullptr;
 };
 
 int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T,
@@ -349,7 +368,12 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
     e.smooth = smooth;
     e.centres = b->centres; e.covars = b->covars; e.m = cl->m; e.P = cl->P; e.c = cl->c;
     if (!vbhem::plan_emission(e, c.em_lds)) c.split.ok = false;
+    if (c.split.ok && u_gemm_ok(b) && vbhem::plan_emission_u(e, c.em_lds_u)) {
+      c.use_u = true;
+      e.zfix = b->U;  // a prepared operand carries its shift in its head
+    }
   }
+  c.base = b;
   const bool have_elems = plan_fb(b->SB, b->d, b->covmode, cl->K, cl->S, T, c.plan);
   if (!c.split.ok && !have_elems)
     return fail(VBHEM_ERR_UNSUPPORTED,
@@ -443,8 +467,29 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   if (c.split.ok) {
     vbhem::EmissionArgs ea = c.em;
     ea.i_begin = i_begin; ea.i_end = i_end; ea.i_buf0 = i_buf0; ea.E = Ebuf; ea.e_ld = e_ld;
+    size_t em_lds = c.em_lds;
     hipEvent_t em0 = timing_on(st) ? timing_event(st) : nullptr;
-    e = vbhem::launch_emission(ea, c.em_lds, st);
+    if (c.use_u) {
+      em_lds = c.em_lds_u;
+      if (c.base->U) {
+        ea.U = c.base->U;
+        ea.u_col0 = 0;
+      } else {  // this call's operand for bases [i_begin, i_end), shifted like W' / bias'
+        if (!c.u_ws) return fail(VBHEM_ERR_WORKSPACE, "no operand buffer for the emission GEMM");
+        const vbhem_base_t *b = c.base;
+        vbhem::UPrepArgs ua{};
+        ua.N = b->N; ua.SB = b->SB; ua.d = b->d; ua.covmode = b->covmode;
+        ua.kdp = c.em.kdp; ua.i_begin = i_begin; ua.i_end = i_end;
+        ua.u_col0 = (long long)i_begin * b->SB / 16 * 16;
+        ua.nstates = b->nstates; ua.centres = b->centres; ua.covars = b->covars;
+        ua.U = c.u_ws; ua.z = c.em.shift;
+        e = vbhem::launch_u_prep(ua, st);
+        if (e != hipSuccess) return hip_fail(e, "u_prep_kernel");
+        ea.U = c.u_ws;
+        ea.u_col0 = ua.u_col0;
+      }
+    }
+    e = vbhem::launch_emission(ea, em_lds, st);
     if (e != hipSuccess) return hip_fail(e, "emission_kernel");
     if (em0) g_timing.em.emplace_back(em0, timing_event(st));
   }
@@ -509,6 +554,33 @@ size_t vbhem_stats_len(int K, int S, int d, int covmode) {
   return (size_t)K + (size_t)K * S + (size_t)K * S * S + 2 + (size_t)K * S * vbhem_stats_nu(d, covmode);
 }
 
+size_t vbhem_prepare_base_bytes(const vbhem_base_t *base) {
+  if (!base || base->N < 0 || base->SB < 1 || base->d < 1 || base->d > vbhem::kUHead ||
+      (base->covmode != VBHEM_COV_DIAG && base->covmode != VBHEM_COV_FULL))
+    return 0;
+  if (vbhem::emission_kdp(base->d, base->covmode) / 4 > vbhem::kUMaxKq) return 0;
+  return vbhem::u_doubles((long long)base->N * base->SB, base->d, base->covmode) * sizeof(double);
+}
+
+int vbhem_prepare_base(const vbhem_base_t *base, double *U_dev, size_t bytes, void *stream) {
+  const size_t need = vbhem_prepare_base_bytes(base);
+  if (need == 0)
+    return fail(VBHEM_ERR_UNSUPPORTED, "vbhem_prepare_base: invalid descriptor or d too large");
+  if (!U_dev || bytes < need)
+    return fail(VBHEM_ERR_WORKSPACE, "vbhem_prepare_base: need " + std::to_string(need) + " bytes");
+  if (base->N > 0 && (!base->centres || !base->covars))
+    return fail(VBHEM_ERR_ARG, "vbhem_prepare_base: null base array");
+  vbhem::UPrepArgs ua{};
+  ua.N = base->N; ua.SB = base->SB; ua.d = base->d; ua.covmode = base->covmode;
+  ua.kdp = vbhem::emission_kdp(base->d, base->covmode);
+  ua.i_begin = 0; ua.i_end = base->N; ua.u_col0 = 0;
+  ua.nstates = base->nstates; ua.centres = base->centres; ua.covars = base->covars;
+  ua.U = U_dev; ua.z = nullptr;  // shift = mean of the valid base means
+  hipError_t e = vbhem::launch_u_prep(ua, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "u_prep_kernel");
+  return VBHEM_OK;
+}
+
 size_t vbhem_pairs_workspace_bytes(const vbhem_base_t *base, const vbhem_cluster_t *clus, int T) {
   if (check_inputs(base, clus, T, false) != VBHEM_OK) return 0;
   PairsWs w;
@@ -541,6 +613,7 @@ int estep_pairs_impl(const vbhem_base_t *base, const vbhem_cluster_t *clus, int 
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T, smooth);
   if (rc != VBHEM_OK) return rc;
+  ctx.u_ws = w.U;
   if (!ctx.split.ok) {
     hipError_t e0 = hipMemsetAsync(w.flags, 0, vbhem::kFlagHead * sizeof(int), st);
     if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
@@ -642,6 +715,7 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   FbCtx ctx;
   rc = prepare_fb(ctx, base, clus, T);
   if (rc != VBHEM_OK) return rc;
+  ctx.u_ws = w.U;
   // gated schedule: split kernel + list statistics tile must apply
   size_t sl_lds = 0;
   const bool gated = g_fused_mode == VBHEM_FUSED_GATED && ctx.split.ok &&
@@ -843,6 +917,7 @@ int estep_pairs_host_impl(int device, const vbhem_base_t *bh, const vbhem_cluste
   vbhem_base_t bd = *bh;
   vbhem_cluster_t cd = *ch;
   bd.nstates = nullptr;
+  bd.U = nullptr;  // host entry point: the call builds its own operand
   bd.prior = d_in[0]; bd.A = d_in[1]; bd.centres = d_in[2]; bd.covars = d_in[3];
   cd.logA = d_in[4]; cd.logPi = d_in[5]; cd.m = d_in[6]; cd.P = d_in[7]; cd.c = d_in[8];
   size_t wsb = 0;
@@ -899,6 +974,7 @@ struct vbhem_ctx {
   double *prior = nullptr, *A = nullptr, *centres = nullptr, *covars = nullptr;
   double *logA = nullptr, *logPi = nullptr, *m = nullptr, *P = nullptr, *c = nullptr;
   double *tildeN = nullptr, *logOmega = nullptr, *stats = nullptr, *hatZ = nullptr, *LL = nullptr;
+  double *U = nullptr;  // the prepared operand of the emission GEMM (vbhem_prepare_base), or null
   void *ws = nullptr;
 };
 
@@ -909,7 +985,7 @@ void ctx_free(vbhem_ctx *x) {
   int prev = 0;
   const bool dev_ok = hipGetDevice(&prev) == hipSuccess && hipSetDevice(x->device) == hipSuccess;
   void *ptrs[] = {x->nstates, x->prior, x->A, x->centres, x->covars, x->logA, x->logPi, x->m,
-                  x->P, x->c, x->tildeN, x->logOmega, x->stats, x->hatZ, x->LL, x->ws};
+                  x->P, x->c, x->tildeN, x->logOmega, x->stats, x->hatZ, x->LL, x->U, x->ws};
   for (void *q : ptrs)
     if (q) (void)hipFree(q);
   if (x->stream) (void)hipStreamDestroy(x->stream);
@@ -975,7 +1051,15 @@ int vbhem_ctx_create(int device, const vbhem_base_t *bh, int K, int S, int R, in
     if (e != hipSuccess) { ctx_free(x); return hip_fail(e, "vbhem_ctx_create(upload)"); }
   }
   vbhem_base_t bd{bh->N, bh->SB, bh->d, bh->covmode, x->nstates, x->prior, x->A, x->centres,
-                  x->covars};
+                  x->covars, nullptr};
+  // the base set stays resident: its emission-GEMM operand is built once, here
+  if (const size_t ub = vbhem_prepare_base_bytes(&bd)) {
+    e = hipMalloc(&x->U, ub);
+    if (e != hipSuccess) { ctx_free(x); return hip_fail(e, "vbhem_ctx_create(U)"); }
+    rc = vbhem_prepare_base(&bd, x->U, ub, x->stream);
+    if (rc != VBHEM_OK) { ctx_free(x); return rc; }
+    bd.U = x->U;
+  }
   vbhem_cluster_t cd{K, S, x->logA, x->logPi, x->m, x->P, x->c};
   x->ws_bytes = vbhem_fused_trials_workspace_bytes(&bd, &cd, R, T);
   if (x->ws_bytes == 0) { ctx_free(x); return fail(VBHEM_ERR_ARG, "vbhem_ctx_create: bad sizes"); }
@@ -1009,7 +1093,7 @@ int vbhem_ctx_fused(vbhem_ctx_t *x, const vbhem_cluster_t *ch, const double *til
     e = hipMemcpyAsync(x->tildeN, tildeN_host, N * 8, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return hip_fail(e, "vbhem_ctx_fused(upload)");
   vbhem_base_t bd{x->N, x->SB, x->d, x->covmode, x->nstates, x->prior, x->A, x->centres,
-                  x->covars};
+                  x->covars, x->U};
   vbhem_cluster_t cd{x->K, x->S, x->logA, x->logPi, x->m, x->P, x->c};
   int rc = vbhem_estep_fused_trials(&bd, &cd, x->R, x->T, x->tildeN, x->logOmega, x->stats,
                                     x->hatZ, x->LL, x->ws, x->ws_bytes, st);

@@ -73,7 +73,12 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
   // finite means count: a diverged cluster (NaN constants, e.g. one trial of a
   // batched launch) must not poison the shift, and so every other cluster's E.
   const int NP = kPrepThreads / d, part = tid / d, a0 = tid - part * d;
-  if (part < NP) {
+  if (p.zfix) {  // the shift the prepared operand U was built with
+    for (int a = tid; a < d; a += kPrepThreads) {
+      zs[a] = p.zfix[a];
+      if (r == 0) p.shift[a] = zs[a];
+    }
+  } else if (part < NP) {
     double s = 0.0, n = 0.0;
     for (int q = part; q < KS; q += NP) {
       const double v = p.m[(size_t)q * d + a0];
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
     pm[tid] = n;
   }
   __syncthreads();
-  for (int a = tid; a < d; a += kPrepThreads) {
+  for (int a = tid; a < d && !p.zfix; a += kPrepThreads) {
     double s = 0.0, n = 0.0;
     for (int q = 0; q < NP; ++q) {
       s += zp[q * d + a];
@@ -95,8 +100,7 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
     zs[a] = n > 0.0 ? s / n : 0.0;
     if (r == 0) p.shift[a] = zs[a];
   }
-  __syncthreads();  // pm is reused below
-  __syncthreads();
+  __syncthreads();  // zs published; pm is reused below
   // W' = -W/2 and bias' = -bias/2 (exact scalings), so E = bias' + sum W' U;
   // rows r >= K*S and k-rows e >= KD are the zero padding of the [kdp][ksp] layout
   const int KSP = p.ksp;
@@ -418,6 +422,223 @@ __global__ __launch_bounds__(kEmMaxThreads) void emission_gen_kernel(EmissionArg
 }
 
 // ---------------------------------------------------------------------------
+// The prepared operand U (vbhem_prepare_base, or per call for the bases a call
+// processes) and the GEMM on it.
+//
+// u_shift_kernel: z = mean of the centres of every valid base state (i, b < nstates[i])
+//   of [0, N): phase 0 -- block q sums a fixed contiguous column range; phase 1 -- one
+//   block adds the partials in block order (fixed order: bit-reproducible).
+// u_prep_kernel: one block per column tile writes the tile's kq * 64 doubles in MFMA
+//   B-operand lane order (vbhem_internal.h, kUHead):
+//   full: u(e, col) = Sigma_ab + Sigma_ba + 2 mu'_a mu'_b (a < b) | Sigma_aa + mu'_a^2 (e < NPF),
+//         mu'_(e - NPF) (e < NPF + d);   diag: Sigma_e + mu'_e^2 | mu'_(e - d);   mu' = mu - z.
+// emission_u_kernel<KQB, RC>: E = bias' + W'^T U, persistent over rounds of one 16-column
+//   tile per wavefront: the tile's U (kq <= KQB doubles per lane) is loaded once into
+//   registers (coalesced: 512 B per k-step); W' is staged in LDS in A-operand lane order,
+//   RC row tiles (16 rows each) per chunk -- once per block when every row fits one chunk
+//   (K*S <= 128 at kq <= 12), else chunk by chunk per round; accumulators start at bias'.
+//   Nothing of the base set is recomputed per cluster row chunk, W' is never read from L2
+//   per k-step (the raw/generic kernels' costs at d > 8).
+// ---------------------------------------------------------------------------
+constexpr int kUShiftBlocks = 256;
+constexpr int kUThreads = 256;
+
+__global__ __launch_bounds__(kUThreads) void u_shift_kernel(UPrepArgs p, int phase, int nblk) {
+  __shared__ double sp[kUThreads], sn[kUThreads];
+  const int tid = threadIdx.x, d = p.d;
+  const int P = kUThreads / d, part = tid / d, a = tid - part * d;
+  double *partial = p.U + kUHead;  // [nblk][d + 1] (the tile area, rewritten later)
+  double s = 0.0, n = 0.0;
+  if (phase == 0) {
+    const long long ncol = (long long)p.N * p.SB;
+    const long long per = (ncol + gridDim.x - 1) / gridDim.x;
+    const long long c0 = (long long)blockIdx.x * per, c1 = min(ncol, c0 + per);
+    if (part < P) {
+      for (long long col = c0 + part; col < c1; col += P) {
+        const int i = (int)(col / p.SB), b = (int)(col - (long long)i * p.SB);
+        const int ns = p.nstates ? p.nstates[i] : p.SB;
+        if (b < ns) {
+          s += p.centres[col * d + a];
+          n += 1.0;
+        }
+      }
+    }
+  } else if (part < P) {
+    for (int q = part; q < nblk; q += P) {
+      s += partial[(size_t)q * (d + 1) + a];
+      n += (a == 0) ? partial[(size_t)q * (d + 1) + d] : 0.0;
+    }
+  }
+  sp[tid] = s;
+  sn[tid] = n;
+  __syncthreads();
+  if (tid < d) {
+    double ss = 0.0, nn = 0.0;
+    for (int q = 0; q < P; ++q) {
+      ss += sp[q * d + tid];
+      nn += sn[q * d + (phase == 0 ? tid : 0)];
+    }
+    if (phase == 0) {
+      partial[(size_t)blockIdx.x * (d + 1) + tid] = ss;
+      if (tid == 0) partial[(size_t)blockIdx.x * (d + 1) + d] = nn;
+    } else {
+      p.U[tid] = nn > 0.0 ? ss / nn : 0.0;
+    }
+  }
+  if (phase == 1)
+    for (int x = d + tid; x < kUHead; x += kUThreads) p.U[x] = 0.0;
+}
+
+__global__ __launch_bounds__(kUThreads) void u_prep_kernel(UPrepArgs p) {
+  __shared__ double zs[kUHead];
+  const int tid = threadIdx.x, d = p.d, SB = p.SB, kq = p.kdp / 4;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d;
+  const int dd = full ? d * d : d;
+  const double *z = p.z ? p.z : p.U;
+  for (int a = tid; a < d; a += kUThreads) zs[a] = z[a];
+  __syncthreads();
+  const long long tile = blockIdx.x;
+  const long long c_begin = (long long)p.i_begin * SB, c_end = (long long)p.i_end * SB;
+  double *Ut = p.U + kUHead + (size_t)tile * kq * 64;
+  for (int x = tid; x < kq * 64; x += kUThreads) {
+    const int t = x >> 6, l = x & 63, kl = l >> 4, cl = l & 15;
+    const int e = 4 * t + kl;
+    const long long col = p.u_col0 + tile * 16 + cl;
+    double u = 0.0;
+    if (col >= c_begin && col < c_end) {
+      const double *C = p.covars + (size_t)col * dd;
+      const double *mu = p.centres + (size_t)col * d;
+      if (e < NPF) {
+        int a = e, b = e;
+        if (full) packed_ab(e, d, a, b);
+        const double ma = mu[a] - zs[a], mb = mu[b] - zs[b];
+        if (!full) u = fma(ma, ma, C[a]);
+        else if (a == b) u = fma(ma, ma, C[a * d + a]);
+        else u = fma(2.0 * ma, mb, C[a * d + b] + C[b * d + a]);
+      } else if (e < NPF + d) {
+        u = mu[e - NPF] - zs[e - NPF];
+      }
+    }
+    Ut[x] = u;
+  }
+}
+
+template <int KQB, int RC>
+__global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NT = blockDim.x, NW = NT >> 6;
+  const int kq = p.kdp / 4, KS = p.K * p.S, SB = p.SB;
+  const int nrt = p.ksp / 16, nchunk = nrt / RC;
+  double *Wl = lds;                            // [kq][RC][64] W' chunk, A-operand lane order
+  double *bl = Wl + (size_t)kq * RC * 64;      // [RC * 16] bias' of the chunk
+  const long long c_begin = (long long)p.i_begin * SB, c_end = (long long)p.i_end * SB;
+  const long long t_first = (c_begin - p.u_col0) / 16;
+  const long long t_last = (c_end - p.u_col0 + 15) / 16;
+  const long long per_round = (long long)gridDim.x * NW;
+  const long long rounds = (t_last - t_first + per_round - 1) / per_round;
+  const int kl = lane >> 4, cl = lane & 15;
+  const size_t ldE = (size_t)p.e_ld;
+  const double sm = p.smooth;
+  auto stage = [&](int ch) {
+    __syncthreads();  // the previous chunk's reads are done
+    const int n = kq * RC * 64;
+    for (int x = tid; x < n; x += NT) {
+      const int t = x / (RC * 64), rem = x - t * (RC * 64), rt = rem >> 6, l = rem & 63;
+      const int row = (ch * RC + rt) * 16 + (l & 15), e = 4 * t + (l >> 4);
+      Wl[x] = p.W[(size_t)e * p.ksp + row];
+    }
+    for (int x = tid; x < RC * 16; x += NT) bl[x] = p.bias[ch * RC * 16 + x];
+    __syncthreads();
+  };
+  if (nchunk == 1) stage(0);
+  for (long long r = 0; r < rounds; ++r) {
+    const long long tile = t_first + r * per_round + (long long)blockIdx.x * NW + wave;
+    const bool tv = tile < t_last;
+    const double *Ut = p.U + kUHead + (size_t)(tv ? tile : t_first) * kq * 64 + lane;
+    double u[KQB];
+#pragma unroll
+    for (int t = 0; t < KQB; ++t) {  // clamped address: no load past the tile
+      const double v = Ut[(size_t)(t < kq ? t : 0) * 64];
+      u[t] = t < kq ? v : 0.0;
+    }
+    const long long col = p.u_col0 + tile * 16 + cl;
+    const bool cv = tv && col >= c_begin && col < c_end;
+    double *Ec = p.E + (cv ? col - (long long)p.i_buf0 * SB : 0);
+    for (int ch = 0; ch < nchunk; ++ch) {
+      if (nchunk > 1) stage(ch);
+      double4_t acc[RC];
+#pragma unroll
+      for (int q = 0; q < RC; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[q][v] = bl[q * 16 + kl + 4 * v];
+#pragma unroll
+      for (int t = 0; t < KQB; ++t) {
+        if (t < kq) {
+#pragma unroll
+          for (int q = 0; q < RC; ++q)
+            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(Wl[(t * RC + q) * 64 + lane], u[t],
+                                                          acc[q], 0, 0, 0);
+        }
+      }
+      if (cv) {
+#pragma unroll
+        for (int q = 0; q < RC; ++q)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int row = (ch * RC + q) * 16 + kl + 4 * v;
+            if (row < KS) Ec[(size_t)row * ldE] = sm != 1.0 ? acc[q][v] / sm : acc[q][v];
+          }
+      }
+    }
+  }
+}
+
+hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st) {
+  if (a.d < 1 || a.d > kUHead || a.u_col0 % 16 != 0) return hipErrorInvalidValue;
+  const long long c_end = (long long)a.i_end * a.SB;
+  const long long ntile = u_tiles(c_end - a.u_col0);
+  if (!a.z) {  // partial sums parked in the tile area (u_prep_kernel rewrites it)
+    const long long area = ntile * (a.kdp / 4) * 64;
+    const int nblk = (int)std::max<long long>(1, std::min<long long>(kUShiftBlocks, area / (a.d + 1)));
+    hipLaunchKernelGGL(u_shift_kernel, dim3(nblk), dim3(kUThreads), 0, st, a, 0, nblk);
+    hipLaunchKernelGGL(u_shift_kernel, dim3(1), dim3(kUThreads), 0, st, a, 1, nblk);
+  }
+  if (ntile > 0 && a.i_end > a.i_begin)
+    hipLaunchKernelGGL(u_prep_kernel, dim3((unsigned)ntile), dim3(kUThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+bool plan_emission_u(EmissionArgs &a, size_t &lds) {
+  const int kq = a.kdp / 4;
+  if (kq > kUMaxKq) {
+    a.urc = 0;
+    return false;
+  }
+  a.ukqb = kq <= 4 ? 4 : kq <= 12 ? 12 : kUMaxKq;
+  a.urc = kq <= 12 ? 8 : 4;   // ksp / 16 is a multiple of 8: RC divides it
+  a.nwave = 8;
+  lds = ((size_t)kq * a.urc * 64 + (size_t)a.urc * 16) * sizeof(double);
+  return true;
+}
+
+template <int KQB, int RC>
+static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st) {
+  auto *fn = &emission_u_kernel<KQB, RC>;
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
+  if (e != hipSuccess) return e;
+  const int cus = device_cus();
+  const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), a.nwave * 64, lds);
+  const long long c_begin = (long long)a.i_begin * a.SB, c_end = (long long)a.i_end * a.SB;
+  const long long ntile = (c_end - a.u_col0 + 15) / 16 - (c_begin - a.u_col0) / 16;
+  const long long want = (ntile + a.nwave - 1) / a.nwave;
+  const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, (long long)cus * per_cu));
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(a.nwave * 64), lds, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 bool plan_emission(EmissionArgs &a, size_t &lds) {
   const bool full = a.covmode == kCovFull;
   const int d = a.d;
@@ -477,6 +698,11 @@ static hipError_t launch_raw_kq(const EmissionArgs &a, size_t lds, hipStream_t s
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   if (ncols <= 0) return hipSuccess;
+  if (a.U && a.urc) {
+    if (a.ukqb == 4) return launch_u_fn<4, 8>(a, lds, st);
+    if (a.ukqb == 12) return launch_u_fn<12, 8>(a, lds, st);
+    return launch_u_fn<kUMaxKq, 4>(a, lds, st);
+  }
   if (a.wfull) {
     // KD = d(d+1)/2 + d (full) or 2d (diag), d <= 8 even: k-steps 2, 4, 7, 11 (full),
     // 1, 2, 3, 4 (diag)

@@ -157,6 +157,13 @@ struct EmissionArgs {
   double *W, *bias, *shift;  // W' = -W/2 [kdp][ksp], bias' = -bias/2 [ksp], z [d] (emission_prep_kernel)
   double *E;                 // [K*S][(i - i_buf0) * SB + b]  (row stride e_ld)
   double smooth;             // E /= smooth when != 1 (VHEM sibling)
+  // prepared-operand GEMM (emission_u_kernel): U in the u_prep layout, its tile 0 at
+  // global column u_col0; zfix = the shift U was built with (emission_prep_kernel
+  // then uses it for W', bias'), or null (z = mean of the finite cluster means)
+  const double *U, *zfix;
+  long long u_col0;
+  int urc;    // row tiles per LDS chunk of W' (emission_u_kernel), 0: old kernels
+  int ukqb;   // register bucket of the U tile (k-steps)
   // per-call side jobs of emission_prep_kernel
   const double *logA;        // [K][S][S]
   double *Atg;               // [K][S][S] A' = exp(logA - rowmax), or null
@@ -164,6 +171,32 @@ struct EmissionArgs {
   int n_zero;
 };
 bool plan_emission(EmissionArgs &a, size_t &lds);
+// emission_u_kernel's plan: row chunking and LDS; false when the shape needs the
+// raw / generic kernels (k-steps > kUMaxKq).  launch_emission takes it when a.U is set.
+bool plan_emission_u(EmissionArgs &a, size_t &lds);
+
+// The base-set operand U of the K1 GEMM (vbhem_prepare_base): for column tile ct
+// (16 columns (i,b), global column u_col0 + 16 ct + cl) and k-step t, the 64
+// doubles of the MFMA B operand in lane order: U[(ct kq + t) 64 + 16 kl + cl] =
+// u(e = 4t + kl, col), zero for e >= KD and for columns past the end.  Buffer:
+// [kUHead doubles: z (d) | 0][ntile * kq * 64].
+constexpr int kUHead = 64;
+constexpr int kUMaxKq = 40;
+inline long long u_tiles(long long ncols) { return (ncols + 15) / 16; }
+inline size_t u_doubles(long long ncols, int d, int covmode) {
+  return (size_t)kUHead + (size_t)u_tiles(ncols) * (emission_kdp(d, covmode) / 4) * 64;
+}
+struct UPrepArgs {
+  int N, SB, d, covmode, kdp;
+  int i_begin, i_end;         // bases whose columns are built
+  long long u_col0;           // global column of tile 0 (a multiple of 16)
+  const int *nstates;
+  const double *centres, *covars;
+  double *U;                  // the buffer (head + tiles)
+  const double *z;            // the shift (device), or null: u_shift_kernel computes the
+                              // mean of the valid base means of [0, N) into the head first
+};
+hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st);
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st);
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st);
 

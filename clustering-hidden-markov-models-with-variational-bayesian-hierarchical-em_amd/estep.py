@@ -22,9 +22,12 @@ F64 = torch.float64
 
 
 class EStepEngine:
-    def __init__(self, base: BaseSet, K: int, S: int, T: int, device=None, trials: int = 1):
+    def __init__(self, base: BaseSet, K: int, S: int, T: int, device=None, trials: int = 1,
+                 prepare: bool = True):
         """K clusters in total; with ``trials`` = R > 1 they are R independent EM
-        trials of K / R clusters each, trial-major (vbhem_estep_fused_trials)."""
+        trials of K / R clusters each, trial-major (vbhem_estep_fused_trials).
+        ``prepare``: build the base set's emission-GEMM operand once here
+        (vbhem_prepare_base) instead of in every call."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -47,7 +50,14 @@ class EStepEngine:
         self.logOmega = torch.zeros((K,), dtype=F64, device=dv)
         bb = self.base
         self._bt = _capi.BaseT(N, SB, d, bb.covmode, _capi.ptr(bb.nstates), _capi.ptr(bb.prior),
-                               _capi.ptr(bb.A), _capi.ptr(bb.centres), _capi.ptr(bb.covars))
+                               _capi.ptr(bb.A), _capi.ptr(bb.centres), _capi.ptr(bb.covars), None)
+        self._U = None
+        ub = int(self.lib.vbhem_prepare_base_bytes(ctypes.byref(self._bt))) if prepare else 0
+        if ub > 0:
+            self._U = torch.empty((ub // 8,), dtype=F64, device=dv)
+            _capi.check(self.lib.vbhem_prepare_base(ctypes.byref(self._bt), _capi.ptr(self._U), ub,
+                                                    self._stream()), "vbhem_prepare_base")
+            self._bt.U = _capi.ptr(self._U)
         self._ct = _capi.ClusterT(K, S, _capi.ptr(self.c_logA), _capi.ptr(self.c_logPi),
                                   _capi.ptr(self.c_m), _capi.ptr(self.c_P), _capi.ptr(self.c_c))
         self.trials = int(trials)

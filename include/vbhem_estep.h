@@ -61,6 +61,11 @@ typedef struct {
   const double *A;       /* [N][SB][SB] hmm_b.A, A[i][from][to]                */
   const double *centres; /* [N][SB][d] emit{k}.centres                          */
   const double *covars;  /* [N][SB][d][d] | [N][SB][d]   emit{k}.covars         */
+  /* Optional: the base set's operand of the emission GEMM, prepared once by
+   * vbhem_prepare_base (device memory, cluster independent), or NULL -- then every
+   * call builds it for the bases it processes in its workspace.  Ignored by the
+   * *_host entry points (they prepare their own). */
+  const double *U;
 } vbhem_base_t;
 
 /* h3m_r: the K cluster HMMs' variational constants for this EM iteration
@@ -74,6 +79,17 @@ typedef struct {
   const double *P;       /* [K][S][d][d] invCovR = v.*W  | [K][S][d] v*W (diag) */
   const double *c;       /* [K][S]     logdetCovPlusDdivlamR = -logLambdaTilde + d/lambda */
 } vbhem_cluster_t;
+
+/* The base set's side of the emission GEMM (K1), prepared once per base set:
+ * E[(i,b),(j,s)] = bias'(j,s) + sum_e W'(e,(j,s)) U(e,(i,b)) with U built from the
+ * base covariances and the base means shifted by z = the mean of the valid base
+ * means (a fixed, cluster-independent shift: the quadratic form is shift invariant,
+ * the shift keeps its expanded terms small).  vbhem_prepare_base_bytes: the device
+ * bytes of U for `base` (0: unsupported descriptor); vbhem_prepare_base fills them
+ * (device pointers in `base`, enqueued on `stream`).  Pass the buffer as base->U to
+ * the device entry points; it stays valid while the base arrays are unchanged. */
+size_t vbhem_prepare_base_bytes(const vbhem_base_t *base);
+int vbhem_prepare_base(const vbhem_base_t *base, double *U_dev, size_t bytes, void *stream);
 
 /* Per-pair outputs of the reference MEX (mex.c:396-409), laid out [N][K][...]:
  *   LL_elbo [N][K]; sum_nu_1 [N][K][S]; emit_pr [N][K][S]; emit_mu [N][K][S][d];
