@@ -294,7 +294,7 @@ def main():
     fb_launch_ms = tk["fb_ms"] / max(1, tk["fb_launches"])
     pairs_per_launch = tk["fb_pairs"] / max(1, tk["fb_launches"])
     split = S <= 16 and Sb <= S and d <= 64
-    gated = split and tk["gated_fwd_launches"] > 0
+    gated = split and tkb["gated_fwd_launches"] > 0
     if gated:
         fpp = bwd_flops_per_pair(S, Sb, T)
     else:
@@ -304,7 +304,7 @@ def main():
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
     lpc = 1 if S <= 4 else 2 if S <= 8 else 4      # split_lpc (dense / list modes)
     lpc_bwd = 1 if S <= 8 else 2                    # split_lpc_bwd (backward mode)
-    if gated and S <= 8 and not os.environ.get("VBHEM_NO_BWD2"):
+    if gated and S <= 16 and not os.environ.get("VBHEM_NO_BWD2"):
         kname = f"vbhem::fb_bwd2_kernel<{S}>"
     else:
         kname = (f"vbhem::fb_split_kernel<{S}, {lpc_bwd if gated else lpc}, {1 if gated else 0}>"

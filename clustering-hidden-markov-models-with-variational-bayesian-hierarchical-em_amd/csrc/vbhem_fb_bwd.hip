@@ -36,8 +36,9 @@
 #include "vbhem_log_table.h"
 #include "vbhem_math.h"
 
+// waves per SIMD the kernel is compiled for (register budget 512 / W)
 #ifndef VBHEM_BWD2_WAVES
-#define VBHEM_BWD2_WAVES 3
+#define VBHEM_BWD2_WAVES(S) ((S) <= 12 ? 3 : 2)
 #endif
 
 namespace vbhem {
@@ -90,9 +91,11 @@ __device__ __forceinline__ void wave_sync() {
 
 template <int S>
 struct Bwd2Layout {
-  static constexpr int LPP = (S + 1) / 2;            // lanes per pair
+  static constexpr int CPL = S <= 8 ? 2 : 1;         // base-state columns per lane
+  static constexpr int LPP = (S + CPL - 1) / CPL;    // lanes per pair
   static constexpr int PPW = 64 / LPP;               // pairs per wavefront
-  static constexpr int SP = 2 * LPP;                 // slab columns (padded)
+  static constexpr int NA = (S * S + 15) / 16 > 4 ? (S * S + 15) / 16 : 4;  // A' doubles per lane
+  static constexpr int SP = CPL * LPP;               // slab columns (padded)
   static constexpr int XCS = (S + 1) / 2 * 2 + 2;    // slab column stride (even: 16-B rows)
   static constexpr int XP = SP * XCS + 2;            // per-pair slab (doubles)
   static constexpr int OFF_CL = kTabD;               // amax [S], lpi [S]
@@ -102,11 +105,11 @@ struct Bwd2Layout {
 }  // namespace
 
 template <int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBHEM_BWD2_WAVES)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBHEM_BWD2_WAVES(S))))
 void fb_bwd2_kernel(const SplitArgs p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using LY = Bwd2Layout<S>;
-  constexpr int LPP = LY::LPP, PPW = LY::PPW;
+  constexpr int LPP = LY::LPP, PPW = LY::PPW, CPL = LY::CPL, NA = LY::NA;
   const int tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
   const int PPB = NW * PPW;
   const int SB = p.SB, K = p.K, T = p.T;
@@ -150,12 +153,12 @@ void fb_bwd2_kernel(const SplitArgs p) {
   const int q = wave * PPW + (valid ? qw : 0);
   double *X = Xall + (size_t)q * LY::XP;
   const int ntile = (p.i_end - p.i_begin + PPB - 1) / PPB;
-  // A' spread over the 16 lanes of every DPP row: entry e = r S + k in register e % 4
-  // of row lane e / 4 (S^2 <= 64)
-  double aq[4];
+  // A' spread over the 16 lanes of every DPP row: entry e = r S + k in register e % NA
+  // of row lane e / NA (16 NA >= S^2)
+  double aq[NA];
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    const int e = 4 * (lane & 15) + x;
+  for (int x = 0; x < NA; ++x) {
+    const int e = NA * (lane & 15) + x;
     aq[x] = e < S * S ? p.Atg[(size_t)j * S * S + e] : 0.0;
   }
 
@@ -164,11 +167,11 @@ void fb_bwd2_kernel(const SplitArgs p) {
     const bool active = valid && i < p.i_end;
     const int ic = active ? i : p.i_begin;
     if (valid && w == 0) F[q] = 0;
-    // ---- per-pair inputs: two columns ----
-    double Ef[2][S], Lf[2][S], arow[2][S], pb[2];
-    bool bv[2];
+    // ---- per-pair inputs: CPL columns ----
+    double Ef[CPL][S], Lf[CPL][S], arow[CPL][S], pb[CPL];
+    bool bv[CPL];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < CPL; ++c) {
       const int b = w + c * LPP;
       bv[c] = b < SB;
       const int bc = bv[c] ? b : SB - 1;
@@ -194,9 +197,9 @@ void fb_bwd2_kernel(const SplitArgs p) {
 
     // ---- K2: backward recursion, t = T-1 .. 1 ----
     for (int t = T - 1; t >= 1; --t) {
-      double G[2][S], M[2];
+      double G[CPL][S], M[CPL];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < CPL; ++c) {
         double v[S];
 #pragma unroll
         for (int k = 0; k < S; ++k) v[k] = Ef[c][k] + Lf[c][k];
@@ -206,18 +209,20 @@ void fb_bwd2_kernel(const SplitArgs p) {
         for (int k = 0; k < S; ++k) v[k] -= m;
         exp_tabc_n<S>(G[c], v, etab);
       }
-      double Z[2][S];
-      // Z = A' G with A'[r][k] broadcast from lane (r S + k) / 4 of the lane's DPP row:
+      double Z[CPL][S];
+      // Z = A' G with A'[r][k] broadcast from lane (r S + k) / NA of the lane's DPP row:
       // no scalar loads, no LDS (sums in k order, as fma chains)
 #pragma unroll
-      for (int r = 0; r < S; ++r) Z[0][r] = Z[1][r] = 0.0;
+      for (int c = 0; c < CPL; ++c)
+#pragma unroll
+        for (int r = 0; r < S; ++r) Z[c][r] = 0.0;
       static_for<0, S * S>([&](auto ec) {
         constexpr int e = decltype(ec)::value, r = e / S, k = e % S;
-        dpp_fmac_bcast<e / 4>(Z[0][r], aq[e & 3], G[0][k]);
-        dpp_fmac_bcast<e / 4>(Z[1][r], aq[e & 3], G[1][k]);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) dpp_fmac_bcast<e / NA>(Z[c][r], aq[e % NA], G[c][k]);
       });
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < CPL; ++c) {
         double lz[S];
 #pragma unroll
         for (int k = 0; k < S; ++k) bad |= bv[c] && !(Z[c][k] >= kZMinB);
@@ -239,7 +244,9 @@ void fb_bwd2_kernel(const SplitArgs p) {
       }
       wave_sync();
 #pragma unroll
-      for (int k = 0; k < S; ++k) Lf[0][k] = Lf[1][k] = 0.0;
+      for (int c = 0; c < CPL; ++c)
+#pragma unroll
+        for (int k = 0; k < S; ++k) Lf[c][k] = 0.0;
 #pragma unroll
       for (int be = 0; be < S; ++be) {
         const double *xc = X + be * LY::XCS;
@@ -256,18 +263,17 @@ void fb_bwd2_kernel(const SplitArgs p) {
           for (int k = 0; k < S; ++k) xs[k] = xc[k];
         }
 #pragma unroll
-        for (int k = 0; k < S; ++k) {
-          Lf[0][k] = fma(arow[0][be], xs[k], Lf[0][k]);
-          Lf[1][k] = fma(arow[1][be], xs[k], Lf[1][k]);
-        }
+        for (int k = 0; k < S; ++k)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) Lf[c][k] = fma(arow[c][be], xs[k], Lf[c][k]);
       }
       wave_sync();
     }
 
     // ---- K3: termination, L_elbo(i, j) = sum_b prior_b * log sum_s exp(lpi + E + L) ----
-    double Y[2];
+    double Y[CPL];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < CPL; ++c) {
       double v1[S], ev[S], m1 = -INFINITY;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
@@ -286,15 +292,15 @@ void fb_bwd2_kernel(const SplitArgs p) {
       Y[c] = pb[c] * (m1 + lzs[0]);
     }
     if (valid) {
-      X[w * LY::XCS] = Y[0];
-      X[(w + LPP) * LY::XCS] = Y[1];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) X[(w + c * LPP) * LY::XCS] = Y[c];
     }
     // fallback flags, as fb_split_kernel: underflow with finite inputs -> exact
     // kernel; non-finite cluster constants or emissions -> L_elbo NaN
     if (bad && active) {
       bool nf = false;
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < CPL; ++c)
 #pragma unroll
         for (int k = 0; k < S; ++k) nf |= !isfinite(Ef[c][k]);
       for (int x = 0; x < S; ++x) nf |= isnan(amax[x]) || isnan(lpi[x]);
@@ -322,14 +328,17 @@ void fb_bwd2_kernel(const SplitArgs p) {
 // ---------------------------------------------------------------------------
 size_t bwd2_lds(int S, int nwb) {
   if (S < 1 || S > kBwd2MaxS) return 0;
-  const int LPP = (S + 1) / 2, PPW = 64 / LPP;
-  const int XCS = (S + 1) / 2 * 2 + 2, XP = 2 * LPP * XCS + 2;
+  const int CPL = S <= 8 ? 2 : 1, LPP = (S + CPL - 1) / CPL, PPW = 64 / LPP;
+  const int XCS = (S + 1) / 2 * 2 + 2, XP = CPL * LPP * XCS + 2;
   const int off_x = (kTabD + 2 * S + 1) / 2 * 2;
   const int ppb = nwb * PPW;
   return ((size_t)off_x + (size_t)ppb * XP + (ppb + 1) / 2 + 1) * sizeof(double);
 }
 
-int bwd2_ppb(int S, int nwb) { return nwb * (64 / ((S + 1) / 2)); }
+int bwd2_ppb(int S, int nwb) {
+  const int CPL = S <= 8 ? 2 : 1;
+  return nwb * (64 / ((S + CPL - 1) / CPL));
+}
 
 template <int S>
 static const void *bwd2_fn() {
@@ -346,6 +355,14 @@ static const void *bwd2_fn_s(int S) {
     case 6: return bwd2_fn<6>();
     case 7: return bwd2_fn<7>();
     case 8: return bwd2_fn<8>();
+    case 9: return bwd2_fn<9>();
+    case 10: return bwd2_fn<10>();
+    case 11: return bwd2_fn<11>();
+    case 12: return bwd2_fn<12>();
+    case 13: return bwd2_fn<13>();
+    case 14: return bwd2_fn<14>();
+    case 15: return bwd2_fn<15>();
+    case 16: return bwd2_fn<16>();
     default: return nullptr;
   }
 }
@@ -366,6 +383,8 @@ hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_
     hipLaunchKernelGGL(fb_bwd2_kernel<s>, dim3(grid), dim3(a.nwb * 64), lds, st, a); \
     break;
     VBHEM_B2(1) VBHEM_B2(2) VBHEM_B2(3) VBHEM_B2(4) VBHEM_B2(5) VBHEM_B2(6) VBHEM_B2(7) VBHEM_B2(8)
+    VBHEM_B2(9) VBHEM_B2(10) VBHEM_B2(11) VBHEM_B2(12) VBHEM_B2(13) VBHEM_B2(14) VBHEM_B2(15)
+    VBHEM_B2(16)
 #undef VBHEM_B2
     default: return hipErrorInvalidValue;
   }

@@ -231,9 +231,10 @@ hipError_t launch_split(const SplitArgs &a, unsigned grid, size_t lds, hipStream
 int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mode
 
 // fb_bwd2_kernel (vbhem_fb_bwd.hip): the backward-only pass (kFbBackward) for
-// S <= kBwd2MaxS, two base-state columns per lane; SplitArgs fields used: SB, K,
-// S, T, nwb, i_begin/i_end/i_buf0, prior, A, logA, logPi, E, e_ld, Atg, LL, flags.
-constexpr int kBwd2MaxS = 8;
+// S <= kBwd2MaxS, two base-state columns per lane (S <= 8) or one; SplitArgs fields
+// used: SB, K, S, T, nwb, i_begin/i_end/i_buf0, prior, A, logA, logPi, E, e_ld,
+// Atg, LL, flags.
+constexpr int kBwd2MaxS = 16;
 size_t bwd2_lds(int S, int nwb);  // dynamic LDS bytes (0: S unsupported)
 int bwd2_ppb(int S, int nwb);     // pairs per block
 int bwd2_resident_blocks(int S, int nwb, size_t lds);
