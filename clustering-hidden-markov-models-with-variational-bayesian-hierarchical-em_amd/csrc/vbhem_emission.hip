@@ -524,71 +524,94 @@ __global__ __launch_bounds__(kUThreads) void u_prep_kernel(UPrepArgs p) {
   }
 }
 
-template <int KQB, int RC>
+template <int KQB, int RC, int NTW, bool EXACT>
 __global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NT = blockDim.x, NW = NT >> 6;
-  const int kq = p.kdp / 4, KS = p.K * p.S, SB = p.SB;
+  const int kq = EXACT ? KQB : p.kdp / 4, KS = p.K * p.S, SB = p.SB;
   const int nrt = p.ksp / 16, nchunk = nrt / RC;
   double *Wl = lds;                            // [kq][RC][64] W' chunk, A-operand lane order
   double *bl = Wl + (size_t)kq * RC * 64;      // [RC * 16] bias' of the chunk
   const long long c_begin = (long long)p.i_begin * SB, c_end = (long long)p.i_end * SB;
   const long long t_first = (c_begin - p.u_col0) / 16;
   const long long t_last = (c_end - p.u_col0 + 15) / 16;
-  const long long per_round = (long long)gridDim.x * NW;
+  const long long per_round = (long long)gridDim.x * NW * NTW;
   const long long rounds = (t_last - t_first + per_round - 1) / per_round;
   const int kl = lane >> 4, cl = lane & 15;
   const size_t ldE = (size_t)p.e_ld;
   const double sm = p.smooth;
+  typedef __attribute__((address_space(3))) void *lds_ptr;
+  typedef __attribute__((address_space(1))) void *glb_ptr;
   auto stage = [&](int ch) {
     __syncthreads();  // the previous chunk's reads are done
-    const int n = kq * RC * 64;
-    for (int x = tid; x < n; x += NT) {
+    // W' chunk straight from L2 into LDS (global_load_lds_dwordx4: lane j lands at
+    // block + 16 j), 1 KB = two A-operand rows per wave instruction, no register
+    // round trip and one wait for the whole chunk
+    const int nblk = kq * RC / 2;
+    for (int b = wave; b < nblk; b += NW) {
+      const int x = b * 128 + 2 * lane;
       const int t = x / (RC * 64), rem = x - t * (RC * 64), rt = rem >> 6, l = rem & 63;
       const int row = (ch * RC + rt) * 16 + (l & 15), e = 4 * t + (l >> 4);
-      Wl[x] = p.W[(size_t)e * p.ksp + row];
+      __builtin_amdgcn_global_load_lds((glb_ptr)(p.W + (size_t)e * p.ksp + row),
+                                       (lds_ptr)(Wl + (size_t)b * 128), 16, 0, 0);
     }
     for (int x = tid; x < RC * 16; x += NT) bl[x] = p.bias[ch * RC * 16 + x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
   if (nchunk == 1) stage(0);
   for (long long r = 0; r < rounds; ++r) {
-    const long long tile = t_first + r * per_round + (long long)blockIdx.x * NW + wave;
-    const bool tv = tile < t_last;
-    const double *Ut = p.U + kUHead + (size_t)(tv ? tile : t_first) * kq * 64 + lane;
-    double u[KQB];
+    // NTW column tiles per wave: each staged W' chunk feeds NTW * RC MFMAs per k-step
+    double u[NTW][KQB];
+    double *Ec[NTW];
+    bool cv[NTW];
 #pragma unroll
-    for (int t = 0; t < KQB; ++t) {  // clamped address: no load past the tile
-      const double v = Ut[(size_t)(t < kq ? t : 0) * 64];
-      u[t] = t < kq ? v : 0.0;
+    for (int n = 0; n < NTW; ++n) {
+      const long long tile = t_first + r * per_round + ((long long)blockIdx.x * NW + wave) * NTW + n;
+      const bool tv = tile < t_last;
+      const double *Ut = p.U + kUHead + (size_t)(tv ? tile : t_first) * kq * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < KQB; ++t) {  // kq is uniform: a scalar branch, no load past the tile
+        if (t < kq) u[n][t] = Ut[(size_t)t * 64];
+        else u[n][t] = 0.0;
+      }
+      const long long col = p.u_col0 + tile * 16 + cl;
+      cv[n] = tv && col >= c_begin && col < c_end;
+      Ec[n] = p.E + (cv[n] ? col - (long long)p.i_buf0 * SB : 0);
     }
-    const long long col = p.u_col0 + tile * 16 + cl;
-    const bool cv = tv && col >= c_begin && col < c_end;
-    double *Ec = p.E + (cv ? col - (long long)p.i_buf0 * SB : 0);
     for (int ch = 0; ch < nchunk; ++ch) {
       if (nchunk > 1) stage(ch);
-      double4_t acc[RC];
+      double4_t acc[NTW][RC];
 #pragma unroll
       for (int q = 0; q < RC; ++q)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[q][v] = bl[q * 16 + kl + 4 * v];
+        for (int v = 0; v < 4; ++v) {
+          const double b = bl[q * 16 + kl + 4 * v];
+#pragma unroll
+          for (int n = 0; n < NTW; ++n) acc[n][q][v] = b;
+        }
 #pragma unroll
       for (int t = 0; t < KQB; ++t) {
         if (t < kq) {
 #pragma unroll
-          for (int q = 0; q < RC; ++q)
-            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(Wl[(t * RC + q) * 64 + lane], u[t],
-                                                          acc[q], 0, 0, 0);
+          for (int q = 0; q < RC; ++q) {
+            const double w = Wl[(t * RC + q) * 64 + lane];
+#pragma unroll
+            for (int n = 0; n < NTW; ++n)
+              acc[n][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, u[n][t], acc[n][q], 0, 0, 0);
+          }
         }
       }
-      if (cv) {
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) {
+        if (!cv[n]) continue;
 #pragma unroll
         for (int q = 0; q < RC; ++q)
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int row = (ch * RC + q) * 16 + kl + 4 * v;
-            if (row < KS) Ec[(size_t)row * ldE] = sm != 1.0 ? acc[q][v] / sm : acc[q][v];
+            if (row < KS) Ec[n][(size_t)row * ldE] = sm != 1.0 ? acc[n][q][v] / sm : acc[n][q][v];
           }
       }
     }
@@ -610,6 +633,12 @@ hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
+#ifndef UNTW
+#define UNTW 2
+#endif
+#ifndef UNWAVE_CHUNKED
+#define UNWAVE_CHUNKED 4
+#endif
 bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   const int kq = a.kdp / 4;
   if (kq > kUMaxKq) {
@@ -618,21 +647,24 @@ bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   }
   a.ukqb = kq <= 4 ? 4 : kq <= 12 ? 12 : kUMaxKq;
   a.urc = kq <= 12 ? 8 : 4;   // ksp / 16 is a multiple of 8: RC divides it
-  a.nwave = 8;
+  // chunked W' (restaged every round): 4-wave blocks, two per CU, so one block's
+  // staging overlaps the other's MFMAs
+  a.nwave = a.ksp / 16 > a.urc ? UNWAVE_CHUNKED : 8;
   lds = ((size_t)kq * a.urc * 64 + (size_t)a.urc * 16) * sizeof(double);
   return true;
 }
 
-template <int KQB, int RC>
+template <int KQB, int RC, int NTW, bool EXACT = false>
 static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st) {
-  auto *fn = &emission_u_kernel<KQB, RC>;
+  if (EXACT && a.kdp / 4 != KQB) return hipErrorInvalidValue;
+  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
   const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), a.nwave * 64, lds);
   const long long c_begin = (long long)a.i_begin * a.SB, c_end = (long long)a.i_end * a.SB;
   const long long ntile = (c_end - a.u_col0 + 15) / 16 - (c_begin - a.u_col0) / 16;
-  const long long want = (ntile + a.nwave - 1) / a.nwave;
+  const long long want = (ntile + (long long)a.nwave * NTW - 1) / ((long long)a.nwave * NTW);
   const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, (long long)cus * per_cu));
   hipLaunchKernelGGL(fn, dim3(grid), dim3(a.nwave * 64), lds, st, a);
   return hipGetLastError();
@@ -699,9 +731,11 @@ hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   if (ncols <= 0) return hipSuccess;
   if (a.U && a.urc) {
-    if (a.ukqb == 4) return launch_u_fn<4, 8>(a, lds, st);
-    if (a.ukqb == 12) return launch_u_fn<12, 8>(a, lds, st);
-    return launch_u_fn<kUMaxKq, 4>(a, lds, st);
+    if (a.ukqb == 4) return launch_u_fn<4, 8, 1>(a, lds, st);
+    if (a.ukqb == 12) return launch_u_fn<12, 8, 1>(a, lds, st);
+    // W' restaged per chunk: two column tiles per wave halve the staging per column
+    if (a.kdp / 4 == 38) return launch_u_fn<38, 4, UNTW, true>(a, lds, st);  // d = 16 full (C5)
+    return launch_u_fn<kUMaxKq, 4, UNTW>(a, lds, st);
   }
   if (a.wfull) {
     // KD = d(d+1)/2 + d (full) or 2d (diag), d <= 8 even: k-steps 2, 4, 7, 11 (full),
