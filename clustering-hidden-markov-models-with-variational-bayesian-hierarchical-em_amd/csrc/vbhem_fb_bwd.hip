@@ -18,14 +18,15 @@
 // cluster j per block, consecutive bases.  Lane w of a pair owns columns b = w and
 // b = w + LPP (padded columns past SB duplicate column SB-1 with zero base
 // transitions and prior: exact no-ops, as in fb_split_kernel).  In registers per
-// column: Ef[S], Lf[S], arow[S] (Ab row b).  Per step:
-//   M = max_s (Ef + Lf), G = exp(Ef + Lf - M)        (table exp, LDS table)
-//   Z = A' G                                          (A' rows as scalar operands)
+// column: Ef[S], V[S] = Ef + Lf, arow[S] (Ab row b).  Per step:
+//   M = max_s V, G = exp(V - M)                       (table exp, LDS table)
+//   Z = A' G                                          (A' rows by DPP broadcast)
 //   sv = M + log Z                                    (table log, LDS table)
-//   Lf = sum_b' Ab[b][b'] sv[.][b']                   (per-pair LDS slab)
+//   V = Ef + sum_b' Ab[b][b'] sv[.][b']               (per-pair LDS slab)
 // with the cluster row maxima folded out of the loop: A' = exp(logA - amax),
 // sv_ref = sv + amax, so L_ref = Lf + amax * rowsum(Ab) and E + L_ref = Ef + Lf
-// with Ef = E + amax * rowsum(Ab) (once per pair).
+// with Ef = E + amax * rowsum(Ab) (once per pair).  exp / log are the
+// short-series exp_tabd_n / log_tabd_n (vbhem_math.h): 9 fp64 operations each.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,13 +46,16 @@ namespace vbhem {
 
 namespace {
 
-constexpr double kZMinB = 1e-200;
-alignas(16) __device__ const double kLogTabB[kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
+// underflow guard of the column sums Z (the fallback to fb_exact_kernel):
+// Z < 2^-665 (~7.6e-201), tested on the high word as a signed integer (negative Z,
+// zero and denormals below it too); NaN shows in the pair's termination value
+constexpr int kZMinHi = 0x16600000;
+alignas(16) __device__ const double kLogTabB[2 * kLogTabDEntries] = VBHEM_LOG512_TABLE_INIT;
 alignas(16) __device__ const double kExpTabB[kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
 
-// compact LDS tables of exp_tabc_n / log_tabc_n (vbhem_math.h)
+// LDS tables of exp_tabd_n / log_tabd_n (vbhem_math.h)
 constexpr int kTabExpD = kExpTabEntries;        // 256 doubles
-constexpr int kTabLogD = 2 * kLogTabEntries;    // 256 doubles
+constexpr int kTabLogD = 2 * kLogTabDEntries;   // 1024 doubles
 constexpr int kTabD = kTabExpD + kTabLogD;
 
 // acc += bcast(a from lane N of this lane's 16-lane row) * b: v_fmac_f64 with DPP
@@ -114,17 +118,14 @@ void fb_bwd2_kernel(const SplitArgs p) {
   const int PPB = NW * PPW;
   const int SB = p.SB, K = p.K, T = p.T;
   double *etab = lds;                    // [256]
-  double *ltab = lds + kTabExpD;         // [128][2]
+  double *ltab = lds + kTabExpD;         // [512][2]
   double *amax = lds + LY::OFF_CL;       // [S]
   double *lpi = amax + S;                // [S]
   double *Xall = lds + LY::OFF_X;        // [PPB][XP]
   int *F = reinterpret_cast<int *>(Xall + (size_t)PPB * LY::XP);  // [PPB]
 
   for (int x = tid; x < kExpTabEntries; x += NT) etab[x] = kExpTabB[2 * x];
-  for (int x = tid; x < kLogTabEntries; x += NT) {
-    ltab[2 * x] = kLogTabB[4 * x];
-    ltab[2 * x + 1] = kLogTabB[4 * x + 1];
-  }
+  for (int x = tid; x < kTabLogD; x += NT) ltab[x] = kLogTabB[x];
   // persistent: NB blocks per cluster; XCD-aware when NB % 8 == 0 (the K blocks
   // walking the same bases share one XCD's L2, as fb_split_kernel's backward mode)
   const int bk = blockIdx.x, NB = (int)gridDim.x / K;
@@ -168,7 +169,8 @@ void fb_bwd2_kernel(const SplitArgs p) {
     const int ic = active ? i : p.i_begin;
     if (valid && w == 0) F[q] = 0;
     // ---- per-pair inputs: CPL columns ----
-    double Ef[CPL][S], Lf[CPL][S], arow[CPL][S], pb[CPL];
+    // V = Ef + L carried whole: the L sum of every step starts from Ef
+    double Ef[CPL][S], V[CPL][S], arow[CPL][S], pb[CPL];
     bool bv[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -186,14 +188,21 @@ void fb_bwd2_kernel(const SplitArgs p) {
       }
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        const double am = amax[k] * rs;
-        Ef[c][k] = Ep[(size_t)k * p.e_ld] + am;
-        Lf[c][k] = -am;
+        const double e = Ep[(size_t)k * p.e_ld];
+        Ef[c][k] = e + amax[k] * rs;
+        V[c][k] = e;
       }
       const double pr = p.prior[(size_t)ic * SB + bc];
       pb[c] = bv[c] ? pr : 0.0;
     }
-    bool bad = false;
+    // column maxima of V, taken where V is produced (an fma result: no canonicalizing
+    // max(x, x) per element as on a loop-carried value)
+    double Mx[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) Mx[c] = tree_max<S>(V[c]);
+    int zmin[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) zmin[c] = 0x7fffffff;
 
     // ---- K2: backward recursion, t = T-1 .. 1 ----
     for (int t = T - 1; t >= 1; --t) {
@@ -201,13 +210,11 @@ void fb_bwd2_kernel(const SplitArgs p) {
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         double v[S];
-#pragma unroll
-        for (int k = 0; k < S; ++k) v[k] = Ef[c][k] + Lf[c][k];
-        const double m = tree_max<S>(v);
+        const double m = Mx[c];
         M[c] = m;
 #pragma unroll
-        for (int k = 0; k < S; ++k) v[k] -= m;
-        exp_tabc_n<S>(G[c], v, etab);
+        for (int k = 0; k < S; ++k) v[k] = V[c][k] - m;
+        exp_tabd_n<S>(G[c], v, etab);
       }
       double Z[CPL][S];
       // Z = A' G with A'[r][k] broadcast from lane (r S + k) / NA of the lane's DPP row:
@@ -225,8 +232,8 @@ void fb_bwd2_kernel(const SplitArgs p) {
       for (int c = 0; c < CPL; ++c) {
         double lz[S];
 #pragma unroll
-        for (int k = 0; k < S; ++k) bad |= bv[c] && !(Z[c][k] >= kZMinB);
-        log_tabc_n<S>(lz, Z[c], ltab);
+        for (int k = 0; k < S; ++k) zmin[c] = min(zmin[c], __double2hiint(Z[c][k]));
+        log_tabd_n<S>(lz, Z[c], ltab);
         double sv[S];
 #pragma unroll
         for (int k = 0; k < S; ++k) sv[k] = M[c] + lz[k];
@@ -246,7 +253,7 @@ void fb_bwd2_kernel(const SplitArgs p) {
 #pragma unroll
       for (int c = 0; c < CPL; ++c)
 #pragma unroll
-        for (int k = 0; k < S; ++k) Lf[c][k] = 0.0;
+        for (int k = 0; k < S; ++k) V[c][k] = Ef[c][k];
 #pragma unroll
       for (int be = 0; be < S; ++be) {
         const double *xc = X + be * LY::XCS;
@@ -265,8 +272,10 @@ void fb_bwd2_kernel(const SplitArgs p) {
 #pragma unroll
         for (int k = 0; k < S; ++k)
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) Lf[c][k] = fma(arow[c][be], xs[k], Lf[c][k]);
+          for (int c = 0; c < CPL; ++c) V[c][k] = fma(arow[c][be], xs[k], V[c][k]);
       }
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) Mx[c] = tree_max<S>(V[c]);
       wave_sync();
     }
 
@@ -277,20 +286,23 @@ void fb_bwd2_kernel(const SplitArgs p) {
       double v1[S], ev[S], m1 = -INFINITY;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        v1[k] = lpi[k] + Ef[c][k] + Lf[c][k];
+        v1[k] = lpi[k] + V[c][k];
         m1 = fmax(m1, v1[k]);
       }
 #pragma unroll
       for (int k = 0; k < S; ++k) v1[k] -= m1;
-      exp_tabc_n<S>(ev, v1, etab);
+      exp_tabd_n<S>(ev, v1, etab);
       double zs = 0.0;
 #pragma unroll
       for (int k = 0; k < S; ++k) zs += ev[k];
       double lzs[1];
       const double zsa[1] = {zs};
-      log_tabc_n<1>(lzs, zsa, ltab);
+      log_tabd_n<1>(lzs, zsa, ltab);
       Y[c] = pb[c] * (m1 + lzs[0]);
     }
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) bad |= bv[c] && (zmin[c] < kZMinHi || !isfinite(Y[c]));
     if (valid) {
 #pragma unroll
       for (int c = 0; c < CPL; ++c) X[(w + c * LPP) * LY::XCS] = Y[c];
