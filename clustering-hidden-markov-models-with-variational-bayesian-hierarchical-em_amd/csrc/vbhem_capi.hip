@@ -346,7 +346,7 @@ struct FbCtx {
   SplitPlan bwd;    // its backward-only mode (gated schedule), possibly another LPC
   // the backward-only pass on fb_bwd2_kernel (S <= 8): LDS bytes, pairs per block
   size_t bwd2_lds = 0;
-  int bwd2_ppb = 0;
+  int bwd2_ppb = 0, bwd2_nwb = 0;
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
   // emission_u_kernel: on the prepared operand (base->U) or one built per call in u_ws
@@ -391,8 +391,9 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
     vbhem::SplitArgs &ab = c.bwd.a;
     ab.prior = b->prior; ab.A = b->A; ab.logA = cl->logA; ab.logPi = cl->logPi;
     if (c.bwd.ok && cl->S <= vbhem::kBwd2MaxS && !std::getenv("VBHEM_NO_BWD2")) {
-      c.bwd2_lds = vbhem::bwd2_lds(cl->S, 4);
-      c.bwd2_ppb = vbhem::bwd2_ppb(cl->S, 4);
+      c.bwd2_nwb = vbhem::bwd2_waves(cl->S);
+      c.bwd2_lds = vbhem::bwd2_lds(cl->S, c.bwd2_nwb);
+      c.bwd2_ppb = vbhem::bwd2_ppb(cl->S, c.bwd2_nwb);
     }
   }
   return VBHEM_OK;
@@ -506,10 +507,10 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     unsigned grid = ntile * (unsigned)ca.K;
     if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
-      ca.nwb = 4;
+      ca.nwb = c.bwd2_nwb;
       const unsigned nt2 = (unsigned)((i_end - i_begin + c.bwd2_ppb - 1) / c.bwd2_ppb);
       const unsigned all = (unsigned)(vbhem::device_cus() *
-                                      std::max(1, vbhem::bwd2_resident_blocks(ca.S, 4, c.bwd2_lds)));
+                                      std::max(1, vbhem::bwd2_resident_blocks(ca.S, ca.nwb, c.bwd2_lds)));
       unsigned nb = std::max(1u, std::min(nt2, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
       e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, c.bwd2_lds, st);

@@ -26,7 +26,7 @@
 // with the cluster row maxima folded out of the loop: A' = exp(logA - amax),
 // sv_ref = sv + amax, so L_ref = Lf + amax * rowsum(Ab) and E + L_ref = Ef + Lf
 // with Ef = E + amax * rowsum(Ab) (once per pair).  exp / log are the
-// short-series exp_tabd_n / log_tabd_n (vbhem_math.h): 9 fp64 operations each.
+// short-series exp_tabe_n / log_tabe_n (vbhem_math.h): 8 fp64 operations each.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -50,12 +50,13 @@ namespace {
 // Z < 2^-665 (~7.6e-201), tested on the high word as a signed integer (negative Z,
 // zero and denormals below it too); NaN shows in the pair's termination value
 constexpr int kZMinHi = 0x16600000;
-alignas(16) __device__ const double kLogTabB[2 * kLogTabDEntries] = VBHEM_LOG512_TABLE_INIT;
-alignas(16) __device__ const double kExpTabB[kExpTabDoubles] = VBHEM_EXP_TABLE_INIT;
+alignas(16) __device__ const double kLogTabB[2 * kLogTabEEntries] = VBHEM_LOG1024_TABLE_INIT;
+alignas(16) __device__ const double kExpTabB[kExpTabEEntries] = VBHEM_EXP2048_TABLE_INIT;
 
-// LDS tables of exp_tabd_n / log_tabd_n (vbhem_math.h)
-constexpr int kTabExpD = kExpTabEntries;        // 256 doubles
-constexpr int kTabLogD = 2 * kLogTabDEntries;   // 1024 doubles
+// LDS tables of exp_tabe_n / log_tabe_n (vbhem_math.h), 16 KB each: staged once
+// per block, one block per CU
+constexpr int kTabExpD = kExpTabEEntries;       // 2048 doubles
+constexpr int kTabLogD = 2 * kLogTabEEntries;   // 2048 doubles
 constexpr int kTabD = kTabExpD + kTabLogD;
 
 // acc += bcast(a from lane N of this lane's 16-lane row) * b: v_fmac_f64 with DPP
@@ -102,29 +103,32 @@ struct Bwd2Layout {
   static constexpr int SP = CPL * LPP;               // slab columns (padded)
   static constexpr int XCS = (S + 1) / 2 * 2 + 2;    // slab column stride (even: 16-B rows)
   static constexpr int XP = SP * XCS + 2;            // per-pair slab (doubles)
-  static constexpr int OFF_CL = kTabD;               // amax [S], lpi [S]
-  static constexpr int OFF_X = (kTabD + 2 * S + 1) / 2 * 2;
+  static constexpr int OFF_CL = 0;                   // amax [S], lpi [S] (dynamic LDS)
+  static constexpr int OFF_X = (2 * S + 1) / 2 * 2;
 };
 
 }  // namespace
 
 template <int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBHEM_BWD2_WAVES(S))))
+__global__ __launch_bounds__(256 * VBHEM_BWD2_WAVES(S)) __attribute__((amdgpu_waves_per_eu(VBHEM_BWD2_WAVES(S))))
 void fb_bwd2_kernel(const SplitArgs p) {
+  // the tables in static LDS (offset 0: table addresses fold into the ds_read
+  // offsets), the per-pair state in the dynamic part after them
+  __shared__ __attribute__((aligned(16))) double tabs[kTabD];
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using LY = Bwd2Layout<S>;
   constexpr int LPP = LY::LPP, PPW = LY::PPW, CPL = LY::CPL, NA = LY::NA;
   const int tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
   const int PPB = NW * PPW;
   const int SB = p.SB, K = p.K, T = p.T;
-  double *etab = lds;                    // [256]
-  double *ltab = lds + kTabExpD;         // [512][2]
+  double *etab = tabs;                   // [2048]
+  double *ltab = tabs + kTabExpD;        // [1024][2] of {1/(2c), -log(1/c)}
   double *amax = lds + LY::OFF_CL;       // [S]
   double *lpi = amax + S;                // [S]
   double *Xall = lds + LY::OFF_X;        // [PPB][XP]
   int *F = reinterpret_cast<int *>(Xall + (size_t)PPB * LY::XP);  // [PPB]
 
-  for (int x = tid; x < kExpTabEntries; x += NT) etab[x] = kExpTabB[2 * x];
+  for (int x = tid; x < kTabExpD; x += NT) etab[x] = kExpTabB[x];
   for (int x = tid; x < kTabLogD; x += NT) ltab[x] = kLogTabB[x];
   // persistent: NB blocks per cluster; XCD-aware when NB % 8 == 0 (the K blocks
   // walking the same bases share one XCD's L2, as fb_split_kernel's backward mode)
@@ -214,7 +218,7 @@ void fb_bwd2_kernel(const SplitArgs p) {
         M[c] = m;
 #pragma unroll
         for (int k = 0; k < S; ++k) v[k] = V[c][k] - m;
-        exp_tabd_n<S>(G[c], v, etab);
+        exp_tabe_n<S>(G[c], v, etab);
       }
       double Z[CPL][S];
       // Z = A' G with A'[r][k] broadcast from lane (r S + k) / NA of the lane's DPP row:
@@ -233,7 +237,7 @@ void fb_bwd2_kernel(const SplitArgs p) {
         double lz[S];
 #pragma unroll
         for (int k = 0; k < S; ++k) zmin[c] = min(zmin[c], __double2hiint(Z[c][k]));
-        log_tabd_n<S>(lz, Z[c], ltab);
+        log_tabe_n<S>(lz, Z[c], ltab);
         double sv[S];
 #pragma unroll
         for (int k = 0; k < S; ++k) sv[k] = M[c] + lz[k];
@@ -291,13 +295,13 @@ void fb_bwd2_kernel(const SplitArgs p) {
       }
 #pragma unroll
       for (int k = 0; k < S; ++k) v1[k] -= m1;
-      exp_tabd_n<S>(ev, v1, etab);
+      exp_tabe_n<S>(ev, v1, etab);
       double zs = 0.0;
 #pragma unroll
       for (int k = 0; k < S; ++k) zs += ev[k];
       double lzs[1];
       const double zsa[1] = {zs};
-      log_tabd_n<1>(lzs, zsa, ltab);
+      log_tabe_n<1>(lzs, zsa, ltab);
       Y[c] = pb[c] * (m1 + lzs[0]);
     }
     bool bad = false;
@@ -338,11 +342,14 @@ void fb_bwd2_kernel(const SplitArgs p) {
 }
 
 // ---------------------------------------------------------------------------
+// one block of 4 x (waves per SIMD) waves per CU: the 32 KB of tables once per CU
+int bwd2_waves(int S) { return 4 * VBHEM_BWD2_WAVES(S); }
+
 size_t bwd2_lds(int S, int nwb) {
   if (S < 1 || S > kBwd2MaxS) return 0;
   const int CPL = S <= 8 ? 2 : 1, LPP = (S + CPL - 1) / CPL, PPW = 64 / LPP;
   const int XCS = (S + 1) / 2 * 2 + 2, XP = CPL * LPP * XCS + 2;
-  const int off_x = (kTabD + 2 * S + 1) / 2 * 2;
+  const int off_x = (2 * S + 1) / 2 * 2;  // dynamic part only: the tables are static
   const int ppb = nwb * PPW;
   return ((size_t)off_x + (size_t)ppb * XP + (ppb + 1) / 2 + 1) * sizeof(double);
 }

@@ -235,6 +235,7 @@ int split_resident_blocks(const SplitArgs &a, size_t lds);  // per CU, for a.mod
 // used: SB, K, S, T, nwb, i_begin/i_end/i_buf0, prior, A, logA, logPi, E, e_ld,
 // Atg, LL, flags.
 constexpr int kBwd2MaxS = 16;
+int bwd2_waves(int S);            // waves per block (one block per CU)
 size_t bwd2_lds(int S, int nwb);  // dynamic LDS bytes (0: S unsupported)
 int bwd2_ppb(int S, int nwb);     // pairs per block
 int bwd2_resident_blocks(int S, int nwb, size_t lds);

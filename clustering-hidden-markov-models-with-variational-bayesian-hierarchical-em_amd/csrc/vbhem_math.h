@@ -461,23 +461,26 @@ __host__ __device__ __forceinline__ void log_tabc_n(double (&y)[N], const double
 
 // ---- short-series variants for fb_bwd2_kernel (vbhem_fb_bwd.hip) ----
 // Fewer fp64 VALU operations per element for a kernel that is fp64-issue bound,
+// bought with larger LDS tables (16 KB each; the kernel's blocks are one per CU),
 // at an accuracy the backward recursion does not see (its log is added to the
 // column maximum and summed into L; its exp feeds A' G, dominated by the
-// max-term's 1):
-//   exp_tabd_n: exp_tabc_n with a one-constant reduction r = x - n ln2/256 (the
-//     double nearest ln 2 / 256 is 9.1e-20 away: 3.3e-17 |x| relative, at most
-//     0.3 ulp on [-1, 0] where the terms that matter live).  <= 2 ulp + 0.3 |x|
-//     ulp on [-700, 0]; x < -700 returns exp(-700).
-//   log_tabd_n: 512 intervals (1/1024 below 1, 1/512 above), {1/c, -log(1/c)} for
-//     every interval, |r| <= 2^-10, so the log1p series stops at r^5 (dropped
-//     terms < 2e-19).  Error <= 2 ulp + 3e-18 absolute (-log(1/c) rounded to a
-//     double, and no exact-r interval at 1: log(1) returns ~1e-19, not 0).
-constexpr int kLogTabDEntries = 512;
+// max-term's 1).  8 fp64 operations each:
+//   exp_tabe_n: 2^(j/2048) table (rounded), |r| <= ln2/4096, cubic; one-constant
+//     reduction r = x - n ln2/2048 (the double nearest ln2/2048 is 1.1e-20 away:
+//     3.3e-17 |x| relative, at most 0.3 ulp on [-1, 0] where the terms that
+//     matter live).  <= 2 ulp + 0.3 |x| ulp on [-700, 0]; x < -700 returns
+//     exp(-700) (the clamp keeps the exponent add normal).
+//   log_tabe_n: 1024 intervals (1/2048 below 1, 1/1024 above), {1/(2c), -log(1/c)}
+//     for every interval, |r| <= 2^-11, log1p series to r^4 (dropped terms <
+//     6e-18).  Error <= 2 ulp + 1e-17 absolute (-log(1/c) rounded to a double,
+//     no exact-r interval at 1: log(1) returns ~6e-18, not 0).
+constexpr int kExpTabEEntries = 2048;
+constexpr int kLogTabEEntries = 1024;
 
 template <int N>
-__host__ __device__ __forceinline__ void exp_tabd_n(double (&y)[N], const double (&xin)[N],
+__host__ __device__ __forceinline__ void exp_tabe_n(double (&y)[N], const double (&xin)[N],
                                                     const double *th) {
-  constexpr double kInvLn2N = 369.3299304675746, kLn2N = 0x1.62e42fefa39efp-9,
+  constexpr double kInvLn2N = 2954.639443740597, kLn2N = 0x1.62e42fefa39efp-12,
                    kShift = 0x1.8p52;
   double r[N], t[N];
   int k[N];
@@ -495,17 +498,17 @@ __host__ __device__ __forceinline__ void exp_tabd_n(double (&y)[N], const double
 #endif
     r[i] = fma(-n, kLn2N, x);
 #if defined(__HIP_DEVICE_COMPILE__)
-    // k opaque to the combiner: (ni >> 8) << 20 + hi stays v_ashrrev + v_lshl_add
+    // k opaque to the combiner: (ni >> 11) << 20 + hi stays v_ashrrev + v_lshl_add
     // instead of becoming shift, mask and add
-    asm("v_ashrrev_i32 %0, 8, %1" : "=v"(k[i]) : "v"(ni));
+    asm("v_ashrrev_i32 %0, 11, %1" : "=v"(k[i]) : "v"(ni));
 #else
-    k[i] = ni >> 8;
+    k[i] = ni >> 11;
 #endif
-    t[i] = th[ni & 255];
+    t[i] = th[ni & 2047];
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const double q = fma(fma(r[i], 1.0 / 24.0, 1.0 / 6.0), r[i], 0.5);
+    const double q = fma(r[i], 1.0 / 6.0, 0.5);
     const double p = fma(q, r[i] * r[i], r[i]);
     const double m = fma(t[i], p, t[i]);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -520,7 +523,7 @@ __host__ __device__ __forceinline__ void exp_tabd_n(double (&y)[N], const double
 }
 
 template <int N>
-__host__ __device__ __forceinline__ void log_tabd_n(double (&y)[N], const double (&z)[N],
+__host__ __device__ __forceinline__ void log_tabe_n(double (&y)[N], const double (&z)[N],
                                                     const double *tab) {
   constexpr double kLn2 = 0x1.62e42fefa39efp-1;
   double zz[N], ic[N], lc[N];
@@ -537,32 +540,33 @@ __host__ __device__ __forceinline__ void log_tabd_n(double (&y)[N], const double
     const unsigned lo = (unsigned)bits;
 #endif
     const unsigned t = hi - 0x3fe60000u;
-    const int idx = (int)((t >> 11) & 511u);
     k[i] = (int)t >> 20;
 #if defined(__HIP_DEVICE_COMPILE__)
     zz[i] = __hiloint2double((int)(hi - (t & 0xfff00000u)), lo);
     // byte offset of the 16-B entry straight from t: shift and mask, no scaling
-    const unsigned off = (t >> 7) & (511u << 4);
+    const unsigned off = (t >> 6) & (1023u << 4);
     const double2 e = *reinterpret_cast<const double2 *>(
         __builtin_assume_aligned(reinterpret_cast<const char *>(tab) + off, 16));
     ic[i] = e.x;
     lc[i] = e.y;
 #else
+    const int idx = (int)((t >> 10) & 1023u);
     const unsigned long long zb = ((unsigned long long)(hi - (t & 0xfff00000u)) << 32) | lo;
     __builtin_memcpy(&zz[i], &zb, 8);
     ic[i] = tab[2 * idx];
     lc[i] = tab[2 * idx + 1];
 #endif
   }
+  // with s = r / 2 (the table holds 1/(2c)): log1p(r) = 2s + s^2 (-2 + s (8/3 - 4s)),
+  // every fma with at most one non-inline constant (gfx9 VOP3 takes no literal)
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const double r = fma(zz[i], ic[i], -1.0);
+    const double sh = fma(zz[i], ic[i], -0.5);
     const double w = fma((double)k[i], kLn2, lc[i]);
-    const double r2 = r * r;
-    double q = fma(r, 1.0 / 5.0, -1.0 / 4.0);
-    q = fma(q, r, 1.0 / 3.0);
-    q = fma(q, r, -0.5);
-    y[i] = fma(q, r2, r) + w;
+    const double s2 = sh * sh;
+    double q = fma(sh, -4.0, 8.0 / 3.0);
+    q = fma(q, sh, -2.0);
+    y[i] = fma(q, s2, fma(sh, 2.0, w));
   }
 }
 

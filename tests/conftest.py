@@ -141,10 +141,10 @@ def mathcheck():
     lib.logtab_host.restype = None
     lib.logtab_device.argtypes = [ctypes.c_int, dp, dp, dp]
     lib.logtab_device.restype = ctypes.c_int
-    for name in ("logtabf_host", "logtabc_host", "logtabd_host"):
+    for name in ("logtabf_host", "logtabc_host", "logtabe_host"):
         getattr(lib, name).argtypes = [ctypes.c_int, dp, dp, dp]
         getattr(lib, name).restype = None
-    for name in ("logtabf_device", "logtabc_device", "logtabd_device"):
+    for name in ("logtabf_device", "logtabc_device", "logtabe_device"):
         getattr(lib, name).argtypes = [ctypes.c_int, dp, dp, dp]
         getattr(lib, name).restype = ctypes.c_int
     return lib

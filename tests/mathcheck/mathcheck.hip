@@ -18,8 +18,10 @@ struct CompactTabs {
   double e[vbhem::kExpTabEntries];
   double l[2 * vbhem::kLogTabEntries];
 };
-static const double kLog512Host[2 * vbhem::kLogTabDEntries] = VBHEM_LOG512_TABLE_INIT;
-__device__ const double kLog512Dev[2 * vbhem::kLogTabDEntries] = VBHEM_LOG512_TABLE_INIT;
+static const double kLogEHost[2 * vbhem::kLogTabEEntries] = VBHEM_LOG1024_TABLE_INIT;
+__device__ const double kLogEDev[2 * vbhem::kLogTabEEntries] = VBHEM_LOG1024_TABLE_INIT;
+static const double kExpEHost[vbhem::kExpTabEEntries] = VBHEM_EXP2048_TABLE_INIT;
+__device__ const double kExpEDev[vbhem::kExpTabEEntries] = VBHEM_EXP2048_TABLE_INIT;
 static CompactTabs compact_host() {
   CompactTabs c;
   for (int j = 0; j < vbhem::kExpTabEntries; ++j) c.e[j] = kExpTabHost[2 * j];
@@ -52,19 +54,19 @@ __global__ void logtabc_kernel(int n, const double* __restrict__ x, double* __re
   }
 }
 
-__global__ void logtabd_kernel(int n, const double* __restrict__ x, double* __restrict__ l,
+__global__ void logtabe_kernel(int n, const double* __restrict__ x, double* __restrict__ l,
                                double* __restrict__ e) {
-  __shared__ __attribute__((aligned(16))) double lt[2 * vbhem::kLogTabDEntries];
-  __shared__ __attribute__((aligned(16))) double et[vbhem::kExpTabEntries];
-  for (int k = threadIdx.x; k < vbhem::kExpTabEntries; k += blockDim.x) et[k] = kExpTabDev[2 * k];
-  for (int k = threadIdx.x; k < 2 * vbhem::kLogTabDEntries; k += blockDim.x) lt[k] = kLog512Dev[k];
+  __shared__ __attribute__((aligned(16))) double lt[2 * vbhem::kLogTabEEntries];
+  __shared__ __attribute__((aligned(16))) double et[vbhem::kExpTabEEntries];
+  for (int k = threadIdx.x; k < vbhem::kExpTabEEntries; k += blockDim.x) et[k] = kExpEDev[k];
+  for (int k = threadIdx.x; k < 2 * vbhem::kLogTabEEntries; k += blockDim.x) lt[k] = kLogEDev[k];
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     double y[1], z[1] = {x[i]}, m[1] = {-x[i]};
-    vbhem::log_tabd_n<1>(y, z, lt);
+    vbhem::log_tabe_n<1>(y, z, lt);
     l[i] = y[0];
-    vbhem::exp_tabd_n<1>(y, m, et);
+    vbhem::exp_tabe_n<1>(y, m, et);
     e[i] = y[0];
   }
 }
@@ -140,13 +142,12 @@ void logtabc_host(int n, const double* x, double* l, double* e) {
 }
 
 // short-series pair of fb_bwd2_kernel: log at x, exp at -x
-void logtabd_host(int n, const double* x, double* l, double* e) {
-  static const CompactTabs c = compact_host();
+void logtabe_host(int n, const double* x, double* l, double* e) {
   for (int i = 0; i < n; i++) {
     double y[1], z[1] = {x[i]}, m[1] = {-x[i]};
-    vbhem::log_tabd_n<1>(y, z, kLog512Host);
+    vbhem::log_tabe_n<1>(y, z, kLogEHost);
     l[i] = y[0];
-    vbhem::exp_tabd_n<1>(y, m, c.e);
+    vbhem::exp_tabe_n<1>(y, m, kExpEHost);
     e[i] = y[0];
   }
 }
@@ -160,7 +161,7 @@ static int logtab_device_impl(int n, const double* x, double* l, double* e, int 
   if (st == hipSuccess) st = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
   if (st == hipSuccess && n > 0) {
     if (fast == 2) logtabc_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
-    else if (fast == 3) logtabd_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
+    else if (fast == 3) logtabe_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
     else logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de, fast);
     st = hipGetLastError();
   }
@@ -184,7 +185,7 @@ int logtabc_device(int n, const double* x, double* l, double* e) {
   return logtab_device_impl(n, x, l, e, 2);
 }
 
-int logtabd_device(int n, const double* x, double* l, double* e) {
+int logtabe_device(int n, const double* x, double* l, double* e) {
   return logtab_device_impl(n, x, l, e, 3);
 }
 
