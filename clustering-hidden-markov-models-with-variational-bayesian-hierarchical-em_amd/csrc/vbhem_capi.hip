@@ -754,6 +754,16 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     if (rc != VBHEM_OK) return rc;
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     sa.assign = gated && g0 == 0;
+    // the emission GEMM's operand for this group (prepared, or built by run_fb)
+    sa.U = nullptr;
+    if (ctx.split.ok && ctx.use_u) {
+      sa.ukdp = ctx.em.kdp;
+      if (base->U) {
+        sa.U = base->U; sa.uz = base->U; sa.u_col0 = 0;
+      } else if (ctx.u_ws) {
+        sa.U = ctx.u_ws; sa.uz = ctx.em.shift; sa.u_col0 = (long long)g0 * SB / 16 * 16;
+      }
+    }
     const int nchunk = std::max(1, chunks(g1 - g0));
     hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
     e = vbhem::launch_resp(sa, nchunk, st);

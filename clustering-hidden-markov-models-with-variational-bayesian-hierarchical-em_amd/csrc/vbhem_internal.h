@@ -115,6 +115,12 @@ struct StatsArgs {
   int assign;      // gated schedule, first group: write the slab entries instead of adding
   int KT, SL;      // batched trials: clusters per trial (K = R * KT) and the per-trial
                    // statistics length; slab = R sections of SL (KT = K, SL = slab_len: one)
+  // the emission GEMM's prepared operand for the bases of this call (null: not built);
+  // stats_list_u_kernel reads the emission moments from it instead of the covariances
+  const double *U, *uz;  // operand, its shift z (d doubles)
+  long long u_col0;      // first column of U
+  int ukdp;              // k-extent of U (multiple of 4)
+  int nzero;             // stats_list_u_kernel with assign: slabs [gridDim.x, nzero) get zeros
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).

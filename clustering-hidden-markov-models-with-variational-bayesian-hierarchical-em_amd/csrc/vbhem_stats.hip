@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "vbhem_internal.h"
 
@@ -793,6 +794,203 @@ hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
   return launch_stats_t<16>(a, nchunk, ngroups, lds, st);
 }
 
+// ---------------------------------------------------------------------------
+// stats_list_u_kernel<FPL, SM>: stats_list_kernel on the emission GEMM's prepared
+// operand U (vbhem_emission.hip: per base-state column the features
+// [Sigma_ab + Sigma_ba + 2 mu'_a mu'_b (a < b) | Sigma_aa + mu'_a^2, mu'], mu' = mu - z),
+// so the emission moments need no gather of the d x d covariances and no
+// per-element rebuild.  Block (c, j) = part c of cluster j's list, as
+// stats_list_kernel; wave w takes the part's pairs w, w + 4, ...:
+//   lane f (+ 64 q) owns moment column f = 0 (ones) | 1 + a (mu_a) | 1 + d + k (packed
+//   (a, b) of Sigma + mu mu') for every state s: acc[q][s] += sum_b Z tnu(s, b) u(b, f),
+//   with Z tnu and the pair's U columns staged per pair in a wave-private LDS slab (U
+//   read coalesced: lanes over (k-step, k, base state), SB contiguous columns per row);
+//   sum_xi / sum_nu_1 accumulate lane-parallel from global memory.
+// Waves reduce in fixed order (bit-reproducible), then every output is shifted back:
+//   mu_a = m'_a + z_a N,  (Sigma + mu mu')_ab = Q'_ab + z_a m'_b + z_b m'_a + z_a z_b N
+// (Q' = half the off-diagonal feature), N = sum Z tnu, m' = sum Z tnu mu'.
+// ---------------------------------------------------------------------------
+constexpr int kSuWaves = 4;
+
+template <int FPL, int SM>
+__global__ __launch_bounds__(64 * kSuWaves) void stats_list_u_kernel(const StatsArgs p) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU, kq = p.ukdp / 4;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d;
+  const int j = blockIdx.y, c = blockIdx.x, nch = gridDim.x;
+  const int OT = S * SB, TS = (OT + 1) / 2 * 2, KP = p.ukdp + 1;
+  const int WS = TS + (SB * KP + 1) / 2 * 2;
+  double *tw = lds + (size_t)wave * WS;                 // [SB][S] Z tnu of the wave's pair
+  double *uw = tw + TS;                                 // [SB][KP] its U columns
+  double *red = lds + (size_t)kSuWaves * WS;           // [S][NU] | [S] | [S][S]
+  double *zs = red + (size_t)S * NU + S + S * S;       // [d]
+  for (int a = tid; a < d; a += 64 * kSuWaves) zs[a] = p.uz[a];
+  // my moment columns: U feature (-1: the ones column), valid
+  int ue[FPL];
+  bool fv[FPL];
+#pragma unroll
+  for (int q = 0; q < FPL; ++q) {
+    const int f = lane + 64 * q;
+    fv[q] = f < NU;
+    ue[q] = f == 0 ? -1 : f <= d ? NPF + f - 1 : f - 1 - d;
+  }
+  double acc[FPL][SM], accx[4], accn = 0.0;
+#pragma unroll
+  for (int q = 0; q < FPL; ++q)
+#pragma unroll
+    for (int s2 = 0; s2 < SM; ++s2) acc[q][s2] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) accx[e] = 0.0;
+  const int tot = p.list_tot[j];
+  const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
+  const int *lst = p.list + (size_t)j * p.list_cap;
+  const double *Ub0 = p.U + kUHead;
+  for (int nb = n0 + wave; nb < n1; nb += 64 * kSuWaves) {
+    // the bases of the next 64 pairs of this wave, one per lane
+    const int nl = nb + lane * kSuWaves;
+    const int il = nl < n1 ? lst[nl] : 0;
+    const int np = min(64, (n1 - nb + kSuWaves - 1) / kSuWaves);
+    for (int k = 0; k < np; ++k) {
+      const int i = __builtin_amdgcn_readlane(il, k);
+      const size_t lp = (size_t)(i - p.i_buf0) * K + j;
+      const double z = p.Z[lp];
+      // every load of the pair in flight before the first LDS write (a plain loop
+      // waits on each load before its store)
+      {
+        double v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int x = lane + 64 * e;
+          v[e] = x < OT ? p.tnu[lp * OT + x] : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int x = lane + 64 * e;
+          if (x < OT) {
+            const int s2 = x / SB, b = x - s2 * SB;
+            tw[b * S + s2] = z * v[e];
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int x = lane + 64 * e;
+        if (x < S * S) accx[e] = fma(z, p.xi[lp * S * S + x], accx[e]);
+      }
+      if (lane < S) accn = fma(z, p.nu1[lp * S + lane], accn);
+      const long long c0 = (long long)i * SB - p.u_col0;
+      for (int x0 = lane; x0 < 4 * kq * SB; x0 += 64 * 8) {
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int x = x0 + 64 * e;
+          const int t4 = x / SB, b = x - t4 * SB;  // t4 = 4 t + k: feature e
+          const long long col = c0 + b;
+          v[e] = x < 4 * kq * SB
+                     ? Ub0[(size_t)(col >> 4) * kq * 64 + (t4 >> 2) * 64 + (t4 & 3) * 16 + (col & 15)]
+                     : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int x = x0 + 64 * e;
+          const int t4 = x / SB, b = x - t4 * SB;
+          if (x < 4 * kq * SB) uw[b * KP + t4] = v[e];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int b = 0; b < SM; ++b) {
+        if (b < SB) {
+          double uv[FPL];
+#pragma unroll
+          for (int q = 0; q < FPL; ++q)
+            uv[q] = !fv[q] ? 0.0 : ue[q] < 0 ? 1.0 : uw[b * KP + ue[q]];
+#pragma unroll
+          for (int s2 = 0; s2 < SM; ++s2) {
+            if (s2 < S) {
+              const double tv = tw[b * S + s2];
+#pragma unroll
+              for (int q = 0; q < FPL; ++q) acc[q][s2] = fma(tv, uv[q], acc[q][s2]);
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  // fixed-order reduction over the waves
+  for (int w = 0; w < kSuWaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < FPL; ++q)
+#pragma unroll
+        for (int s2 = 0; s2 < SM; ++s2) {
+          const int f = lane + 64 * q;
+          if (fv[q] && s2 < S) {
+            double *r = red + (size_t)s2 * NU + f;
+            *r = w == 0 ? acc[q][s2] : *r + acc[q][s2];
+          }
+        }
+      if (lane < S) {
+        double *r = red + (size_t)S * NU + lane;
+        *r = w == 0 ? accn : *r + accn;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int x = lane + 64 * e;
+        if (x < S * S) {
+          double *r = red + (size_t)S * NU + S + x;
+          *r = w == 0 ? accx[e] : *r + accx[e];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int KT = p.KT, tr = j / KT, jt = j - tr * KT;
+  double *tsl = p.slabs + (size_t)c * p.slab_len + (size_t)tr * p.SL;
+  const int NO = S * NU + S + S * S;
+  for (int o = tid; o < NO; o += 64 * kSuWaves) {
+    double v;
+    double *dst;
+    if (o < S * NU) {
+      const int s2 = o / NU, f = o - s2 * NU;
+      const double *rs = red + (size_t)s2 * NU;
+      const double N = rs[0];
+      if (f == 0) {
+        v = N;
+      } else if (f <= d) {
+        v = fma(zs[f - 1], N, rs[f]);
+      } else {
+        int a = f - 1 - d, b = a;
+        if (full) {
+          int k = a;
+          a = 0;
+          while (k >= d - a) { k -= d - a; ++a; }
+          b = a + k;
+        }
+        const double q2 = (full && a != b) ? 0.5 * rs[f] : rs[f];
+        v = q2 + (zs[a] * rs[1 + b] + zs[b] * rs[1 + a]) + zs[a] * zs[b] * N;
+      }
+      dst = tsl + KT + (size_t)KT * S + (size_t)KT * S * S + 2 + (size_t)jt * S * NU + o;
+    } else if (o < S * NU + S) {
+      v = red[o];
+      dst = tsl + KT + (size_t)jt * S + (o - S * NU);
+    } else {
+      v = red[o];
+      dst = tsl + KT + (size_t)KT * S + (size_t)jt * S * S + (o - S * NU - S);
+    }
+    *dst = p.assign ? v : *dst + v;
+    if (p.assign)  // the slabs past this grid's chunks hold nothing of cluster j
+      for (int cz = c + nch; cz < p.nzero; cz += nch) dst[(size_t)(cz - c) * p.slab_len] = 0.0;
+  }
+}
+
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st) {
   const size_t lds = ((size_t)2 * a.K + kListThreads / 64 + 2 * kListThreads) * sizeof(int);
   hipLaunchKernelGGL(gate_list_kernel, dim3(nchunk), dim3(kListThreads), lds, st, a);
@@ -817,9 +1015,47 @@ bool plan_stats_list(StatsArgs &a, size_t &lds) {
   return a.PB >= 1;
 }
 
+template <int FPL, int SM>
+static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  const int OT = a.S * a.SB, KP = a.ukdp + 1;
+  const size_t ws = (size_t)(OT + 1) / 2 * 2 + ((size_t)a.SB * KP + 1) / 2 * 2;
+  const size_t lds = ((size_t)kSuWaves * ws + (size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) *
+                     sizeof(double);
+  auto *fn = &stats_list_u_kernel<FPL, SM>;
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fn, grid, dim3(64 * kSuWaves), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int FPL>
+static hipError_t launch_su_s(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  if (a.S <= 4) return launch_su<FPL, 4>(a, grid, st);
+  if (a.S <= 8) return launch_su<FPL, 8>(a, grid, st);
+  if (a.S <= 12) return launch_su<FPL, 12>(a, grid, st);
+  return launch_su<FPL, 16>(a, grid, st);
+}
+
 hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st) {
   const int NO = a.S + a.S * a.S + a.S * a.NU;
   const dim3 grid(nchunk, a.K);
+  // on the prepared operand when the call has one (S <= 16: the split kernel's range)
+  if (a.U && a.S <= 16 && a.SB <= a.S && a.NU <= 3 * 64 && !std::getenv("VBHEM_NO_STATS_U")) {
+    StatsArgs b = a;
+    b.nzero = nchunk;
+    // the per-block cost (wave reduction, slab writes) grows with the output count NO:
+    // at most ~4M block outputs per launch (C4: 512 x 16 blocks of 432, C5: 64 x 32 of
+    // 1992 -- measured: 16384 blocks of 1992 ran 1.3x slower than 2048)
+    const long long NOb = (long long)a.S + (long long)a.S * a.S + (long long)a.S * a.NU;
+    long long cap = (4ll << 20) / (NOb * std::max(1, a.K));
+    if (const char *ev = std::getenv("VBHEM_SU_BLOCKS"))  // A/B
+      cap = std::atoi(ev) / std::max(1, a.K);
+    const int nb = (int)std::max(1ll, std::min((long long)nchunk, cap));
+    const dim3 g2(nb, a.K);
+    if (a.NU <= 64) return launch_su_s<1>(b, g2, st);
+    if (a.NU <= 128) return launch_su_s<2>(b, g2, st);
+    return launch_su_s<3>(b, g2, st);
+  }
   if (NO <= 4 * kSlThreads) {
     hipLaunchKernelGGL((stats_list_kernel<4>), grid, dim3(kSlThreads), lds, st, a);
   } else {

@@ -109,3 +109,32 @@ def test_prepared_operand_layout(vb):
     last = ncols - 16 * (ntile - 1)
     assert np.all(tiles[-1, :, :, last:] == 0.0)
     del _capi
+
+
+@pytest.mark.parametrize("name", ["full_d8", "full_d16", "diag_d12", "full_d2_face"])
+@pytest.mark.parametrize("prepare", [True, False])
+def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
+    """Gated statistics from the prepared operand (stats_list_u_kernel: moments read from
+    U and shifted back by z) vs the covariance gather (stats_list_kernel), with several
+    base groups (the second group adds into the slabs) and fewer blocks than chunks (the
+    first group zero-fills the slabs past its grid)."""
+    from vbhem_amd import host
+    from vbhem_amd.estep import EStepEngine
+    N, K, S, Sb, d, cov, extra = SHAPES[name]
+    N = max(N, 40)
+    cs = make_case(N, K, S, Sb, d, cov, seed=11 + len(name), **extra)
+    monkeypatch.setenv("VBHEM_GROUP_BASES", str(N // 2 + 1))
+    outs = []
+    for env in ({"VBHEM_NO_STATS_U": "1"}, {}, {"VBHEM_SU_BLOCKS": str(K)}):
+        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        eng = EStepEngine(cs["bs"], K, S, cs["T"], device=DEV, prepare=prepare)
+        eng.set_clusters(cs["consts"])
+        eng.set_log_omega(host.log_omega_tilde(cs["P"].alpha))
+        st = eng.fused((100.0 * N) * eng.base.omega).cpu().numpy()
+        outs.append(st)
+    assert np.isfinite(outs[0]).all()
+    for st in outs[1:]:
+        assert stat_err(st, outs[0]) < 1e-10, (name, prepare, stat_err(st, outs[0]))
