@@ -175,6 +175,9 @@ struct SplitPlan {
   size_t lds_bwd = 0;   // kFbBackward (no lattice)
   size_t lds_list = 0;  // kFbList (lattice + work-item prefix)
   int ppb = 0;
+  // kFbList: its own geometry (up to 8 waves per block, compact tables in LDS)
+  vbhem::SplitArgs al{};
+  size_t lds_l = 0;
 };
 
 // Geometry of fb_split_kernel; must match SplitLayout<S, LPC> (vbhem_internal.h).
@@ -215,6 +218,36 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T, int LPC) {
       sp.lds_list = lds_list;
       sp.ppb = ppb;
       sp.ok = true;
+    }
+  }
+  // list mode: the lattice dominates LDS and the kernel runs 2 waves per SIMD, so the
+  // most waves per CU come from one 8-wave block (C4: 156 KB) rather than 4-wave
+  // blocks that no longer pair up once the 4 KB of tables are added
+  int best_w = 0;
+  for (int nwb : {8, 4, 2, 1}) {
+    if (!sp.ok) break;
+    const int NT = nwb * 64;
+    const int ppb = NT / LPP;
+    if (ppb < 1) continue;
+    const int off_Y = OFF_X + ppb * XP;
+    const int off_F = (off_Y + ppb * S + 1) / 2 * 2;
+    const int off_R = (off_F + (ppb + 1) / 2 + 1) / 2 * 2;
+    const size_t lattice = (size_t)std::max(0, T - 2) * SH * NT;
+    const size_t xi_park = S > 8 ? (size_t)ppb * S * S * LPC * SH : 0;
+    const size_t region = std::max<size_t>(std::max(lattice, xi_park), 2);
+    const int off_L = (int)(off_R + region);
+    const int off_T = (off_L + (K + 2) / 2 + 1) / 2 * 2;
+    const size_t lds = ((size_t)off_T + vbhem::kExpTabEntries + 2 * vbhem::kLogTabEntries) * sizeof(double);
+    if (lds > kLdsLimit) continue;
+    const int waves = std::min(8, nwb * (int)(kLdsLimit / lds));
+    if (waves > best_w) {
+      best_w = waves;
+      vbhem::SplitArgs x = sp.a;
+      x.nwb = nwb;
+      x.off_Y = off_Y; x.off_F = off_F; x.off_R = off_R; x.off_L = off_L; x.off_T = off_T;
+      x.mode = vbhem::kFbList;
+      sp.al = x;
+      sp.lds_l = lds;
     }
   }
   return sp;
@@ -388,6 +421,8 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
   if (c.split.ok) {
     vbhem::SplitArgs &a = c.split.a;
     a.prior = b->prior; a.A = b->A; a.logA = cl->logA; a.logPi = cl->logPi;
+    vbhem::SplitArgs &al = c.split.al;
+    al.prior = b->prior; al.A = b->A; al.logA = cl->logA; al.logPi = cl->logPi;
     vbhem::SplitArgs &ab = c.bwd.a;
     ab.prior = b->prior; ab.A = b->A; ab.logA = cl->logA; ab.logPi = cl->logPi;
     if (c.bwd.ok && cl->S <= vbhem::kBwd2MaxS && !std::getenv("VBHEM_NO_BWD2")) {
@@ -426,7 +461,8 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
                 hipStream_t st) {
   if (i_end <= i_begin) return VBHEM_OK;
   // flags[0] is zero here: the backward pass's fb_exact_kernel reset it
-  vbhem::SplitArgs ca = c.split.a;
+  if (!c.split.lds_l) return fail(VBHEM_ERR_UNSUPPORTED, "gate-list pass does not fit LDS");
+  vbhem::SplitArgs ca = c.split.al;
   ca.mode = vbhem::kFbList;
   ca.E = Ebuf; ca.e_ld = e_ld;
   ca.i_begin = i_begin; ca.i_end = i_end; ca.i_buf0 = i_buf0;
@@ -434,7 +470,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
   ca.list = list; ca.list_tot = list_tot; ca.list_cap = list_cap;
   hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
-  hipError_t e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_list), c.split.lds_list, st);
+  hipError_t e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_l), c.split.lds_l, st);
   if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
   if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
   vbhem::FbArgs a = c.plan.a;
@@ -719,7 +755,7 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   ctx.u_ws = w.U;
   // gated schedule: split kernel + list statistics tile must apply
   size_t sl_lds = 0;
-  const bool gated = g_fused_mode == VBHEM_FUSED_GATED && ctx.split.ok &&
+  const bool gated = g_fused_mode == VBHEM_FUSED_GATED && ctx.split.ok && ctx.split.lds_l &&
                      vbhem::plan_stats_list(sa, sl_lds);
   if (R > 1 && !gated)
     return fail(VBHEM_ERR_UNSUPPORTED,

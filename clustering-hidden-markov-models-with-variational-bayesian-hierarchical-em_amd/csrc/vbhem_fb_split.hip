@@ -187,7 +187,7 @@ __device__ __forceinline__ void load_row(double (&dst)[SH], const double *row, i
 // List mode: the gated pairs of every cluster cut into PPB-pair work items,
 // contiguous item ranges per block (cluster constants restaged when j changes).
 template <int S, int LPC, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kFbBackward ? VBHEM_BWD_WAVES(S) : 2)))
+__global__ __launch_bounds__(MODE == kFbList ? 512 : 256) __attribute__((amdgpu_waves_per_eu(MODE == kFbBackward ? VBHEM_BWD_WAVES(S) : 2)))
 void fb_split_kernel(const SplitArgs p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using LY = SplitLayout<S, LPC>;
@@ -195,7 +195,8 @@ void fb_split_kernel(const SplitArgs p) {
   constexpr int LPP = S * LPC;  // lanes per pair
   constexpr bool kWaveLocal = (LPP & (LPP - 1)) == 0;  // pairs never straddle a wave
   constexpr bool kFwd = MODE != kFbBackward;
-  constexpr bool kTab = MODE == kFbBackward;  // table-driven log (LDS table)
+  constexpr bool kTab = MODE != kFbDense;  // tables in LDS (list mode: the compact pair)
+  constexpr bool kTabC = MODE == kFbList;   // exp_tabc_n / log_tabc_n on 4 KB of tables
   const int tid = threadIdx.x;
   const int NT = p.nwb * 64;
   const int PPB = NT / LPP;
@@ -207,10 +208,12 @@ void fb_split_kernel(const SplitArgs p) {
   double *lpi = amax + S;        // [S]
   double *R = lds + p.off_R;     // lattice [(T-2)][SH][NT]
   int *F = reinterpret_cast<int *>(lds + p.off_F);  // [PPB] fallback flags
-  // backward mode: the tables staged in LDS; the other modes (LDS taken by the
-  // lattice) read them from global memory (8 KB, L1/L2-resident)
-  const double *ltab = kTab ? lds + p.off_T : kLogTab;  // [kLogTabDoubles]
-  const double *etab = kTab ? lds + p.off_T + kLogTabDoubles : kExpTab;  // [kExpTabDoubles]
+  // backward mode: the padded tables staged in LDS; list mode: the compact ones
+  // (exp 2^(j/256) [256] | log {1/c, log c} [128][2]: 4 KB next to the lattice, one
+  // 8-wave block per CU); dense mode (LDS taken by the lattice) reads them from
+  // global memory (8 KB, L1/L2-resident)
+  const double *ltab = kTabC ? lds + p.off_T + kExpTabEntries : kTab ? lds + p.off_T : kLogTab;
+  const double *etab = kTabC ? lds + p.off_T : kTab ? lds + p.off_T + kLogTabDoubles : kExpTab;
 
   // ---------------- cluster constants: A' = exp(logA - rowmax), rowmax, logPi --------------
   auto stage_cluster = [&](int j) {
@@ -321,7 +324,8 @@ void fb_split_kernel(const SplitArgs p) {
         double ex[SH];
 #pragma unroll
         for (int k = 0; k < SH; ++k) ex[k] = (E[k] + L[k]) - M;
-        exp_tabf_n<SH>(G, ex, etab);
+        if constexpr (kTabC) exp_tabc_n<SH>(G, ex, etab);
+        else exp_tabf_n<SH>(G, ex, etab);
       }
       // partial Z for every owner's rows, then reduce-scatter
       double Pz[LPC * SH];
@@ -357,7 +361,8 @@ void fb_split_kernel(const SplitArgs p) {
         bad |= bvalid && rv && !(Z[k] >= kZMinS);
         zz[k] = rv ? Z[k] : 1.0;
       }
-      log_tabf_n<SH>(lz, zz, ltab);
+      if constexpr (kTabC) log_tabc_n<SH>(lz, zz, ltab);
+      else log_tabf_n<SH>(lz, zz, ltab);
 #pragma unroll
       for (int k = 0; k < SH; ++k) sv[k] = M + am[k] + lz[k];
       if (kFwd && t <= T - 2) {
@@ -446,7 +451,9 @@ void fb_split_kernel(const SplitArgs p) {
           double ex[SH];
 #pragma unroll
           for (int k = 0; k < SH; ++k) ex[k] = E[k] - M;
-          exp_tabf_n<SH>(G, ex, etab);  // the backward sweep's G_{T-1}, bit for bit
+          // the backward sweep's G_{T-1}, bit for bit
+          if constexpr (kTabC) exp_tabc_n<SH>(G, ex, etab);
+          else exp_tabf_n<SH>(G, ex, etab);
         } else {
           const double *slot = R + (size_t)(t - 1) * SH * NT + tid;
 #pragma unroll
@@ -616,6 +623,11 @@ void fb_split_kernel(const SplitArgs p) {
       run_pair(j, p.i_begin + tile * PPB, p.i_end, nullptr, -1);
   } else {
     // work items: cluster j owns ceil(list_tot[j] / PPB) consecutive items
+    for (int x = tid; x < kExpTabEntries; x += NT) lds[p.off_T + x] = kExpTab[2 * x];
+    for (int x = tid; x < kLogTabEntries; x += NT) {
+      lds[p.off_T + kExpTabEntries + 2 * x] = kLogTab[4 * x];
+      lds[p.off_T + kExpTabEntries + 2 * x + 1] = kLogTab[4 * x + 1];
+    }
     int *pre = reinterpret_cast<int *>(lds + p.off_L);  // [K + 1]
     if (tid == 0) {
       int s = 0;
