@@ -98,7 +98,7 @@ namespace {
 constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
 constexpr int kExactThreads = vbhem::kExactBlock * vbhem::kExactBlocks;  // fallback threads
-constexpr int kChunkMinBases = 32;                 // fused epilogue: bases per chunk, at least
+constexpr int kChunkMinBases = 64;                 // fused epilogue: bases per chunk, at least
 constexpr size_t kGroupBudget = (size_t)8 << 30;  // per-pair buffers per group (fused)
 constexpr int kMaxSlabs = 512;    // statistics chunks (= resp/stats blocks per group)
 

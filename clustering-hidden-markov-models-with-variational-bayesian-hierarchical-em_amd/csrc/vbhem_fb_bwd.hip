@@ -157,7 +157,11 @@ void fb_bwd2_kernel(const SplitArgs p) {
   const bool valid = qw < PPW;
   const int q = wave * PPW + (valid ? qw : 0);
   double *X = Xall + (size_t)q * LY::XP;
-  const int ntile = (p.i_end - p.i_begin + PPB - 1) / PPB;
+  // wave-granular tiles of PPW pairs, dealt wave-major over the cluster's NB blocks
+  // (wave w of block t0 takes tiles w NB + t0, + NB NW, ...): the tiles left over
+  // past a whole number of rounds land one per CU instead of all on the first
+  // blocks' CUs (small shards: 12 500 bases = 4.07 rounds ran as 5)
+  const int ntile = (p.i_end - p.i_begin + PPW - 1) / PPW;
   // A' spread over the 16 lanes of every DPP row: entry e = r S + k in register e % NA
   // of row lane e / NA (16 NA >= S^2)
   double aq[NA];
@@ -167,8 +171,8 @@ void fb_bwd2_kernel(const SplitArgs p) {
     aq[x] = e < S * S ? p.Atg[(size_t)j * S * S + e] : 0.0;
   }
 
-  for (int tile = t0; tile < ntile; tile += NB) {
-    const int i = p.i_begin + tile * PPB + q;
+  for (int tile = wave * NB + t0; tile < ntile; tile += NB * NW) {
+    const int i = p.i_begin + tile * PPW + (valid ? qw : 0);
     const bool active = valid && i < p.i_end;
     const int ic = active ? i : p.i_begin;
     if (valid && w == 0) F[q] = 0;
