@@ -657,7 +657,12 @@ void fb_split_kernel(const SplitArgs p) {
       const int jj = jn;
       const int icur = inext;
       if (wi + 1 < w1) inext = item(wi + 1, jj, jn);  // next item's base: in flight now
-      __syncthreads();  // previous item's LDS traffic (slabs, lattice, parked H) done
+      // a block barrier only where LDS is shared across waves: the cluster constants
+      // (restaged when the cluster changes) and, for S > 8, the parked H blocks; slabs,
+      // flags and lattice are wave-private (pairs never straddle a wave), so the waves
+      // otherwise drift apart and one wave's load stall at an item start hides behind
+      // the other's compute
+      if (!(kWaveLocal && S <= 8) || jj != jcur) __syncthreads();
       if (jj != jcur) {
         stage_cluster(jj);
         jcur = jj;
