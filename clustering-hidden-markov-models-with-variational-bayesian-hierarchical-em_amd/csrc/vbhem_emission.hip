@@ -639,6 +639,9 @@ hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st) {
 #ifndef UNWAVE_CHUNKED
 #define UNWAVE_CHUNKED 4
 #endif
+#ifndef UNWAVE_SINGLE
+#define UNWAVE_SINGLE 4  // 133 VGPRs at kq <= 12: 3 waves per SIMD, 4-wave blocks use them all
+#endif
 bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   const int kq = a.kdp / 4;
   if (kq > kUMaxKq) {
@@ -649,7 +652,7 @@ bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   a.urc = kq <= 12 ? 8 : 4;   // ksp / 16 is a multiple of 8: RC divides it
   // chunked W' (restaged every round): 4-wave blocks, two per CU, so one block's
   // staging overlaps the other's MFMAs
-  a.nwave = a.ksp / 16 > a.urc ? UNWAVE_CHUNKED : 8;
+  a.nwave = a.ksp / 16 > a.urc ? UNWAVE_CHUNKED : UNWAVE_SINGLE;
   lds = ((size_t)kq * a.urc * 64 + (size_t)a.urc * 16) * sizeof(double);
   return true;
 }
