@@ -181,10 +181,18 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # one rank per GPU over RCCL ("nccl"); VBHEM_BENCH_BACKEND=gloo rehearses the
+    # multi-rank path with several ranks sharing the GPUs there are (host-staged)
+    backend = os.environ.get("VBHEM_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import pkgload
     vb = pkgload.load()
