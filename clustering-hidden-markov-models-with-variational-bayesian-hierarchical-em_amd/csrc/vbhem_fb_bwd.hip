@@ -170,6 +170,14 @@ void fb_bwd2_kernel(const SplitArgs p) {
     const int e = NA * (lane & 15) + x;
     aq[x] = e < S * S ? p.Atg[(size_t)j * S * S + e] : 0.0;
   }
+  // A'[r][0], block-uniform: scalar loads once, kept in SGPRs
+  double a0[S];
+  {
+    typedef const double __attribute__((address_space(4))) cdouble;
+    const cdouble *Ag = (const cdouble *)(p.Atg + (size_t)j * S * S);
+#pragma unroll
+    for (int r = 0; r < S; ++r) a0[r] = Ag[r * S];
+  }
 
   for (int tile = wave * NB + t0; tile < ntile; tile += NB * NW) {
     const int i = p.i_begin + tile * PPW + (valid ? qw : 0);
@@ -226,15 +234,18 @@ void fb_bwd2_kernel(const SplitArgs p) {
       }
       double Z[CPL][S];
       // Z = A' G with A'[r][k] broadcast from lane (r S + k) / NA of the lane's DPP row:
-      // no scalar loads, no LDS (sums in k order, as fma chains)
+      // no LDS (sums in k order, as fma chains); each chain starts with a plain
+      // multiply by A'[r][0] held in SGPRs (no zeroing move per accumulator)
 #pragma unroll
       for (int c = 0; c < CPL; ++c)
 #pragma unroll
-        for (int r = 0; r < S; ++r) Z[c][r] = 0.0;
+        for (int r = 0; r < S; ++r) Z[c][r] = a0[r] * G[c][0];
       static_for<0, S * S>([&](auto ec) {
         constexpr int e = decltype(ec)::value, r = e / S, k = e % S;
+        if constexpr (k > 0) {
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) dpp_fmac_bcast<e / NA>(Z[c][r], aq[e % NA], G[c][k]);
+          for (int c = 0; c < CPL; ++c) dpp_fmac_bcast<e / NA>(Z[c][r], aq[e % NA], G[c][k]);
+        }
       });
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
