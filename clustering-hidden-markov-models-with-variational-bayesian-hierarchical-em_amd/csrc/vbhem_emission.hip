@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 #include "vbhem_internal.h"
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(kUThreads) void u_prep_kernel(UPrepArgs p) {
   }
 }
 
-template <int KQB, int RC, int NTW, bool EXACT>
+template <int KQB, int RC, int NTW, bool EXACT, bool PF = false>
 __global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -561,6 +562,57 @@ __global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
     __syncthreads();
   };
   if (nchunk == 1) stage(0);
+  if constexpr (PF) {  // NTW == 1, W' in one chunk (the launcher checks)
+    {
+      // W' resident for the whole kernel: the next round's tile of U is loaded while
+      // this round's MFMAs run (one tile per wave, double-buffered in registers)
+      auto load_u = [&](long long r, double (&u)[KQB]) {
+        const long long tile = t_first + r * per_round + (long long)blockIdx.x * NW + wave;
+        const double *Ut = p.U + kUHead + (size_t)(tile < t_last ? tile : t_first) * kq * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < KQB; ++t) u[t] = t < kq ? Ut[(size_t)t * 64] : 0.0;
+      };
+      double u[KQB], un[KQB];
+      if (rounds > 0) load_u(0, u);
+#pragma unroll 1
+      for (long long r = 0; r < rounds; ++r) {
+        const long long tile = t_first + r * per_round + (long long)blockIdx.x * NW + wave;
+        const long long col = p.u_col0 + tile * 16 + cl;
+        const bool cv = tile < t_last && col >= c_begin && col < c_end;
+        double *Ec = p.E + (cv ? col - (long long)p.i_buf0 * SB : 0);
+        if (r + 1 < rounds) load_u(r + 1, un);
+        // W' is loop-invariant: an opaque offset keeps its LDS reads in the loop
+        // (hoisted, 88 values would take 176 VGPRs)
+        int woff = lane, boff = kl;
+        asm volatile("" : "+v"(woff), "+v"(boff));
+        double4_t acc[RC];
+#pragma unroll
+        for (int q = 0; q < RC; ++q)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[q][v] = bl[q * 16 + boff + 4 * v];
+#pragma unroll
+        for (int t = 0; t < KQB; ++t) {
+          if (t < kq) {
+#pragma unroll
+            for (int q = 0; q < RC; ++q)
+              acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(Wl[(t * RC + q) * 64 + woff], u[t], acc[q],
+                                                            0, 0, 0);
+          }
+        }
+        if (cv) {
+#pragma unroll
+          for (int q = 0; q < RC; ++q)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int row = q * 16 + kl + 4 * v;
+              if (row < KS) Ec[(size_t)row * ldE] = sm != 1.0 ? acc[q][v] / sm : acc[q][v];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < KQB; ++t) u[t] = un[t];
+      }
+    }
+  } else {
   for (long long r = 0; r < rounds; ++r) {
     // NTW column tiles per wave: each staged W' chunk feeds NTW * RC MFMAs per k-step
     double u[NTW][KQB];
@@ -616,6 +668,7 @@ __global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
       }
     }
   }
+  }
 }
 
 hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st) {
@@ -657,10 +710,11 @@ bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   return true;
 }
 
-template <int KQB, int RC, int NTW, bool EXACT = false>
+template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false>
 static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st) {
   if (EXACT && a.kdp / 4 != KQB) return hipErrorInvalidValue;
-  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT>;
+  if (PF && (NTW != 1 || a.ksp / 16 != RC)) return hipErrorInvalidValue;
+  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
@@ -734,8 +788,10 @@ hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   if (ncols <= 0) return hipSuccess;
   if (a.U && a.urc) {
-    if (a.ukqb == 4) return launch_u_fn<4, 8, 1>(a, lds, st);
-    if (a.ukqb == 12) return launch_u_fn<12, 8, 1>(a, lds, st);
+    // W' in one chunk (K S <= 128): the double-buffered variant
+    const bool one = a.ksp / 16 == a.urc && !std::getenv("VBHEM_NO_UPF");
+    if (a.ukqb == 4) return one ? launch_u_fn<4, 8, 1, false, true>(a, lds, st) : launch_u_fn<4, 8, 1>(a, lds, st);
+    if (a.ukqb == 12) return one ? launch_u_fn<12, 8, 1, false, true>(a, lds, st) : launch_u_fn<12, 8, 1>(a, lds, st);
     // W' restaged per chunk: two column tiles per wave halve the staging per column
     if (a.kdp / 4 == 38) return launch_u_fn<38, 4, UNTW, true>(a, lds, st);  // d = 16 full (C5)
     return launch_u_fn<kUMaxKq, 4, UNTW>(a, lds, st);
