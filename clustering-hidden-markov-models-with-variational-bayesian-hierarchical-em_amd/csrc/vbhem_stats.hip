@@ -64,7 +64,10 @@ constexpr double kGateZ = 1e-8;  // vbhem_compute_Statistics.m:35  (Z_Ni(i) > 1e
 // ---------------------------------------------------------------------------
 // resp_kernel: one wavefront per base (lanes over clusters j).
 // ---------------------------------------------------------------------------
-constexpr int kRespThreads = 256;
+#ifndef VBHEM_RESP_THREADS
+#define VBHEM_RESP_THREADS 512  // 8 waves per chunk block: 2x the bases in flight (C4 -10 us)
+#endif
+constexpr int kRespThreads = VBHEM_RESP_THREADS;
 
 __device__ __forceinline__ double group_max(double v, int G) {
   for (int off = G >> 1; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
