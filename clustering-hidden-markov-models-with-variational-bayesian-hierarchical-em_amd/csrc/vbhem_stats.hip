@@ -690,18 +690,30 @@ __global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
   }
 }
 
-// 256 threads = 32 columns x 8 slab partitions: partition p sums slabs
-// p, p+8, p+16, ... (coalesced 256-B rows), then the 8 partials are added in
-// fixed order -- deterministic, and ~slab_len/32 blocks fill the chip.
-constexpr int kFinalCols = 32, kFinalParts = 8;
+// 256 threads = 16 columns x 16 slab partitions: partition p sums slabs
+// p, p+16, p+32, ... (128-B rows, four loads in flight per thread), then the 16
+// partials are added in fixed order -- deterministic; ~slab_len/16 blocks (C4:
+// 506) keep every CU's loads in flight (32-column blocks left it latency-bound).
+constexpr int kFinalCols = 16, kFinalParts = 16;
 __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab,
                                                           int slab_len, double *out) {
   __shared__ double part[kFinalParts][kFinalCols];
   const int c = threadIdx.x % kFinalCols, pp = threadIdx.x / kFinalCols;
   const int x = blockIdx.x * kFinalCols + c;
   double acc = 0.0;
-  if (x < slab_len)
-    for (int k = pp; k < nslab; k += kFinalParts) acc += slabs[(size_t)k * slab_len + x];
+  if (x < slab_len) {
+    int k = pp;
+    for (; k + 3 * kFinalParts < nslab; k += 4 * kFinalParts) {
+      const double *q = slabs + (size_t)k * slab_len + x;
+      const double v0 = q[0], v1 = q[(size_t)kFinalParts * slab_len],
+                   v2 = q[(size_t)2 * kFinalParts * slab_len], v3 = q[(size_t)3 * kFinalParts * slab_len];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; k < nslab; k += kFinalParts) acc += slabs[(size_t)k * slab_len + x];
+  }
   part[pp][c] = acc;
   __syncthreads();
   if (pp == 0 && x < slab_len) {
