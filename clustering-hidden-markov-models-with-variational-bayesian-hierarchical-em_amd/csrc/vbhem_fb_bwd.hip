@@ -240,8 +240,11 @@ void fb_bwd2_kernel(const SplitArgs p) {
       for (int c = 0; c < CPL; ++c)
 #pragma unroll
         for (int r = 0; r < S; ++r) Z[c][r] = a0[r] * G[c][0];
+      // k outer, r inner: consecutive DPP fmacs write different accumulators (a DPP
+      // instruction reading a VGPR the previous VALU instruction wrote needs two wait
+      // states: r-inner chains cost an s_nop per fmac at S = 12); per-r order unchanged
       static_for<0, S * S>([&](auto ec) {
-        constexpr int e = decltype(ec)::value, r = e / S, k = e % S;
+        constexpr int f = decltype(ec)::value, k = f / S, r = f % S, e = r * S + k;
         if constexpr (k > 0) {
 #pragma unroll
           for (int c = 0; c < CPL; ++c) dpp_fmac_bcast<e / NA>(Z[c][r], aq[e % NA], G[c][k]);
