@@ -917,7 +917,7 @@ __global__ __launch_bounds__(64 * kSuWaves) void stats_list_u_kernel(const Stats
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
+#pragma unroll 1
       for (int b = 0; b < SM; ++b) {
         if (b < SB) {
           double uv[FPL];
