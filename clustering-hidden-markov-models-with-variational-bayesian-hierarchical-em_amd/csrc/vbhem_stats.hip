@@ -1055,7 +1055,10 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   const int NO = a.S + a.S * a.S + a.S * a.NU;
   const dim3 grid(nchunk, a.K);
   // on the prepared operand when the call has one (S <= 16: the split kernel's range)
-  if (a.U && a.S <= 16 && a.SB <= a.S && a.NU <= 3 * 64 && !std::getenv("VBHEM_NO_STATS_U")) {
+  // (NU > 64, e.g. d = 16 full at C5: the covariance gather of stats_list_kernel
+  // measured 2 % faster, 1.74 vs 1.78 ms per 100 k-base step; VBHEM_STATS_U=1 forces it)
+  const bool su = a.NU <= 64 || std::getenv("VBHEM_STATS_U");
+  if (a.U && su && a.S <= 16 && a.SB <= a.S && a.NU <= 3 * 64 && !std::getenv("VBHEM_NO_STATS_U")) {
     StatsArgs b = a;
     b.nzero = nchunk;
     // the per-block cost (wave reduction, slab writes) grows with the output count NO:

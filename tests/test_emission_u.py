@@ -125,8 +125,11 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     cs = make_case(N, K, S, Sb, d, cov, seed=11 + len(name), **extra)
     monkeypatch.setenv("VBHEM_GROUP_BASES", str(N // 2 + 1))
     outs = []
-    for env in ({"VBHEM_NO_STATS_U": "1"}, {}, {"VBHEM_SU_BLOCKS": str(K)}):
-        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS"):
+    # VBHEM_STATS_U=1: the prepared-operand kernel also where the default picks the
+    # covariance path (NU > 64)
+    for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1"},
+                {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K)}):
+        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
