@@ -1,4 +1,4 @@
-// vbhem_fb_bwd.hip -- the gated schedule's backward-only pass for S <= 8: K2 (the
+// vbhem_fb_bwd.hip -- the gated schedule's backward-only pass for S <= 16: K2 (the
 // backward recursion, mex.c:915-1015) and K3 (termination, mex.c:1020-1080) for
 // EVERY pair, writing L_elbo; the forward quantities of the gated pairs come from
 // fb_split_kernel's list mode afterwards (vbhem_fb_split.hip).
@@ -8,15 +8,16 @@
 // VALU do not run concurrently: scripts/ubench_valu.hip), and in fb_split_kernel's
 // one-column-per-lane layout a third of the kernel time went to waiting on the
 // scalar loads of the cluster matrix A' (64 doubles do not fit the 102 SGPRs, so
-// every step reloads them; removing those loads alone cut the kernel 2.10 -> 1.44
-// ms).  Here every lane owns TWO base-state columns of its pair, so each scalar
-// A' value feeds two FMAs, each slab read feeds two FMAs, and the lane has twice
-// the independent exp/log chains.
+// every step reloaded them).  Here A' is spread over the 16 lanes of each DPP row
+// and applied by v_fmac_f64 with a row_newbcast operand, and for S <= 8 every lane
+// owns TWO base-state columns of its pair, so each broadcast and each slab read
+// feeds two FMAs and the lane has twice the independent exp/log chains.
 //
-// Layout.  LPP = ceil(S/2) lanes per pair, PPW = floor(64/LPP) pairs per
-// wavefront (pairs never straddle a wavefront: every exchange is wave-local), one
-// cluster j per block, consecutive bases.  Lane w of a pair owns columns b = w and
-// b = w + LPP (padded columns past SB duplicate column SB-1 with zero base
+// Layout.  CPL = 2 (S <= 8) or 1 columns per lane, LPP = ceil(S/CPL) lanes per
+// pair, PPW = floor(64/LPP) pairs per wavefront (pairs never straddle a wavefront:
+// every exchange is wave-local), one cluster j per block, tiles of one wavefront's
+// PPW consecutive bases dealt wave-major.  Lane w of a pair owns columns b = w (and
+// b = w + LPP) (padded columns past SB duplicate column SB-1 with zero base
 // transitions and prior: exact no-ops, as in fb_split_kernel).  In registers per
 // column: Ef[S], V[S] = Ef + Lf, arow[S] (Ab row b).  Per step:
 //   M = max_s V, G = exp(V - M)                       (table exp, LDS table)
