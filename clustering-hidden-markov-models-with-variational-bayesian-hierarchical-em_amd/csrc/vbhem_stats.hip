@@ -15,6 +15,10 @@
 //                      moments of mex.c:1348-1469 contracted over the base states
 //                      and the bases at once: a (K*S) x (N*Sb) x NU GEMM on
 //                      v_mfma_f64_16x16x4f64, K-dim streamed in batches of NBB bases.
+//   gate_list_kernel / stats_list_kernel / stats_list_u_kernel  the gated schedule's
+//                      per-cluster lists of pairs with Z > 1e-8 and the sums over
+//                      them only (the base moments gathered from the covariances,
+//                      or read from the emission GEMM's prepared operand U).
 //   stats_final_kernel fixed-order sum of the per-chunk slabs.
 //
 // Grid: x = chunk of consecutive bases, y = group of JG clusters (rows j*S+s),
