@@ -831,6 +831,52 @@ hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds,
 // ---------------------------------------------------------------------------
 constexpr int kSuWaves = 4;
 
+// the prepared-operand statistics' output phase: the block's reduced sums in red
+// ([S][NU] | [S] | [S][S]) shifted back by z and written (or added) to slab c
+__device__ __forceinline__ void su_output(const StatsArgs &p, const double *red, const double *zs,
+                                          int c, int nch, int j, int tid) {
+  const int S = p.S, NU = p.NU, d = p.d;
+  const bool full = p.covmode == kCovFull;
+  const int KT = p.KT, tr = j / KT, jt = j - tr * KT;
+  double *tsl = p.slabs + (size_t)c * p.slab_len + (size_t)tr * p.SL;
+  const int NO = S * NU + S + S * S;
+  for (int o = tid; o < NO; o += 64 * kSuWaves) {
+    double v;
+    double *dst;
+    if (o < S * NU) {
+      const int s2 = o / NU, f = o - s2 * NU;
+      const double *rs = red + (size_t)s2 * NU;
+      const double N = rs[0];
+      if (f == 0) {
+        v = N;
+      } else if (f <= d) {
+        v = fma(zs[f - 1], N, rs[f]);
+      } else {
+        int a = f - 1 - d, b = a;
+        if (full) {
+          int k = a;
+          a = 0;
+          while (k >= d - a) { k -= d - a; ++a; }
+          b = a + k;
+        }
+        const double q2 = (full && a != b) ? 0.5 * rs[f] : rs[f];
+        v = q2 + (zs[a] * rs[1 + b] + zs[b] * rs[1 + a]) + zs[a] * zs[b] * N;
+      }
+      dst = tsl + KT + (size_t)KT * S + (size_t)KT * S * S + 2 + (size_t)jt * S * NU + o;
+    } else if (o < S * NU + S) {
+      v = red[o];
+      dst = tsl + KT + (size_t)jt * S + (o - S * NU);
+    } else {
+      v = red[o];
+      dst = tsl + KT + (size_t)KT * S + (size_t)jt * S * S + (o - S * NU - S);
+    }
+    *dst = p.assign ? v : *dst + v;
+    if (p.assign)  // the slabs past this grid's chunks hold nothing of cluster j
+      for (int cz = c + nch; cz < p.nzero; cz += nch) dst[(size_t)(cz - c) * p.slab_len] = 0.0;
+  }
+}
+
+
 template <int FPL, int SM>
 __global__ __launch_bounds__(64 * kSuWaves) void stats_list_u_kernel(const StatsArgs p) {
   extern __shared__ double lds[];
@@ -971,43 +1017,133 @@ __global__ __launch_bounds__(64 * kSuWaves) void stats_list_u_kernel(const Stats
     }
     __syncthreads();
   }
-  const int KT = p.KT, tr = j / KT, jt = j - tr * KT;
-  double *tsl = p.slabs + (size_t)c * p.slab_len + (size_t)tr * p.SL;
-  const int NO = S * NU + S + S * S;
-  for (int o = tid; o < NO; o += 64 * kSuWaves) {
-    double v;
-    double *dst;
-    if (o < S * NU) {
-      const int s2 = o / NU, f = o - s2 * NU;
-      const double *rs = red + (size_t)s2 * NU;
-      const double N = rs[0];
-      if (f == 0) {
-        v = N;
-      } else if (f <= d) {
-        v = fma(zs[f - 1], N, rs[f]);
-      } else {
-        int a = f - 1 - d, b = a;
-        if (full) {
-          int k = a;
-          a = 0;
-          while (k >= d - a) { k -= d - a; ++a; }
-          b = a + k;
-        }
-        const double q2 = (full && a != b) ? 0.5 * rs[f] : rs[f];
-        v = q2 + (zs[a] * rs[1 + b] + zs[b] * rs[1 + a]) + zs[a] * zs[b] * N;
-      }
-      dst = tsl + KT + (size_t)KT * S + (size_t)KT * S * S + 2 + (size_t)jt * S * NU + o;
-    } else if (o < S * NU + S) {
-      v = red[o];
-      dst = tsl + KT + (size_t)jt * S + (o - S * NU);
-    } else {
-      v = red[o];
-      dst = tsl + KT + (size_t)KT * S + (size_t)jt * S * S + (o - S * NU - S);
+  su_output(p, red, zs, c, nch, j, tid);
+}
+
+// stats_list_g_kernel<LG, SM>: stats_list_u_kernel for small moment vectors
+// (NU <= LG <= 32, e.g. d = 2 diag: NU = 5): a wavefront is 64 / LG lane groups, each
+// taking its own pair (group g of wave w: pairs w G + g, + 4 G, ...), so a pair
+// no longer leaves 59 of 64 lanes idle.  Per group a private LDS slab; the groups
+// and waves reduce in fixed order (bit-reproducible), output as stats_list_u_kernel.
+template <int LG, int SM>
+__global__ __launch_bounds__(64 * kSuWaves) void stats_list_g_kernel(const StatsArgs p) {
+  extern __shared__ double lds[];
+  constexpr int NG = 64 / LG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane / LG, gl = lane - grp * LG;
+  const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU, kq = p.ukdp / 4;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d;
+  const int j = blockIdx.y, c = blockIdx.x, nch = gridDim.x;
+  const int OT = S * SB, TS = (OT + 1) / 2 * 2, KP = p.ukdp + 1;
+  const int WS = TS + (SB * KP + 1) / 2 * 2;
+  double *tw = lds + (size_t)(wave * NG + grp) * WS;   // [SB][S] Z tnu of the group's pair
+  double *uw = tw + TS;                                 // [SB][KP] its U columns
+  double *red = lds + (size_t)kSuWaves * NG * WS;      // [S][NU] | [S] | [S][S]
+  double *zs = red + (size_t)S * NU + S + S * S;       // [d]
+  for (int a = tid; a < d; a += 64 * kSuWaves) zs[a] = p.uz[a];
+  const bool fv = gl < NU;
+  const int ue = gl == 0 ? -1 : gl <= d ? NPF + gl - 1 : gl - 1 - d;
+  double acc[SM], accx[4], accn = 0.0;
+#pragma unroll
+  for (int s2 = 0; s2 < SM; ++s2) acc[s2] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) accx[e] = 0.0;
+  const int tot = p.list_tot[j];
+  const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
+  const int *lst = p.list + (size_t)j * p.list_cap;
+  const double *Ub0 = p.U + kUHead;
+  const int nu4 = 4 * kq * SB;
+  // wave-uniform trip count; a group past the part's end stages a zero-weight copy
+  for (int nb = n0 + wave * NG; nb < n1; nb += kSuWaves * NG) {
+    const int n = nb + grp;
+    const bool pv = n < n1;
+    const int i = lst[pv ? n : n0];
+    const size_t lp = (size_t)(i - p.i_buf0) * K + j;
+    const double z = pv ? p.Z[lp] : 0.0;
+    double tv[4], xv[4], uv[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = gl + LG * e;
+      tv[e] = x < OT ? p.tnu[lp * OT + x] : 0.0;
+      xv[e] = x < S * S ? p.xi[lp * S * S + x] : 0.0;
     }
-    *dst = p.assign ? v : *dst + v;
-    if (p.assign)  // the slabs past this grid's chunks hold nothing of cluster j
-      for (int cz = c + nch; cz < p.nzero; cz += nch) dst[(size_t)(cz - c) * p.slab_len] = 0.0;
+    const double nv = gl < S ? p.nu1[lp * S + gl] : 0.0;
+    const long long c0 = (long long)i * SB - p.u_col0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int x = gl + LG * e;
+      const int t4 = x / SB, b = x - t4 * SB;
+      const long long col = c0 + b;
+      uv[e] = x < nu4 ? Ub0[(size_t)(col >> 4) * kq * 64 + (t4 >> 2) * 64 + (t4 & 3) * 16 + (col & 15)]
+                      : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = gl + LG * e;
+      if (x < OT) {
+        const int s2 = x / SB, b = x - s2 * SB;
+        tw[b * S + s2] = z * tv[e];
+      }
+      accx[e] = fma(z, xv[e], accx[e]);
+    }
+    accn = fma(z, nv, accn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int x = gl + LG * e;
+      const int t4 = x / SB, b = x - t4 * SB;
+      if (x < nu4) uw[b * KP + t4] = uv[e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (fv) {
+#pragma unroll 1
+      for (int b = 0; b < SB; ++b) {
+        const double u = ue < 0 ? 1.0 : uw[b * KP + ue];
+#pragma unroll
+        for (int s2 = 0; s2 < SM; ++s2)
+          if (s2 < S) acc[s2] = fma(tw[b * S + s2], u, acc[s2]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  // fixed-order reduction: waves in order, and within a wave its groups in order
+  // (exec-masked stores of one wavefront retire in program order)
+  for (int w = 0; w < kSuWaves; ++w) {
+    if (wave == w) {
+      for (int g = 0; g < NG; ++g) {
+        if (grp == g) {
+          const bool first = w == 0 && g == 0;
+#pragma unroll
+          for (int s2 = 0; s2 < SM; ++s2)
+            if (fv && s2 < S) {
+              double *r = red + (size_t)s2 * NU + gl;
+              *r = first ? acc[s2] : *r + acc[s2];
+            }
+          if (gl < S) {
+            double *r = red + (size_t)S * NU + gl;
+            *r = first ? accn : *r + accn;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int x = gl + LG * e;
+            if (x < S * S) {
+              double *r = red + (size_t)S * NU + S + x;
+              *r = first ? accx[e] : *r + accx[e];
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+    __syncthreads();
+  }
+  su_output(p, red, zs, c, nch, j, tid);
 }
 
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st) {
@@ -1047,6 +1183,36 @@ static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st
   return hipGetLastError();
 }
 
+template <int LG, int SM>
+static hipError_t launch_sg(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  const int OT = a.S * a.SB, KP = a.ukdp + 1;
+  const size_t ws = (size_t)(OT + 1) / 2 * 2 + ((size_t)a.SB * KP + 1) / 2 * 2;
+  const size_t lds = ((size_t)kSuWaves * (64 / LG) * ws + (size_t)a.S * a.NU + a.S +
+                      (size_t)a.S * a.S + a.d) * sizeof(double);
+  auto *fn = &stats_list_g_kernel<LG, SM>;
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fn, grid, dim3(64 * kSuWaves), lds, st, a);
+  return hipGetLastError();
+}
+
+// lanes per pair group for the grouped kernel (0: shape too large for it)
+static int sg_lanes(const StatsArgs &a) {
+  if (std::getenv("VBHEM_NO_STATS_G")) return 0;
+  const int OT = a.S * a.SB, nu4 = a.ukdp * a.SB;
+  for (int LG : {8, 16, 32})
+    if (a.NU <= LG && OT <= 4 * LG && a.S * a.S <= 4 * LG && nu4 <= 8 * LG) return LG;
+  return 0;
+}
+
+template <int LG>
+static hipError_t launch_sg_s(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  if (a.S <= 4) return launch_sg<LG, 4>(a, grid, st);
+  if (a.S <= 8) return launch_sg<LG, 8>(a, grid, st);
+  if (a.S <= 12) return launch_sg<LG, 12>(a, grid, st);
+  return launch_sg<LG, 16>(a, grid, st);
+}
+
 template <int FPL>
 static hipError_t launch_su_s(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
   if (a.S <= 4) return launch_su<FPL, 4>(a, grid, st);
@@ -1074,6 +1240,16 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
       cap = std::atoi(ev) / std::max(1, a.K);
     const int nb = (int)std::max(1ll, std::min((long long)nchunk, cap));
     const dim3 g2(nb, a.K);
+    // the grouped kernel runs 64 / LG pairs per wave at once: half the blocks (C3,
+    // 80 per cluster: statistics 0.047 -> 0.043 ms; with 156 it was 0.057)
+    const int lg = sg_lanes(a);
+    const dim3 gg(std::getenv("VBHEM_SU_BLOCKS") ? nb : std::max(1, nb / 2), a.K);
+    switch (lg) {
+      case 8: return launch_sg_s<8>(b, gg, st);
+      case 16: return launch_sg_s<16>(b, gg, st);
+      case 32: return launch_sg_s<32>(b, gg, st);
+      default: break;
+    }
     if (a.NU <= 64) return launch_su_s<1>(b, g2, st);
     if (a.NU <= 128) return launch_su_s<2>(b, g2, st);
     return launch_su_s<3>(b, g2, st);

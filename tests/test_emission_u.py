@@ -114,8 +114,9 @@ def test_prepared_operand_layout(vb):
 @pytest.mark.parametrize("name", ["full_d8", "full_d16", "diag_d12", "full_d2_face"])
 @pytest.mark.parametrize("prepare", [True, False])
 def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
-    """Gated statistics from the prepared operand (stats_list_u_kernel: moments read from
-    U and shifted back by z) vs the covariance gather (stats_list_kernel), with several
+    """Gated statistics from the prepared operand (stats_list_u_kernel, and
+    stats_list_g_kernel for small NU: moments read from U and shifted back by z) vs the
+    covariance gather (stats_list_kernel), with several
     base groups (the second group adds into the slabs) and fewer blocks than chunks (the
     first group zero-fills the slabs past its grid)."""
     from vbhem_amd import host
@@ -127,9 +128,12 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     outs = []
     # VBHEM_STATS_U=1: the prepared-operand kernel also where the default picks the
     # covariance path (NU > 64)
+    # VBHEM_NO_STATS_G=1: the one-pair-per-wave kernel where the grouped one (small NU)
+    # is the default
     for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1"},
-                {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K)}):
-        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U"):
+                {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K)},
+                {"VBHEM_STATS_U": "1", "VBHEM_NO_STATS_G": "1"}):
+        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U", "VBHEM_NO_STATS_G"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
