@@ -214,13 +214,18 @@ def main():
     eng.set_log_omega(logOm)
     tN = (float(opt["Nv"]) * N) * eng.base.omega
     allreduce = make_allreduce()
-    # the statistics land in pinned host memory (what the host M-step reads)
-    host_stats = torch.empty((eng.stats_len,), dtype=torch.float64, pin_memory=True)
+    # the statistics land in pinned host memory (what the host M-step reads): one
+    # rank writes them there straight from the statistics kernel; several ranks
+    # all-reduce the device vector, then copy it
+    host_stats = eng.host_stats_buffer()
 
     def step():
-        st = eng.fused(tN)
-        allreduce(st)
-        host_stats.copy_(st, non_blocking=True)
+        if world == 1 and not os.environ.get("VBHEM_BENCH_COPY"):
+            eng.fused(tN, out=host_stats)
+        else:
+            st = eng.fused(tN)
+            allreduce(st)
+            host_stats.copy_(st, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
         return host_stats
 

@@ -81,6 +81,7 @@ EXPORTS = {
     "vbhem_estep_fused_trials": (_c_int, [ctypes.POINTER(BaseT), ctypes.POINTER(ClusterT), _c_int,
                                           _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "vbhem_last_fallback_count": (_c_int, [_vp, _vp]),
+    "vbhem_host_device_pointer": (_c_int, [_vp, ctypes.POINTER(_vp)]),
     "vbhem_ctx_create": (_c_int, [_c_int, ctypes.POINTER(BaseT), _c_int, _c_int, _c_int, _c_int,
                                   ctypes.POINTER(_vp)]),
     "vbhem_ctx_fused": (_c_int, [_vp, ctypes.POINTER(ClusterT), _vp, _vp, _vp, _vp, _vp]),

@@ -44,6 +44,25 @@ def tilde_n(engine: EStepEngine, Nv: float, total_N: int) -> torch.Tensor:
     return (float(Nv) * float(total_N)) * engine.base.omega.to(torch.float64)
 
 
+def fused_stats_host(engine: EStepEngine, tN: torch.Tensor,
+                     allreduce: Optional[Callable[[torch.Tensor], None]]) -> np.ndarray:
+    """One fused E-step; its packed statistics on the host for the M-step.
+    Single process: the statistics kernel writes them straight into a pinned
+    host buffer (no copy after the E-step).  Sharded: device vector, all-reduce,
+    then a copy."""
+    if allreduce is None and isinstance(engine, EStepEngine):
+        buf = getattr(engine, "_em_host_stats", None)
+        if buf is None:
+            buf = engine._em_host_stats = engine.host_stats_buffer()
+        engine.fused(tN, out=buf)
+        torch.cuda.current_stream(engine.device).synchronize()
+        return buf.numpy().copy()
+    stats = engine.fused(tN)
+    if allreduce is not None:
+        allreduce(stats)
+    return stats.cpu().numpy()
+
+
 def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
                         total_N: Optional[int] = None,
                         allreduce: Optional[Callable[[torch.Tensor], None]] = None,
@@ -69,10 +88,7 @@ def vbhem_h3m_c_step_fc(post: Posterior, engine: EStepEngine, opt: dict, *,
         logOmega = host.log_omega_tilde(post.alpha)
         engine.set_clusters(consts)
         engine.set_log_omega(logOmega)
-        stats = engine.fused(tN)
-        if allreduce is not None:
-            allreduce(stats)
-        st = host.unpack_stats(stats.cpu().numpy(), K, S, d, covmode)
+        st = host.unpack_stats(fused_stats_host(engine, tN, allreduce), K, S, d, covmode)
         Nj = st["Nj"] + 1e-50
         L = host.lower_bound(st["Lt1"], st["Lt7"], Nj, logOmega, post, consts, opt, covmode)
         do_break = False
@@ -158,10 +174,7 @@ def vbhem_h3m_c_trials(posts: List[Posterior], engine: EStepEngine, opt: dict, *
     while not all(done):
         engine.set_clusters(_stack_constants(consts))
         engine.set_log_omega(np.concatenate(logOm))
-        stats = engine.fused(tN)
-        if allreduce is not None:
-            allreduce(stats)
-        vec = stats.cpu().numpy()
+        vec = fused_stats_host(engine, tN, allreduce)
         for r in range(R):
             if done[r]:
                 continue

@@ -70,6 +70,7 @@ class EStepEngine:
         self.LL = torch.zeros((N, K), dtype=F64, device=dv)
         self._ws_fused = None
         self._ws_pairs = None
+        self._mapped = None  # (host_stats_buffer tensor, its device address)
 
     # -- inputs -------------------------------------------------------------
     @property
@@ -130,31 +131,61 @@ class EStepEngine:
         return out
 
     # -- fused E-step --------------------------------------------------------
-    def fused(self, tildeN: torch.Tensor) -> torch.Tensor:
+    def host_stats_buffer(self) -> torch.Tensor:
+        """A pinned host vector of stats_len doubles for ``fused(out=...)`` (its
+        device address is resolved once, here)."""
+        buf = torch.zeros((self.stats_len,), dtype=F64, pin_memory=True)
+        self._mapped = (buf, self._device_address(buf))
+        return buf
+
+    def _device_address(self, host: torch.Tensor) -> int:
+        p = ctypes.c_void_p()
+        _capi.check(self.lib.vbhem_host_device_pointer(ctypes.c_void_p(host.data_ptr()),
+                                                       ctypes.byref(p)), "vbhem_host_device_pointer")
+        return int(p.value)
+
+    def _out_ptr(self, out: torch.Tensor) -> int:
+        if out.dtype != F64 or not out.is_contiguous() or out.numel() != self.stats_len:
+            raise ValueError(f"out must be a contiguous fp64 vector of {self.stats_len} entries")
+        if out.is_cuda:
+            if out.device != self.device:
+                raise ValueError("out is on another device")
+            return _capi.ptr(out)
+        if self._mapped is not None and self._mapped[0] is out:
+            return self._mapped[1]
+        # pinned host memory: the kernel writes it through its device address
+        return self._device_address(out)
+
+    def fused(self, tildeN: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         """Pairs + responsibilities + gated Z-weighted sums + ELBO partials.
 
         tildeN: [N] (device, fp64) virtual-sample counts of this shard.
-        Returns the packed statistics vector (device, [stats_len]); hat_Z and
+        Returns the packed statistics vector ([stats_len]): ``self.stats`` on the
+        device, or ``out`` when given -- a device vector, or a pinned host vector
+        (``host_stats_buffer``) that the statistics kernel writes directly (no
+        copy after the E-step; read it after synchronising the stream).  hat_Z and
         L_elbo are left in ``self.hatZ`` / ``self.LL``."""
         if self._ws_fused is None:
             nb = int(self.lib.vbhem_fused_trials_workspace_bytes(
                 ctypes.byref(self._bt), ctypes.byref(self._ct), self.trials, self.T))
             self._ws_fused = torch.empty((max(nb, 1),), dtype=torch.uint8, device=self.device)
+        res = self.stats if out is None else out
+        sp = _capi.ptr(self.stats) if out is None else self._out_ptr(out)
         if self.trials == 1:
             rc = self.lib.vbhem_estep_fused(
                 ctypes.byref(self._bt), ctypes.byref(self._ct), self.T, _capi.ptr(tildeN),
-                _capi.ptr(self.logOmega), _capi.ptr(self.stats), _capi.ptr(self.hatZ),
+                _capi.ptr(self.logOmega), sp, _capi.ptr(self.hatZ),
                 _capi.ptr(self.LL), _capi.ptr(self._ws_fused), self._ws_fused.numel(),
                 self._stream())
             _capi.check(rc, "vbhem_estep_fused")
         else:
             rc = self.lib.vbhem_estep_fused_trials(
                 ctypes.byref(self._bt), ctypes.byref(self._ct), self.trials, self.T,
-                _capi.ptr(tildeN), _capi.ptr(self.logOmega), _capi.ptr(self.stats),
+                _capi.ptr(tildeN), _capi.ptr(self.logOmega), sp,
                 _capi.ptr(self.hatZ), _capi.ptr(self.LL), _capi.ptr(self._ws_fused),
                 self._ws_fused.numel(), self._stream())
             _capi.check(rc, "vbhem_estep_fused_trials")
-        return self.stats
+        return res
 
     def fallback_count(self) -> int:
         """Pairs of the last fused call that needed the exact fallback (syncs)."""

@@ -212,6 +212,13 @@ int vbhem_set_fused_mode(int mode);
  * log-sum-exp fell below its safe range.  Synchronises `stream`. */
 int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
 
+/* Device address of pinned (page-locked, mapped) host memory, for callers that
+ * let vbhem_estep_fused write its statistics straight into host memory (the
+ * host M-step's input: no device-to-host copy after the E-step; the kernel's
+ * stores cross the bus).  The host reads the vector after synchronising the
+ * stream.  VBHEM_ERR_ARG if host_ptr is not registered pinned memory. */
+int vbhem_host_device_pointer(void *host_ptr, void **dev_ptr);
+
 /* Kernel timing for benchmarking/profiling, per host thread: while enabled,
  * hipEvents are recorded on the launch stream around the kernel launches of this
  * thread (never into a stream that is capturing a graph: such launches are simply

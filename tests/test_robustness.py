@@ -150,3 +150,48 @@ def test_fused_mode_is_per_thread(capi_lib):
     assert seen == {"prev": _capi.FUSED_GATED, "now": _capi.FUSED_DENSE}
     # the main thread's schedule is untouched by the worker
     assert _capi.set_fused_mode(prev_main) == _capi.FUSED_GATED
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("trials", [1, 2])
+def test_fused_into_pinned_host_memory(vb, trials):
+    """fused(out=pinned host vector): the statistics kernel writes the host buffer
+    directly (no device-to-host copy); bit-identical to the device vector, also
+    with several base groups (the first group writes, later ones add) and on
+    repeat calls into the same buffer."""
+    import os
+    from vbhem_amd import host
+    cs = make_case(500, 4, 5, 5, 3, 1, seed=43, tau=8)
+    c0 = cs["consts"]
+    consts = c0 if trials == 1 else {k: np.concatenate([np.asarray(c0[k])] * trials) for k in c0}
+    logOm = host.log_omega_tilde(cs["P"].alpha)
+    tN = _tn(cs)
+    old = os.environ.get("VBHEM_GROUP_BASES")
+    for group in (None, "128"):
+        if group is None:
+            os.environ.pop("VBHEM_GROUP_BASES", None)
+        else:
+            os.environ["VBHEM_GROUP_BASES"] = group
+        try:
+            eng = _engine(vb, cs, trials=trials, consts=consts)
+            eng.set_log_omega(np.concatenate([logOm] * trials))
+            ref = eng.fused(tN).clone()
+            buf = eng.host_stats_buffer()
+            assert not buf.is_cuda and buf.is_pinned()
+            for _ in range(2):
+                buf.fill_(np.nan)
+                out = eng.fused(tN, out=buf)
+                assert out is buf
+                torch.cuda.current_stream().synchronize()
+                assert torch.equal(buf, ref.cpu())
+            other = torch.empty_like(buf).pin_memory()  # resolved per call
+            eng.fused(tN, out=other)
+            torch.cuda.synchronize()
+            assert torch.equal(other, ref.cpu())
+        finally:
+            if old is None:
+                os.environ.pop("VBHEM_GROUP_BASES", None)
+            else:
+                os.environ["VBHEM_GROUP_BASES"] = old
+    with pytest.raises(Exception):
+        eng.fused(tN, out=torch.zeros(eng.stats_len, dtype=torch.float64))  # pageable memory
