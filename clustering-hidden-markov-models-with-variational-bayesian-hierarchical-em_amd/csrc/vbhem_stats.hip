@@ -101,6 +101,41 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
   double l1 = 0.0, l7 = 0.0;
+  if (K <= G) {
+    // one cluster per lane: the next base's tilde_N and L_elbo are loaded while
+    // this base's ẑ is computed (a C4 wave walks 6 bases of its chunk in turn)
+    const int stride = NW * BPW;
+    const double lo = gl < K ? p.logOmega[gl] : 0.0;
+    int i = b0 + wave * BPW + sub;
+    int ii = i < b1 ? i : b0;
+    double tn = p.tildeN[ii];
+    double ll = gl < K ? p.LL[(size_t)ii * K + gl] : 0.0;
+    for (; i - sub < b1; i += stride) {
+#pragma clang fp contract(off)
+      const bool iv = i < b1;
+      const int in = i + stride < b1 ? i + stride : b0;
+      const double tn_n = p.tildeN[in];
+      const double ll_n = gl < K ? p.LL[(size_t)in * K + gl] : 0.0;
+      const double lz = tn * (lo + ll);  // rounded before the shift (see below)
+      double mx = gl < K ? lz : -INFINITY;
+      mx = group_max(mx, G);
+      double sm = gl < K ? exp(lz - mx) : 0.0;
+      sm = group_sum(sm, G);
+      const double lse = mx + log(sm);
+      if (iv && gl < K) {
+        const double hz = exp(lz - lse) + 1e-50;
+        const double Z = hz * tn;
+        p.hatZ[(size_t)i * K + gl] = hz;
+        p.Z[(size_t)(i - p.i_buf0) * K + gl] = Z;
+        accNj[(wave * BPW + sub) * K + gl] += Z;
+        if (Z > kGateZ) atomicAdd(&gcnt[gl], 1);
+        l1 += Z * ll;
+        l7 += hz * log(hz);
+      }
+      tn = tn_n;
+      ll = ll_n;
+    }
+  } else
   for (int i = b0 + wave * BPW + sub; i - sub < b1; i += NW * BPW) {
     // log_Z = tilde_N .* (logOmega + L_elbo) is rounded before the shift, as in
     // step_fc.m:275-276 (an fma-contracted shift would let the winning entry
@@ -292,6 +327,7 @@ __global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs
     const int r = tid / KC, j = j0 + (tid - r * KC);
     if (r < R) {
       int sb = 0, stt = 0;
+#pragma unroll 8
       for (int c = r; c < nchunk; c += R) {
         const int v = p.gate_cnt[(size_t)c * K + j];
         stt += v;
@@ -316,12 +352,22 @@ __global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs
     for (int j = tid; j < K; j += kListThreads) p.list_tot[j] = total[j];
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, me, nchunk, b0, b1);
+  constexpr int kJB = 16;  // clusters whose Z are loaded together (one round trip, not K)
   for (int i0 = b0; i0 < b1; i0 += kListThreads) {
     const int i = i0 + tid;
     const bool iv = i < b1;
     const double *Zi = p.Z + (size_t)((iv ? i : b0) - p.i_buf0) * K;
+    unsigned gbits = 0;
     for (int j = 0; j < K; ++j) {
-      const bool g = iv && Zi[j] > kGateZ;
+      if ((j & (kJB - 1)) == 0) {
+        double z[kJB];
+#pragma unroll
+        for (int q = 0; q < kJB; ++q) z[q] = j + q < K ? Zi[j + q] : 0.0;
+        gbits = 0;
+#pragma unroll
+        for (int q = 0; q < kJB; ++q) gbits |= (iv && z[q] > kGateZ) ? 1u << q : 0u;
+      }
+      const bool g = (gbits >> (j & (kJB - 1))) & 1u;
       const unsigned long long m = __ballot(g);
       if (lane == 0) wcnt[wave] = __popcll(m);
       __syncthreads();
