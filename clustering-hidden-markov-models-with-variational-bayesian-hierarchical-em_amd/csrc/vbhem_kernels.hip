@@ -377,6 +377,9 @@ __global__ __launch_bounds__(kExactBlock) void fb_exact_kernel(const FbArgs p, d
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int nt = gridDim.x * blockDim.x;
   const int cnt = __atomic_load_n(p.flag_count, __ATOMIC_RELAXED);
+  // nothing flagged (the usual case): every block reads 0 -- nobody writes the
+  // counter while it is 0 -- so all leave at once, with no reset to do
+  if (cnt == 0) return;
   const int S = p.S, SB = p.SB, d = p.d, T = p.T;
   double *w = scratch + (size_t)gt * scratch_stride;
   double *E = w, *L = E + S * SB, *Ln = L + S * SB, *lt = Ln + S * SB, *nu = lt + S * SB,

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kRespThreads) void resp_trials_kernel(const StatsAr
 // gate_list_kernel: the gated pairs as per-cluster lists of bases, ascending i
 // (list[j][n], n < list_tot[j]).  Block = the resp_kernel chunk: its offset in
 // cluster j's list is the gate count of the chunks before it; inside the chunk
-// the bases are ranked by a block-wide ballot scan, one cluster at a time.
+// the bases are ranked by wave ballots (masks in LDS, one barrier per slice).
 // Deterministic (no global atomics): the same list every call.
 // ---------------------------------------------------------------------------
 constexpr int kListThreads = 256;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs
   const int K = p.K, nchunk = gridDim.x, me = blockIdx.x;
   int *before = ish;          // [K] this chunk's offset in every cluster's list
   int *total = ish + K;       // [K]
-  int *wcnt = ish + 2 * K;    // [NW]
+  int *wcnt = ish + 2 * K;    // [NW] (unused slot)
   // this chunk's offset (gate counts of chunks c < me) and cluster totals: thread
   // (r, j) sums chunks c = r, r + R, ...; then the R partials of each j in order
   int *pb = wcnt + NW;        // [R][K]
@@ -352,35 +352,42 @@ __global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs
     for (int j = tid; j < K; j += kListThreads) p.list_tot[j] = total[j];
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, me, nchunk, b0, b1);
+  // per 256-base slice: every wave ballots all K clusters into LDS masks (no
+  // barrier per cluster), one barrier, then each thread places its base in the
+  // lists that gate it in, after the bases of the lower waves and chunks
+  unsigned long long *msk = reinterpret_cast<unsigned long long *>(
+      ish + ((2 * K + NW + 2 * kListThreads + 1) & ~1));  // [NW][K], 8-byte aligned
   constexpr int kJB = 16;  // clusters whose Z are loaded together (one round trip, not K)
   for (int i0 = b0; i0 < b1; i0 += kListThreads) {
     const int i = i0 + tid;
     const bool iv = i < b1;
     const double *Zi = p.Z + (size_t)((iv ? i : b0) - p.i_buf0) * K;
-    unsigned gbits = 0;
-    for (int j = 0; j < K; ++j) {
-      if ((j & (kJB - 1)) == 0) {
-        double z[kJB];
+    for (int j0 = 0; j0 < K; j0 += kJB) {
+      double z[kJB];
 #pragma unroll
-        for (int q = 0; q < kJB; ++q) z[q] = j + q < K ? Zi[j + q] : 0.0;
-        gbits = 0;
+      for (int q = 0; q < kJB; ++q) z[q] = j0 + q < K ? Zi[j0 + q] : 0.0;
 #pragma unroll
-        for (int q = 0; q < kJB; ++q) gbits |= (iv && z[q] > kGateZ) ? 1u << q : 0u;
-      }
-      const bool g = (gbits >> (j & (kJB - 1))) & 1u;
-      const unsigned long long m = __ballot(g);
-      if (lane == 0) wcnt[wave] = __popcll(m);
-      __syncthreads();
-      int off = before[j];
-      for (int w = 0; w < wave; ++w) off += wcnt[w];
-      if (g) p.list[(size_t)j * p.list_cap + off + __popcll(m & ((1ull << lane) - 1ull))] = i;
-      __syncthreads();
-      if (tid == 0) {
-        int t = 0;
-        for (int w = 0; w < NW; ++w) t += wcnt[w];
-        before[j] += t;
+      for (int q = 0; q < kJB; ++q) {
+        const unsigned long long m = __ballot(iv && z[q] > kGateZ);
+        if (lane == 0 && j0 + q < K) msk[wave * K + j0 + q] = m;
       }
     }
+    __syncthreads();
+    for (int j = 0; j < K; ++j) {
+      const unsigned long long m = msk[wave * K + j];
+      if ((m >> lane) & 1ull) {
+        int off = before[j];
+        for (int w = 0; w < wave; ++w) off += __popcll(msk[w * K + j]);
+        p.list[(size_t)j * p.list_cap + off + __popcll(m & ((1ull << lane) - 1ull))] = i;
+      }
+    }
+    __syncthreads();  // every thread has read before[] and the masks
+    for (int j = tid; j < K; j += kListThreads) {
+      int t = 0;
+      for (int w = 0; w < NW; ++w) t += __popcll(msk[w * K + j]);
+      before[j] += t;
+    }
+    __syncthreads();  // before[] updated before the next slice's masks overwrite these
   }
 }
 
@@ -1193,7 +1200,9 @@ __global__ __launch_bounds__(64 * kSuWaves) void stats_list_g_kernel(const Stats
 }
 
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st) {
-  const size_t lds = ((size_t)2 * a.K + kListThreads / 64 + 2 * kListThreads) * sizeof(int);
+  const size_t ints = (size_t)2 * a.K + kListThreads / 64 + 2 * kListThreads;
+  const size_t lds = (ints + 1) / 2 * 2 * sizeof(int) +
+                     (size_t)(kListThreads / 64) * a.K * sizeof(unsigned long long);
   hipLaunchKernelGGL(gate_list_kernel, dim3(nchunk), dim3(kListThreads), lds, st, a);
   return hipGetLastError();
 }
