@@ -71,6 +71,7 @@ class EStepEngine:
         self._ws_fused = None
         self._ws_pairs = None
         self._mapped = None  # (host_stats_buffer tensor, its device address)
+        self._fused_args = None  # (pointers + stream key, entry point, name, ctypes arguments)
 
     # -- inputs -------------------------------------------------------------
     @property
@@ -171,20 +172,21 @@ class EStepEngine:
             self._ws_fused = torch.empty((max(nb, 1),), dtype=torch.uint8, device=self.device)
         res = self.stats if out is None else out
         sp = _capi.ptr(self.stats) if out is None else self._out_ptr(out)
-        if self.trials == 1:
-            rc = self.lib.vbhem_estep_fused(
-                ctypes.byref(self._bt), ctypes.byref(self._ct), self.T, _capi.ptr(tildeN),
-                _capi.ptr(self.logOmega), sp, _capi.ptr(self.hatZ),
-                _capi.ptr(self.LL), _capi.ptr(self._ws_fused), self._ws_fused.numel(),
-                self._stream())
-            _capi.check(rc, "vbhem_estep_fused")
-        else:
-            rc = self.lib.vbhem_estep_fused_trials(
-                ctypes.byref(self._bt), ctypes.byref(self._ct), self.trials, self.T,
-                _capi.ptr(tildeN), _capi.ptr(self.logOmega), sp,
-                _capi.ptr(self.hatZ), _capi.ptr(self.LL), _capi.ptr(self._ws_fused),
-                self._ws_fused.numel(), self._stream())
-            _capi.check(rc, "vbhem_estep_fused_trials")
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        key = (tildeN.data_ptr(), sp, st)
+        if self._fused_args is None or self._fused_args[0] != key:
+            # the call's ctypes arguments, rebuilt only when a pointer or the stream changes
+            # (an EM loop repeats the same call: ~4 us of Python per E-step otherwise)
+            head = (ctypes.byref(self._bt), ctypes.byref(self._ct))
+            head += (self.T,) if self.trials == 1 else (self.trials, self.T)
+            args = head + (_capi.ptr(tildeN), _capi.ptr(self.logOmega), sp, _capi.ptr(self.hatZ),
+                           _capi.ptr(self.LL), _capi.ptr(self._ws_fused), self._ws_fused.numel(),
+                           ctypes.c_void_p(st))
+            fn, name = ((self.lib.vbhem_estep_fused, "vbhem_estep_fused") if self.trials == 1 else
+                        (self.lib.vbhem_estep_fused_trials, "vbhem_estep_fused_trials"))
+            self._fused_args = (key, fn, name, args)
+        _, fn, name, args = self._fused_args
+        _capi.check(fn(*args), name)
         return res
 
     def fallback_count(self) -> int:
