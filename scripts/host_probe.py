@@ -21,6 +21,9 @@ def med(f, n=50):
 
 
 def main():
+    if os.environ.get("VBHEM_SPIN"):  # spin-wait synchronisation (before the device is set up)
+        hip = ctypes.CDLL("libamdhip64.so")
+        print("hipSetDeviceFlags(spin) ->", hip.hipSetDeviceFlags(int(os.environ["VBHEM_SPIN"])))
     import torch
     import pkgload
     vb = pkgload.load()
