@@ -172,6 +172,10 @@ def main():
     ap.add_argument("--tau", type=int, default=None, help="override tau (experiments only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--em-iters", type=int, default=10,
+                    help="EM iterations timed for the em_iteration block (0: skip)")
+    ap.add_argument("--no-shard-sim", action="store_true",
+                    help="skip the single-GPU run at the 8-GPU shard size (N/8 bases)")
     args = ap.parse_args()
 
     import numpy as np
@@ -278,7 +282,8 @@ def main():
         n_gated = int(ng.item())
 
     # the dense schedule (both sweeps for every pair, same outputs) on the same
-    # inputs, for reference: a few steps, reported beside `value`
+    # inputs, for reference: a few steps, reported beside `value`, then its fb
+    # kernel (K2-K4 for every pair) timed alone for its roofline fraction
     dense_steps = max(1, min(args.steps, 5))
     prev_mode = _capi.set_fused_mode(_capi.FUSED_DENSE)
     step()
@@ -293,17 +298,90 @@ def main():
     dtd = torch.tensor([time.perf_counter() - td0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dtd, op=dist.ReduceOp.MAX)
+    _capi.timing_read()
+    _capi.timing_enable(True, fb_only=True)
+    for _ in range(dense_steps):
+        step()
+    torch.cuda.synchronize()
+    tkd = _capi.timing_read()
+    _capi.timing_enable(False)
     _capi.set_fused_mode(prev_mode)
     dense_rel = float((dstats - stats).abs().max() / stats.abs().max().clamp_min(1e-300))
 
-    # host M-step + ELBO cost of one full EM iteration (reported, not in value)
+    # one whole EM iteration as an EM loop pays it (the C++ loop, vbhem_em_run): the
+    # E-step, the all-reduce, the statistics' copy to the host, the bound, the M-step
+    # and the next iteration's psi prelude + constant upload
+    def em_iteration(engine, n_total):
+        if args.em_iters <= 0:
+            return None
+        from vbhem_amd import native_em
+        o = dict(opt, minDiff=0.0)          # no early stop: exactly max_iter + 1 iterations
+        native_em.run(post, engine, o, total_N=n_total, allreduce=allreduce, max_iter=1)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        r = native_em.run(post, engine, o, total_N=n_total, allreduce=allreduce,
+                          max_iter=args.em_iters - 1)
+        torch.cuda.synchronize()
+        dt_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
+        return dict(ms=float(dt_.item()) / r.iters * 1e3, iterations=r.iters,
+                    per_s=r.iters / float(dt_.item()))
+
+    em_it = em_iteration(eng, N)
+    step()   # hat_Z / L_elbo of the bench's own constants again (the EM run moved them)
+
+    # host math of one EM iteration in C++ (vbhem_em_host_iteration: bound, M-step,
+    # next prelude; replicated on every rank), and the Python host path for reference
+    from vbhem_amd import native_em
+    hst = stats.numpy().copy()
+    hi = native_em.HostIteration(post, opt, cov)
+    hi(hst)
+    nrep = 200
     th0 = time.perf_counter()
-    st = host.unpack_stats(stats.numpy(), K, S, d, cov)
+    for _ in range(nrep):
+        hi(hst)
+    host_ms = (time.perf_counter() - th0) / nrep * 1e3
+    th0 = time.perf_counter()
+    st = host.unpack_stats(hst, K, S, d, cov)
     Nj = st["Nj"] + 1e-50
     L = host.lower_bound(st["Lt1"], st["Lt7"], Nj, logOm, post, consts, opt, cov)
     host.mstep(host.finish_statistics(st, cov), Nj, opt, cov, post.W0mode)
     host.cluster_constants(post, cov)
-    host_ms = (time.perf_counter() - th0) * 1e3
+    host_py_ms = (time.perf_counter() - th0) * 1e3
+
+    # strong-scaling simulation on this GPU: rank 0's shard of an 8-GPU run (the
+    # first N/8 bases of the same N-base set), E-step and EM iteration
+    shard_sim = None
+    if world == 1 and not args.no_shard_sim and N >= 8 * 64:
+        ns = N // 8
+        base_s, _, _ = vb.synth_workload(args.config, device=dev, N=N, shard=(0, ns))
+        eng_s = EStepEngine(base_s, K, S, T, device=dev)
+        eng_s.set_clusters(consts)
+        eng_s.set_log_omega(logOm)
+        tN_s = (float(opt["Nv"]) * N) * eng_s.base.omega
+        hs = eng_s.host_stats_buffer()
+        for _ in range(3):
+            eng_s.fused(tN_s, out=hs)
+            torch.cuda.current_stream(dev).synchronize()
+        nss = max(20, args.steps)
+        ts0 = time.perf_counter()
+        for _ in range(nss):
+            eng_s.fused(tN_s, out=hs)
+            torch.cuda.current_stream(dev).synchronize()
+        es_ms = (time.perf_counter() - ts0) / nss * 1e3
+        em_s = em_iteration(eng_s, N)
+        shard_sim = {"bases": ns, "estep_ms": es_ms,
+                     "estep_ceiling_8gpu": (dt / args.steps * 1e3) / es_ms,
+                     "em_iteration": em_s,
+                     "em_ceiling_8gpu_excl_allreduce": (em_it["ms"] / em_s["ms"]
+                                                        if em_it and em_s else None),
+                     "note": ("one GPU running rank 0's shard of an 8-GPU strong-scaling run; "
+                              "the ceilings divide the full-N time by the shard time and leave "
+                              "out the RCCL all-reduce of the packed statistics")}
+        del eng_s
 
     if rank != 0:
         if world > 1:
@@ -330,6 +408,9 @@ def main():
                  if split else "vbhem::fb_pairs_kernel")
     traffic, traffic_src = committed_traffic(args.config, N, world, kname)
     gf_ms = tkb["gated_fwd_ms"] / max(1, tkb["gated_fwd_launches"])
+    dense_ms = tkd["fb_ms"] / max(1, tkd["fb_launches"])
+    dense_fpp = fb_flops_per_pair(S, Sb, T) if split else flops_per_pair(S, Sb, d, T, cov)
+    dense_ach = dense_fpp * tkd["fb_pairs"] / max(1, tkd["fb_launches"]) / (dense_ms * 1e-3) / 1e12
     res = {
         "metric": METRIC,
         "value": args.steps / dt,
@@ -392,12 +473,23 @@ def main():
                            "achieved_TFLOPs": fb_flops_per_pair(S, Sb, T) * n_gated / world
                            / max(gf_ms * 1e-3, 1e-12) / 1e12} if gated else None),
         "dense_schedule": {"value": dense_steps / float(dtd.item()), "unit": "E-steps/s",
-                           "steps": dense_steps, "max_rel_diff_vs_gated": dense_rel},
+                           "steps": dense_steps, "max_rel_diff_vs_gated": dense_rel,
+                           "fb_kernel": (f"vbhem::fb_split_kernel<{S}, {lpc}, 0>" if split
+                                         else "vbhem::fb_pairs_kernel"),
+                           "fb_kernel_ms": dense_ms,
+                           "roofline_frac": dense_ach / PEAK_FP64_TFLOPS,
+                           "achieved_TFLOPs": dense_ach,
+                           "flops_per_pair": dense_fpp},
         "emission_kernel_ms": tkb["em_ms"] / max(1, tkb["em_launches"]),
         "stats_kernels_ms_per_step": tkb["stats_ms"] / bd_steps,
         "breakdown_steps": bd_steps,
-        "reference_equivalent_tflops_per_s": flops_per_pair(S, Sb, d, T, cov) * N * K * args.steps / dt / 1e12,
         "host_mstep_ms": host_ms,
+        "host_mstep_note": ("per-iteration host math of the C++ EM loop "
+                            "(vbhem_em_host_iteration: bound, M-step, next psi prelude), "
+                            "replicated on every rank; host_math_python_ms: the Python path"),
+        "host_math_python_ms": host_py_ms,
+        "em_iteration": em_it,
+        "shard_sim": shard_sim,
         "elbo": L,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -101,6 +101,9 @@ EXPORTS = {
     "vbhem_em_lower_bound": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp, _vp,
                                       _vp, _vp, _vp, ctypes.POINTER(ctypes.c_double)]),
     "vbhem_em_mstep": (_c_int, [ctypes.POINTER(EmOptT), _vp, ctypes.POINTER(PostT)]),
+    "vbhem_em_host_iteration": (_c_int, [ctypes.POINTER(EmOptT), _vp, ctypes.POINTER(PostT), _vp,
+                                         _vp, _vp, _vp, _vp, _vp, _vp,
+                                         ctypes.POINTER(ctypes.c_double)]),
     "vbhem_em_workspace_bytes": (_c_size, [ctypes.POINTER(BaseT), _c_int, _c_int, _c_int]),
     "vbhem_em_run": (_c_int, [ctypes.POINTER(BaseT), _vp, _c_int, ctypes.POINTER(EmOptT),
                               ctypes.POINTER(PostT), _vp, ctypes.POINTER(_c_int),

@@ -101,12 +101,16 @@ def vbhem_h3m_c(base: BaseSet, opt: dict, device="cuda", engine_factory=None,
         uniq = unique_ll(LLall, 2 * opt["minDiff"] * 10)
         one = make(base, K, S, opt["tau"], trials=1)
         hyp_info = {}
+        # vbhem_h3m_c.m:102-105: every bound is invalidated; only the re-optimised
+        # unique trials get one back (:157), so only they can be chosen
+        LLall = np.full_like(LLall, np.nan)
         for q in uniq:
             h = hyp.vbhem_h3m_c_hyp(base, opt, results[q].post, one)
             results[q] = h["result"]
             LLall[q] = h["result"].LL
             hyp_info[q] = h
-    best = int(np.argmax(LLall))
+    # vbhem_h3m_c.m:163: MATLAB's max skips NaN (all NaN: the first entry)
+    best = 0 if np.all(np.isnan(LLall)) else int(np.nanargmax(LLall))
     res = results[best]
     out = dict(result=res, LL=float(LLall[best]), LLall=LLall, best=best, K=K, S=S,
                hyp=hyp_info[best] if hyp_info and best in hyp_info else None)
@@ -124,9 +128,10 @@ def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda
     ``base``: an already converted h3m_b (skips the conversion)."""
     Ks = [int(k) for k in np.atleast_1d(K)]
     Ss = [int(s) for s in np.atleast_1d(S)]
+    opt = dict(opt or {})
     if base is None:
         from .vbhmm_em import vbhmm_remove_empty
-        if opt is None or opt.get("remove_empty", 1):
+        if opt.get("remove_empty", 1):
             hmms = [vbhmm_remove_empty(h, 1e-3) if h is not None else None for h in hmms]
         base = hmms_to_h3m_hem(hmms, COV_FULL, use_post=True)
     if len(Ks) > 1:
@@ -144,6 +149,6 @@ def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda
         h = dict(outs[ind])
         h.update(model_LL_S=LLs, model_S=Ss, model_bestS=Ss[ind], model_all_s=outs)
         return h
-    o = default_options(Ks[0], Ss[0], base.d, **{k: v for k, v in (opt or {}).items()
+    o = default_options(Ks[0], Ss[0], base.d, **{k: v for k, v in opt.items()
                                                   if k not in ("K", "S")})
     return vbhem_h3m_c(base, o, device, engine_factory)

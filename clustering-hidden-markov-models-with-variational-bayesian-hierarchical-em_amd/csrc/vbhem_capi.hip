@@ -729,6 +729,9 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   if (!logOmega_dev || !stats_dev ||
       (base->N > 0 && (!tildeN_dev || !hatZ_dev || !LL_elbo_dev)))
     return fail(VBHEM_ERR_ARG, "null fused argument");
+  if (vbhem::resp_lds(clus->K, clus->K / R) > kLdsLimit)
+    return fail(VBHEM_ERR_UNSUPPORTED, "fused: too many clusters for the responsibilities "
+                                       "kernel (K <= ~2,400)");
   FusedWs w;
   const size_t need = carve_fused(nullptr, base, clus, T, w, R);
   if (!workspace_dev || workspace_bytes < need)
@@ -757,8 +760,10 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   ctx.u_ws = w.U;
   // gated schedule: split kernel + list statistics tile must apply
   size_t sl_lds = 0;
+  // (gate lists: per-wave ballot masks of all K clusters in LDS, K up to ~2,400)
   const bool gated = g_fused_mode == VBHEM_FUSED_GATED && ctx.split.ok && ctx.split.lds_l &&
-                     vbhem::plan_stats_list(sa, sl_lds);
+                     vbhem::plan_stats_list(sa, sl_lds) &&
+                     vbhem::gate_list_lds(K) <= kLdsLimit;
   if (R > 1 && !gated)
     return fail(VBHEM_ERR_UNSUPPORTED,
                 "trials need the gated schedule (split-kernel shapes: S <= 16, Sb <= S)");

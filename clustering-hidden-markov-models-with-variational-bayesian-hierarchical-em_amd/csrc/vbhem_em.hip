@@ -332,6 +332,18 @@ int vbhem_em_mstep(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t 
   return VBHEM_OK;
 }
 
+int vbhem_em_host_iteration(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t *post,
+                             double *logA, double *logPi, double *m, double *P, double *c,
+                             double *logLambdaTilde, double *logOmega, double *L) {
+  if (!L) return VBHEM_ERR_ARG;
+  int rc = vbhem_em_lower_bound(post, opt, stats, logLambdaTilde, logA, logPi, logOmega, L);
+  if (rc != VBHEM_OK) return rc;
+  if (std::isnan(*L)) return VBHEM_OK;  // step_fc.m:338-374: no M-step for an unstable model
+  rc = vbhem_em_mstep(opt, stats, post);
+  if (rc != VBHEM_OK) return rc;
+  return vbhem_em_prelude(post, logA, logPi, m, P, c, logLambdaTilde, logOmega);
+}
+
 size_t vbhem_em_workspace_bytes(const vbhem_base_t *base, int K, int S, int T) {
   if (!base || K < 1 || S < 1) return 0;
   const int d = base->d;
@@ -372,11 +384,11 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
   double lastL = -DBL_MAX, L = -INFINITY;
   int it = 0;
   *stable = 1;
+  double *hA = h.data(), *hPi = hA + nA, *hm = hPi + nPi, *hP = hm + nm, *hc = hP + nP,
+         *hO = hc + nc;
+  int rc = vbhem_em_prelude(post, hA, hPi, hm, hP, hc, lLT.data(), hO);
+  if (rc != VBHEM_OK) return rc;
   while (true) {
-    double *hA = h.data(), *hPi = hA + nA, *hm = hPi + nPi, *hP = hm + nm, *hc = hP + nP,
-           *hO = hc + nc;
-    int rc = vbhem_em_prelude(post, hA, hPi, hm, hP, hc, lLT.data(), hO);
-    if (rc != VBHEM_OK) return rc;
     hipError_t e = hipMemcpyAsync(dc, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return VBHEM_ERR_HIP;
     rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hatZ_dev, LL_dev,
@@ -386,18 +398,18 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     e = hipMemcpyAsync(stats.data(), stats_dev, slen * sizeof(double), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return VBHEM_ERR_HIP;
-    rc = vbhem_em_lower_bound(post, opt, stats.data(), lLT.data(), hA, hPi, hO, &L);
+    // the bound of this iteration's E-step, then (stable) the M-step and the next
+    // iteration's prelude: the whole per-iteration host math, one call
+    rc = vbhem_em_host_iteration(opt, stats.data(), post, hA, hPi, hm, hP, hc, lLT.data(), hO, &L);
     if (rc != VBHEM_OK) return rc;
-    bool do_break = false;
-    if (it > 1 && std::fabs((L - lastL) / lastL) <= opt->minDiff) do_break = true;
-    if (it == opt->max_iter) do_break = true;
     if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, stop before the M-step
       L = -INFINITY;
       *stable = 0;
       break;
     }
-    rc = vbhem_em_mstep(opt, stats.data(), post);
-    if (rc != VBHEM_OK) return rc;
+    bool do_break = false;
+    if (it > 1 && std::fabs((L - lastL) / lastL) <= opt->minDiff) do_break = true;
+    if (it == opt->max_iter) do_break = true;
     LogLs[it] = L;
     ++it;
     lastL = L;

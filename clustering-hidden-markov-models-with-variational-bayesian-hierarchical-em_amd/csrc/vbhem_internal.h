@@ -269,6 +269,8 @@ hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st);
 hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds, hipStream_t st);
 bool plan_stats_list(StatsArgs &a, size_t &lds);
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st);
+size_t gate_list_lds(int K);  // dynamic LDS of gate_list_kernel for K clusters
+size_t resp_lds(int K, int KT);  // dynamic LDS of resp_kernel / resp_trials_kernel
 hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st);
 hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
                               hipStream_t st);

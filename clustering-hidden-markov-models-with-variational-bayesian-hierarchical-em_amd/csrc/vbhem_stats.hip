@@ -840,19 +840,27 @@ static hipError_t launch_stats_t(const StatsArgs &a, int nchunk, int ngroups, si
   return hipGetLastError();
 }
 
-hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
+size_t resp_lds(int K, int KT) {
   int G = 1;
-  while (G < a.K && G < 64) G <<= 1;
+  while (G < K && G < 64) G <<= 1;
+  const size_t R = KT >= 1 && K % KT == 0 ? (size_t)(K / KT) : 1;
+  return ((size_t)(kRespThreads / 64) * ((64 / G) * (size_t)K + 2 * R)) * sizeof(double) +
+         (size_t)K * sizeof(int);
+}
+
+hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
+  // per-wave Nj accumulators of all K clusters in LDS (past 64 KB at K ~ 960: the
+  // launch sets the dynamic-LDS attribute; the caller rejects K past a CU's LDS)
+  const size_t lds = resp_lds(a.K, a.KT);
   if (a.KT != a.K) {  // batched trials
     if (a.K > kRespSlots * 64 || a.KT < 1 || a.K % a.KT != 0) return hipErrorInvalidValue;
-    const int R = a.K / a.KT;
-    const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2 * R)) * sizeof(double) +
-                       (size_t)a.K * sizeof(int);
+    hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&resp_trials_kernel), lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(resp_trials_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
     return hipGetLastError();
   }
-  const size_t lds = ((size_t)(kRespThreads / 64) * ((64 / G) * a.K + 2)) * sizeof(double) +
-                     (size_t)a.K * sizeof(int);
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&resp_kernel), lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(resp_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
   return hipGetLastError();
 }
@@ -1199,10 +1207,18 @@ __global__ __launch_bounds__(64 * kSuWaves) void stats_list_g_kernel(const Stats
   su_output(p, red, zs, c, nch, j, tid);
 }
 
+size_t gate_list_lds(int K) {
+  const size_t ints = (size_t)2 * K + kListThreads / 64 + 2 * kListThreads;
+  return (ints + 1) / 2 * 2 * sizeof(int) +
+         (size_t)(kListThreads / 64) * K * sizeof(unsigned long long);
+}
+
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st) {
-  const size_t ints = (size_t)2 * a.K + kListThreads / 64 + 2 * kListThreads;
-  const size_t lds = (ints + 1) / 2 * 2 * sizeof(int) +
-                     (size_t)(kListThreads / 64) * a.K * sizeof(unsigned long long);
+  // the per-wave ballot masks grow with K: above 64 KB the launch needs the attribute
+  // (the caller keeps the gated schedule only while this fits a CU, gate_list_lds)
+  const size_t lds = gate_list_lds(a.K);
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&gate_list_kernel), lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(gate_list_kernel, dim3(nchunk), dim3(kListThreads), lds, st, a);
   return hipGetLastError();
 }

@@ -142,7 +142,7 @@ def _line_search(f, x0, f0, df0, d, s, a, i, P):
                 ok = True
                 if not np.isfinite(fv + sv):
                     raise FloatingPointError("Objective function returned Inf or NaN")
-            except (FloatingPointError, np.linalg.LinAlgError):
+            except Exception:  # noqa: BLE001 -- minimize_new.m:147-155: any error bisects
                 p3["x"] = (p1["x"] + p3["x"]) / 2       # bisect and retry
                 ok = False
                 p3["f"] = np.nan
@@ -184,7 +184,7 @@ def _minimize(X0, F, length, method, MFEPLS, MSR, mem):
     x0 = np.asarray(X0, dtype=float).reshape(-1)
     fx0, dfx0 = F(x0)
     dfx0 = np.asarray(dfx0, dtype=float).reshape(-1)
-    P = dict(MFEPLS=MFEPLS, SIG=0.5)
+    P = dict(MFEPLS=MFEPLS, SIG=0.1 if method in ("CG", "cg") else 0.5)
     fX = [fx0]
     i = 0
     x, dfx = x0, dfx0
@@ -265,7 +265,36 @@ def _minimize(X0, F, length, method, MFEPLS, MSR, mem):
             x0, dfx0 = x, dfx
             fX.append(fx0)
         return x0, np.array(fX), i
-    raise ValueError("method must be LBFGS or BFGS")
+    if method in ("CG", "cg"):
+        # minimize_new.m CG: Polack-Ribiere conjugate gradients, slope-ratio step
+        ok = False
+        r = -dfx0
+        s = float(-(r @ r))
+        b = -1.0 / (s - 1)
+        bs = np.float64(-1.0)
+        while i < abs(length):
+            b = b * bs / np.fmin(b * s, bs / MSR)
+            x, b, fx0, dfx, i = _line_search(F, x0, fx0, dfx0, r, s, b, i, P)
+            if i < 0:
+                i = -i
+                if ok:
+                    ok = False
+                    r = -dfx
+                else:
+                    break
+            else:
+                ok = True
+                bs = b * s
+                r = float(dfx @ (dfx - dfx0)) / float(dfx0 @ dfx0) * r - dfx
+            s = float(r @ dfx)
+            if s >= 0:
+                r = -dfx
+                s = float(r @ dfx)
+                ok = False
+            x0, dfx0 = x, dfx
+            fX.append(fx0)
+        return x0, np.array(fX), i
+    raise ValueError("method must be LBFGS, BFGS or CG")
 
 
 # ----------------------------------------------------------------------------
@@ -291,8 +320,11 @@ def vbhem_h3m_c_hyp(base: BaseSet, opt: dict, init_post: Posterior, engine: ESte
         return L, dL
 
     X0 = init_x(opt, info)
-    method = {"minimize-lbfgs": "LBFGS", "minimize-bfgs": "BFGS"}.get(
-        opt.get("minimizer", "minimize-lbfgs"), "LBFGS")
+    methods = {"minimize-lbfgs": "LBFGS", "minimize-bfgs": "BFGS", "minimize-cg": "CG"}
+    name = opt.get("minimizer", "minimize-lbfgs")
+    if name not in methods:                              # vbhem_h3m_c_hyp.m:51-52
+        raise ValueError("bad minimizer specified")
+    method = methods[name]
     Xopt, fX, nls = minimize(X0, grad, length=int(length or opt.get("hyp_length", 100)),
                              method=method)
     o2 = set_opt(Xopt, opt, info)

@@ -5,7 +5,8 @@
 in the library; Python only allocates the device buffers and, with several
 ranks, supplies the all-reduce of the packed statistics as a callback.  The
 host steps are also exposed one by one (:func:`prelude`, :func:`mstep`,
-:func:`lower_bound`) and are checked against :mod:`vbhem_amd.host`.
+:func:`lower_bound`) and as one call (:class:`HostIteration`), and are checked
+against :mod:`vbhem_amd.host`.
 """
 from __future__ import annotations
 
@@ -83,6 +84,27 @@ def lower_bound(stats: np.ndarray, post: Posterior, opt: dict, covmode: int, con
         ctypes.byref(pb.t), ctypes.byref(ob.t), _p(st), _p(c["logLambdaTilde"]), _p(c["logA"]),
         _p(c["logPi"]), _p(c["logOmega"]), ctypes.byref(L)), "vbhem_em_lower_bound")
     return float(L.value)
+
+
+class HostIteration:
+    """The per-iteration host math of the C++ EM loop (vbhem_em_host_iteration:
+    bound, M-step, next prelude) on fixed host buffers, callable repeatedly at
+    the cost of one C call (what bench.py times as the EM iteration's host part)."""
+
+    def __init__(self, post: Posterior, opt: dict, covmode: int):
+        self.pb, self.ob = _PostBuf(post, covmode), _OptBuf(opt)
+        self.pre = prelude(post, covmode)
+        self.L = ctypes.c_double()
+        self._args = None
+
+    def __call__(self, stats: np.ndarray) -> float:
+        st = np.ascontiguousarray(stats, dtype=np.float64)
+        if self._args is None or self._args[0] is not st:
+            self._args = (st, ctypes.byref(self.ob.t), _p(st), ctypes.byref(self.pb.t)) + tuple(
+                _p(self.pre[k]) for k in ("logA", "logPi", "m", "P", "c", "logLambdaTilde",
+                                           "logOmega")) + (ctypes.byref(self.L),)
+        _capi.check(_capi.lib().vbhem_em_host_iteration(*self._args[1:]), "vbhem_em_host_iteration")
+        return float(self.L.value)
 
 
 def run(post: Posterior, engine: EStepEngine, opt: dict, *, total_N: Optional[int] = None,

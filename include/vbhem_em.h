@@ -58,6 +58,15 @@ int vbhem_em_lower_bound(const vbhem_post_t *post, const vbhem_em_opt_t *opt,
  * (step_fc.m:396): the posterior is updated in place. */
 int vbhem_em_mstep(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t *post);
 
+/* The per-iteration host math of vbhem_em_run in one call: the bound of the
+ * iteration whose statistics are given (with that iteration's prelude outputs
+ * logA, logPi, logLambdaTilde, logOmega), then -- unless the bound is NaN -- the
+ * M-step (post updated in place) and the prelude of the next iteration (all seven
+ * prelude arrays overwritten).  *L receives the bound. */
+int vbhem_em_host_iteration(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t *post,
+                            double *logA, double *logPi, double *m, double *P, double *c,
+                            double *logLambdaTilde, double *logOmega, double *L);
+
 /* Optional cross-device reduction of the packed statistics (device pointer, n
  * doubles, the launch stream): called once per iteration between the E-step and
  * the host math.  Return 0 on success. */

@@ -2,12 +2,14 @@
  * integration/h3m_mex_common.h -- shared by the two MEX gateways
  * (vbhem_hmm_bwd_fwd_mex.c, hem_hmm_bwd_fwd_mex.c): scalar/field parsing, the
  * host buffers, the base-HMM repack (column-major cells -> row-major, padded to
- * maxN states) and the output scatter into MATLAB cells.  The two reference
+ * maxN states), the cluster repack (clusters of different sizes: mex.c:436-437,
+ * 506) and the per-pair outputs scattered into MATLAB cells.  The two reference
  * gateways share this code too (mex.c:288-409, 459-473, 1108-1122, 1312-1345 /
  * hem_hmm_bwd_fwd_mex.c:288-409).
  */
 #ifndef H3M_MEX_COMMON_H
 #define H3M_MEX_COMMON_H
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -34,6 +36,8 @@ static inline const double *field_pr(const mxArray *s, const char *name, size_t 
 }
 
 typedef struct {
+  int SB;                                  /* base stride (maxN)             */
+  int *N2;                                 /* [Kr] cluster state counts       */
   int *nstates;
   double *prior, *A, *centres, *covars;
   double *logA, *logPi, *m, *P, *c;
@@ -41,6 +45,7 @@ typedef struct {
 } buffers_t;
 
 static inline void free_buffers(buffers_t *b) {
+  mxFree(b->N2);
   mxFree(b->nstates);
   mxFree(b->prior);
   mxFree(b->A);
@@ -64,6 +69,7 @@ static inline void pack_bases(buffers_t *bp, const mxArray *h3m_b, int Kb, int S
                               int covmode) {
   buffers_t b = *bp;
   const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
+  b.SB = SB;
   b.nstates = (int *)mxCalloc((size_t)(Kb ? Kb : 1), sizeof(int));
   b.prior = (double *)mxCalloc((size_t)Kb * SB + 1, sizeof(double));
   b.A = (double *)mxCalloc((size_t)Kb * SB * SB + 1, sizeof(double));
@@ -111,58 +117,104 @@ static inline void pack_bases(buffers_t *bp, const mxArray *h3m_b, int Kb, int S
 }
 
 
-/* cluster HMMs (mex.c:433-457): every cluster has S = maxN2 states.  Fills
- * b->logA, logPi, m, P, c; full covariances take c and P from
- * logdetCovPlusDdivlamR / invCovR (mex.c:785-830), diagonal ones from the emit
- * fields (mex.c:718-760). */
-static inline void pack_clusters(buffers_t *bp, const mxArray *h3m_r, int Kr, int S, int d,
-                                 int covmode, const mxArray *logdetR, const mxArray *invCovR) {
-  buffers_t b = *bp;
-  const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
-  b.logA = (double *)mxCalloc((size_t)Kr * S * S, sizeof(double));
-  b.logPi = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
-  b.m = (double *)mxCalloc((size_t)Kr * S * d, sizeof(double));
-  b.P = (double *)mxCalloc((size_t)Kr * S * dd, sizeof(double));
-  b.c = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
+/* Cluster state counts (mex.c:436-437: N2 = rows of the cluster's transition
+ * field, one per cluster, looped with at :506).  Fills N2[Kr]; returns S = max N2,
+ * the stride the clusters are packed at.  Every N2 must be square and <= maxN2. */
+static inline int cluster_sizes(const mxArray *h3m_r, int Kr, const char *afield, int maxN2,
+                                int *N2) {
+  int S = 0;
   for (int j = 0; j < Kr; j++) {
     const mxArray *hr = mxGetCell(h3m_r, j);
-    if (!hr || !mxIsStruct(hr)) {
-      *bp = b;
-      free_buffers(bp);
+    if (!hr || !mxIsStruct(hr))
       mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d} must be a struct", j + 1);
-    }
-    const mxArray *lA = mxGetField(hr, 0, "logATilde");
-    if (!lA || (int)mxGetM(lA) != S || (int)mxGetN(lA) != S) {
-      *bp = b;
-      free_buffers(bp);
-      mexErrMsgIdAndTxt("vbhem_mex:unsupported",
-                        "h3m_r{%d}.logATilde must be maxN2 x maxN2 (all clusters equal size)", j + 1);
-    }
-    const double *pA = mxGetPr(lA);
-    const double *pPi = field_pr(hr, "logPiTilde", (size_t)S, "h3m_r");
+    const mxArray *lA = mxGetField(hr, 0, afield);
+    const int n = lA ? (int)mxGetM(lA) : 0;
+    if (!lA || n < 1 || (int)mxGetN(lA) != n || n > maxN2)
+      mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d}.%s must be N2 x N2 with N2 <= maxN2",
+                        j + 1, afield);
+    N2[j] = n;
+    if (n > S) S = n;
+  }
+  return S;
+}
+
+static inline void alloc_clusters(buffers_t *b, int Kr, int S, int d, size_t dd) {
+  b->N2 = (int *)mxCalloc((size_t)Kr, sizeof(int));
+  b->logA = (double *)mxCalloc((size_t)Kr * S * S, sizeof(double));
+  b->logPi = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
+  b->m = (double *)mxCalloc((size_t)Kr * S * d, sizeof(double));
+  b->P = (double *)mxCalloc((size_t)Kr * S * dd, sizeof(double));
+  b->c = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
+}
+
+/* Padding of a cluster with N2 < S states to the common stride S (only the fused
+ * gateway runs padded clusters: its responsibilities need every cluster in one
+ * launch).  Padded states are unreachable: no transition into them and zero
+ * prior (log = -inf), so their forward occupancy is 0 up to the restricted exp's
+ * floor exp(-700) ~ 1e-304 (vbhem_math.h), and the real states' recursions see
+ * them only through A' = exp(-inf) = 0.  A padded row moves uniformly to every
+ * state (log 1/S), so its own column sums stay well above the underflow guard;
+ * its emission constants (m = 0, P = 0, c = 0) give a finite E = -d log(2 pi)/2. */
+static inline void pad_clusters(buffers_t *b, int Kr, int S, int d, size_t dd) {
+  for (int j = 0; j < Kr; j++) {
+    const int n = b->N2[j];
     for (int r = 0; r < S; r++) {
+      for (int s = 0; s < S; s++) {
+        double *a = b->logA + ((size_t)j * S + r) * S + s;
+        if (r >= n) *a = -log((double)S);
+        else if (s >= n) *a = -INFINITY;
+      }
+      if (r >= n) {
+        b->logPi[(size_t)j * S + r] = -INFINITY;
+        b->c[(size_t)j * S + r] = 0.0;
+        memset(b->m + ((size_t)j * S + r) * d, 0, sizeof(double) * (size_t)d);
+        memset(b->P + ((size_t)j * S + r) * dd, 0, sizeof(double) * dd);
+      }
+    }
+  }
+}
+
+/* cluster HMMs (mex.c:433-457), N2[j] <= S states each, packed at stride S.
+ * Fills b->N2, logA, logPi, m, P, c; full covariances take c and P from
+ * logdetCovPlusDdivlamR / invCovR (mex.c:785-830: {1 x N2} and [d x d x N2]),
+ * diagonal ones from the emit fields (mex.c:718-760).  Returns S. */
+static inline int pack_clusters(buffers_t *bp, const mxArray *h3m_r, int Kr, int maxN2, int d,
+                                int covmode, const mxArray *logdetR, const mxArray *invCovR) {
+  buffers_t b = *bp;
+  const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
+  int *n2 = (int *)mxCalloc((size_t)Kr, sizeof(int));
+  const int S = cluster_sizes(h3m_r, Kr, "logATilde", maxN2, n2);
+  alloc_clusters(&b, Kr, S, d, dd);
+  memcpy(b.N2, n2, sizeof(int) * (size_t)Kr);
+  mxFree(n2);
+  for (int j = 0; j < Kr; j++) {
+    const mxArray *hr = mxGetCell(h3m_r, j);
+    const int n = b.N2[j];
+    const double *pA = mxGetPr(mxGetField(hr, 0, "logATilde"));
+    const double *pPi = field_pr(hr, "logPiTilde", (size_t)n, "h3m_r");
+    for (int r = 0; r < n; r++) {
       b.logPi[(size_t)j * S + r] = pPi[r];
-      for (int s = 0; s < S; s++) b.logA[((size_t)j * S + r) * S + s] = pA[r + (size_t)s * S];
+      for (int s = 0; s < n; s++) b.logA[((size_t)j * S + r) * S + s] = pA[r + (size_t)s * n];
     }
     const mxArray *emit = mxGetField(hr, 0, "emit");
     const double *ldet = NULL, *icov = NULL;
     if (covmode == VBHEM_COV_FULL) {
       const mxArray *lc = mxGetCell(logdetR, j), *ic = mxGetCell(invCovR, j);
-      if (!lc || mxGetNumberOfElements(lc) != (size_t)S || !ic ||
-          mxGetNumberOfElements(ic) != (size_t)S * d * d) {
+      if (!lc || mxGetNumberOfElements(lc) != (size_t)n || !ic ||
+          mxGetNumberOfElements(ic) != (size_t)n * d * d) {
         *bp = b;
-      free_buffers(bp);
+        free_buffers(bp);
         mexErrMsgIdAndTxt("vbhem_mex:invalidinput",
                           "logdetCovPlusDdivlamR{%d} / invCovR{%d} have wrong sizes", j + 1, j + 1);
       }
       ldet = mxGetPr(lc);
       icov = mxGetPr(ic);
     }
-    for (int s = 0; s < S; s++) {
+    for (int s = 0; s < n; s++) {
       const mxArray *es = emit ? mxGetCell(emit, s) : NULL;
       if (!es) {
         *bp = b;
-      free_buffers(bp);
+        free_buffers(bp);
         mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d}.emit{%d} missing", j + 1, s + 1);
       }
       const double *pm = field_pr(es, "m", (size_t)d, "h3m_r emit");
@@ -183,57 +235,122 @@ static inline void pack_clusters(buffers_t *bp, const mxArray *h3m_r, int Kr, in
       }
     }
   }
-
+  pad_clusters(&b, Kr, S, d, dd);
   *bp = b;
+  return S;
 }
 
-/* outputs (mex.c:396-409, 1108-1122, 1312-1345), column-major */
-static inline void scatter_outputs(mxArray *plhs[], const buffers_t *bp, int Kb, int Kr, int S,
-                                   int d, int covmode) {
+/* The per-pair entry points (vbhem_estep_pairs_host / vhem_estep_pairs_host)
+ * behind one signature. */
+typedef int (*pairs_host_fn)(void *ctx, const vbhem_base_t *base, const vbhem_cluster_t *clus,
+                             int T, double *LL, double *nu1, double *pr, double *mu, double *Mu,
+                             double *xi);
+
+/* The per-pair gateways' computation and outputs (mex.c:396-409, 1108-1122,
+ * 1312-1345; column-major, N2[j]-shaped cells per cluster).  Clusters of
+ * different sizes (mex.c:506) run as one library call per distinct N2 on the
+ * clusters of that size, unpadded: every pair's outputs are those of a call with
+ * only its own cluster, as in the reference's per-cluster loop. */
+static inline void run_pairs_grouped(mxArray *plhs[], buffers_t *bp, int Kb, int Kr, int S,
+                                     int d, int covmode, int T, pairs_host_fn fn, void *ctx,
+                                     const char *fname) {
   const buffers_t b = *bp;
+  const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
   plhs[0] = mxCreateDoubleMatrix(Kb, Kr, mxREAL);
   for (int k = 1; k < 6; k++) plhs[k] = mxCreateCellMatrix(Kb, Kr);
-  double *LL = mxGetPr(plhs[0]);
-  for (int i = 0; i < Kb; i++) {
-    for (int j = 0; j < Kr; j++) {
-      const size_t p = (size_t)i * Kr + j;       /* row-major pair index */
-      const size_t cell = (size_t)i + (size_t)j * Kb; /* IX(i,j,Kb,Kr) */
-      LL[cell] = b.LL[p];
-      mxArray *a_nu = mxCreateDoubleMatrix(1, S, mxREAL);
-      mxArray *a_pr = mxCreateDoubleMatrix(S, 1, mxREAL);
-      mxArray *a_mu = mxCreateDoubleMatrix(S, d, mxREAL);
-      mxArray *a_Mu;
-      if (covmode == VBHEM_COV_FULL) {
-        mwSize dims[3] = {(mwSize)S, (mwSize)d, (mwSize)d};
-        a_Mu = mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
-      } else {
-        a_Mu = mxCreateDoubleMatrix(S, d, mxREAL);
+  double *LLo = mxGetPr(plhs[0]);
+  int *idx = (int *)mxCalloc((size_t)Kr, sizeof(int));
+  for (int n = 1; n <= S; n++) {
+    int cnt = 0;
+    for (int j = 0; j < Kr; j++)
+      if (b.N2[j] == n) idx[cnt++] = j;
+    if (cnt == 0) continue;
+    /* this size's clusters, compact at stride n */
+    double *gA = (double *)mxCalloc((size_t)cnt * n * n, sizeof(double));
+    double *gPi = (double *)mxCalloc((size_t)cnt * n, sizeof(double));
+    double *gm = (double *)mxCalloc((size_t)cnt * n * d, sizeof(double));
+    double *gP = (double *)mxCalloc((size_t)cnt * n * dd, sizeof(double));
+    double *gc = (double *)mxCalloc((size_t)cnt * n, sizeof(double));
+    for (int g = 0; g < cnt; g++) {
+      const int j = idx[g];
+      for (int r = 0; r < n; r++) {
+        gPi[(size_t)g * n + r] = b.logPi[(size_t)j * S + r];
+        gc[(size_t)g * n + r] = b.c[(size_t)j * S + r];
+        for (int s = 0; s < n; s++)
+          gA[((size_t)g * n + r) * n + s] = b.logA[((size_t)j * S + r) * S + s];
+        memcpy(gm + ((size_t)g * n + r) * d, b.m + ((size_t)j * S + r) * d, sizeof(double) * d);
+        memcpy(gP + ((size_t)g * n + r) * dd, b.P + ((size_t)j * S + r) * dd, sizeof(double) * dd);
       }
-      mxArray *a_xi = mxCreateDoubleMatrix(S, S, mxREAL);
-      double *o_nu = mxGetPr(a_nu), *o_pr = mxGetPr(a_pr), *o_mu = mxGetPr(a_mu);
-      double *o_Mu = mxGetPr(a_Mu), *o_xi = mxGetPr(a_xi);
-      for (int s = 0; s < S; s++) {
-        o_nu[s] = b.nu1[p * S + s];
-        o_pr[s] = b.pr[p * S + s];
-        for (int a = 0; a < d; a++) {
-          o_mu[s + (size_t)a * S] = b.mu[(p * S + s) * d + a];
-          if (covmode == VBHEM_COV_FULL) {
-            for (int c2 = 0; c2 < d; c2++)
-              o_Mu[s + (size_t)a * S + (size_t)c2 * S * d] =
-                  b.Mu[((p * S + s) * d + a) * d + c2];
-          } else {
-            o_Mu[s + (size_t)a * S] = b.Mu[(p * S + s) * d + a];
-          }
-        }
-        for (int s2 = 0; s2 < S; s2++) o_xi[s + (size_t)s2 * S] = b.xi[(p * S + s) * S + s2];
-      }
-      mxSetCell(plhs[1], cell, a_nu);
-      mxSetCell(plhs[2], cell, a_pr);
-      mxSetCell(plhs[3], cell, a_mu);
-      mxSetCell(plhs[4], cell, a_Mu);
-      mxSetCell(plhs[5], cell, a_xi);
     }
+    const size_t np = (size_t)Kb * cnt;
+    double *LL = (double *)mxCalloc(np + 1, sizeof(double));
+    double *nu1 = (double *)mxCalloc(np * n + 1, sizeof(double));
+    double *pr = (double *)mxCalloc(np * n + 1, sizeof(double));
+    double *mu = (double *)mxCalloc(np * n * d + 1, sizeof(double));
+    double *Mu = (double *)mxCalloc(np * n * dd + 1, sizeof(double));
+    double *xi = (double *)mxCalloc(np * n * n + 1, sizeof(double));
+    if (Kb > 0) {
+      vbhem_base_t base = {Kb, b.SB, d, covmode, b.nstates, b.prior, b.A, b.centres, b.covars, NULL};
+      vbhem_cluster_t clus = {cnt, n, gA, gPi, gm, gP, gc};
+      const int st = fn(ctx, &base, &clus, T, LL, nu1, pr, mu, Mu, xi);
+      if (st != VBHEM_OK) {
+        free_buffers(bp);
+        mexErrMsgIdAndTxt("vbhem_mex:gpu", "%s failed (%d): %s", fname, st, vbhem_last_error());
+      }
+    }
+    for (int i = 0; i < Kb; i++) {
+      for (int g = 0; g < cnt; g++) {
+        const int j = idx[g];
+        const size_t p = (size_t)i * cnt + g;           /* row-major pair index of the call */
+        const size_t cell = (size_t)i + (size_t)j * Kb;  /* IX(i,j,Kb,Kr) */
+        LLo[cell] = LL[p];
+        mxArray *a_nu = mxCreateDoubleMatrix(1, n, mxREAL);
+        mxArray *a_pr = mxCreateDoubleMatrix(n, 1, mxREAL);
+        mxArray *a_mu = mxCreateDoubleMatrix(n, d, mxREAL);
+        mxArray *a_Mu;
+        if (covmode == VBHEM_COV_FULL) {
+          mwSize dims[3] = {(mwSize)n, (mwSize)d, (mwSize)d};
+          a_Mu = mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
+        } else {
+          a_Mu = mxCreateDoubleMatrix(n, d, mxREAL);
+        }
+        mxArray *a_xi = mxCreateDoubleMatrix(n, n, mxREAL);
+        double *o_nu = mxGetPr(a_nu), *o_pr = mxGetPr(a_pr), *o_mu = mxGetPr(a_mu);
+        double *o_Mu = mxGetPr(a_Mu), *o_xi = mxGetPr(a_xi);
+        for (int s = 0; s < n; s++) {
+          o_nu[s] = nu1[p * n + s];
+          o_pr[s] = pr[p * n + s];
+          for (int a = 0; a < d; a++) {
+            o_mu[s + (size_t)a * n] = mu[(p * n + s) * d + a];
+            if (covmode == VBHEM_COV_FULL) {
+              for (int c2 = 0; c2 < d; c2++)
+                o_Mu[s + (size_t)a * n + (size_t)c2 * n * d] = Mu[((p * n + s) * d + a) * d + c2];
+            } else {
+              o_Mu[s + (size_t)a * n] = Mu[(p * n + s) * d + a];
+            }
+          }
+          for (int s2 = 0; s2 < n; s2++) o_xi[s + (size_t)s2 * n] = xi[(p * n + s) * n + s2];
+        }
+        mxSetCell(plhs[1], cell, a_nu);
+        mxSetCell(plhs[2], cell, a_pr);
+        mxSetCell(plhs[3], cell, a_mu);
+        mxSetCell(plhs[4], cell, a_Mu);
+        mxSetCell(plhs[5], cell, a_xi);
+      }
+    }
+    mxFree(gA);
+    mxFree(gPi);
+    mxFree(gm);
+    mxFree(gP);
+    mxFree(gc);
+    mxFree(LL);
+    mxFree(nu1);
+    mxFree(pr);
+    mxFree(mu);
+    mxFree(Mu);
+    mxFree(xi);
   }
+  mxFree(idx);
 }
 
 #endif /* H3M_MEX_COMMON_H */

@@ -18,11 +18,20 @@
  *   full: c = logdetCovR{j}(k), P = invCovR{j}(:,:,k)  (:585-600)
  *   diag: c = sum(log(covars)), P = 1 ./ covars        (:711-733)
  * and the kernels divide the expected emission log-likelihood by `smooth`
- * (:848-860).  The GPU device is taken from VBHEM_DEVICE (default 0).
+ * (:848-860).  Reduced HMMs may have different state counts N2 <= maxN2: one
+ * library call per distinct N2.  The GPU device is taken from VBHEM_DEVICE (default 0).
  */
 #include <math.h>
 
 #include "h3m_mex_common.h"
+
+static int call_pairs(void *ctx, const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      double *LL, double *nu1, double *pr, double *mu, double *Mu, double *xi) {
+  const char *dev_env = getenv("VBHEM_DEVICE");
+  const int device = dev_env ? atoi(dev_env) : 0;
+  return vhem_estep_pairs_host(device, base, clus, T, *(const double *)ctx, LL, nu1, pr, mu, Mu,
+                               xi);
+}
 
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   if ((nrhs != 6) && (nrhs != 8))
@@ -52,7 +61,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
                       "invalid sizes (Kr=%d Kb=%d T=%d maxN=%d maxN2=%d smooth=%g)", Kr, Kb, T,
                       maxN, maxN2, smooth);
 
-  /* ---- reduced HMMs (:428-447): all clusters must have maxN2 states ----------------- */
+  /* ---- reduced HMMs (:428-447; N2 per cluster) -------------------------------- */
   int d = -1;
   {
     const mxArray *hr = mxGetCell(h3m_r, 0);
@@ -62,39 +71,29 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     if (!c0) mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{1}.emit{1}.centres missing");
     d = (int)mxGetNumberOfElements(c0);
   }
-  const int S = maxN2, SB = maxN;
   const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
   buffers_t b;
   memset(&b, 0, sizeof(b));
-  b.logA = (double *)mxCalloc((size_t)Kr * S * S, sizeof(double));
-  b.logPi = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
-  b.m = (double *)mxCalloc((size_t)Kr * S * d, sizeof(double));
-  b.P = (double *)mxCalloc((size_t)Kr * S * dd, sizeof(double));
-  b.c = (double *)mxCalloc((size_t)Kr * S, sizeof(double));
+  int *n2 = (int *)mxCalloc((size_t)Kr, sizeof(int));
+  const int S = cluster_sizes(h3m_r, Kr, "A", maxN2, n2);
+  alloc_clusters(&b, Kr, S, d, dd);
+  memcpy(b.N2, n2, sizeof(int) * (size_t)Kr);
+  mxFree(n2);
   for (int j = 0; j < Kr; j++) {
     const mxArray *hr = mxGetCell(h3m_r, j);
-    if (!hr || !mxIsStruct(hr)) {
-      free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{%d} must be a struct", j + 1);
-    }
-    const mxArray *mA = mxGetField(hr, 0, "A");
-    if (!mA || (int)mxGetM(mA) != S || (int)mxGetN(mA) != S) {
-      free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:unsupported",
-                        "h3m_r{%d}.A must be maxN2 x maxN2 (all clusters equal size)", j + 1);
-    }
-    const double *pA = mxGetPr(mA);
-    const double *pPi = field_pr(hr, "prior", (size_t)S, "h3m_r");
-    for (int r = 0; r < S; r++) {
+    const int n = b.N2[j];
+    const double *pA = mxGetPr(mxGetField(hr, 0, "A"));
+    const double *pPi = field_pr(hr, "prior", (size_t)n, "h3m_r");
+    for (int r = 0; r < n; r++) {
       b.logPi[(size_t)j * S + r] = log(pPi[r]);
-      for (int s = 0; s < S; s++) b.logA[((size_t)j * S + r) * S + s] = log(pA[r + (size_t)s * S]);
+      for (int s = 0; s < n; s++) b.logA[((size_t)j * S + r) * S + s] = log(pA[r + (size_t)s * n]);
     }
     const mxArray *emit = mxGetField(hr, 0, "emit");
     const double *ldet = NULL, *icov = NULL;
     if (covmode == VBHEM_COV_FULL) {
       const mxArray *lc = mxGetCell(logdetR, j), *ic = mxGetCell(invCovR, j);
-      if (!lc || mxGetNumberOfElements(lc) != (size_t)S || !ic ||
-          mxGetNumberOfElements(ic) != (size_t)S * d * d) {
+      if (!lc || mxGetNumberOfElements(lc) != (size_t)n || !ic ||
+          mxGetNumberOfElements(ic) != (size_t)n * d * d) {
         free_buffers(&b);
         mexErrMsgIdAndTxt("vbhem_mex:invalidinput",
                           "logdetCovR{%d} / invCovR{%d} have wrong sizes", j + 1, j + 1);
@@ -102,7 +101,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
       ldet = mxGetPr(lc);
       icov = mxGetPr(ic);
     }
-    for (int s = 0; s < S; s++) {
+    for (int s = 0; s < n; s++) {
       const mxArray *es = emit ? mxGetCell(emit, s) : NULL;
       if (!es) {
         free_buffers(&b);
@@ -129,30 +128,10 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     }
   }
 
-  pack_bases(&b, h3m_b, Kb, SB, d, covmode);
+  pack_bases(&b, h3m_b, Kb, maxN, d, covmode);
 
-  /* ---- compute on the GPU ---------------------------------------------------- */
-  const size_t np = (size_t)Kb * Kr;
-  b.LL = (double *)mxCalloc(np + 1, sizeof(double));
-  b.nu1 = (double *)mxCalloc(np * S + 1, sizeof(double));
-  b.pr = (double *)mxCalloc(np * S + 1, sizeof(double));
-  b.mu = (double *)mxCalloc(np * S * d + 1, sizeof(double));
-  b.Mu = (double *)mxCalloc(np * S * dd + 1, sizeof(double));
-  b.xi = (double *)mxCalloc(np * S * S + 1, sizeof(double));
-  if (Kb > 0) {
-    vbhem_base_t base = {Kb, SB, d, covmode, b.nstates, b.prior, b.A, b.centres, b.covars};
-    vbhem_cluster_t clus = {Kr, S, b.logA, b.logPi, b.m, b.P, b.c};
-    const char *dev_env = getenv("VBHEM_DEVICE");
-    const int device = dev_env ? atoi(dev_env) : 0;
-    const int st = vhem_estep_pairs_host(device, &base, &clus, T, smooth, b.LL, b.nu1, b.pr, b.mu,
-                                         b.Mu, b.xi);
-    if (st != VBHEM_OK) {
-      free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:gpu", "vhem_estep_pairs_host failed (%d): %s", st,
-                        vbhem_last_error());
-    }
-  }
-
-  scatter_outputs(plhs, &b, Kb, Kr, S, d, covmode);
+  /* ---- compute on the GPU, one call per distinct cluster size ----------------- */
+  double sm = smooth;
+  run_pairs_grouped(plhs, &b, Kb, Kr, S, d, covmode, T, call_pairs, &sm, "vhem_estep_pairs_host");
   free_buffers(&b);
 }

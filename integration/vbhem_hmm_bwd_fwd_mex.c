@@ -15,6 +15,8 @@
  * gateway only repacks MATLAB's column-major cell/struct data into the dense
  * row-major arrays of vbhem_base_t / vbhem_cluster_t, calls
  * vbhem_estep_pairs_host(), and scatters the results back into MATLAB cells.
+ * Clusters may have different state counts N2 <= maxN2 (mex.c:436-437, 506): one
+ * library call per distinct N2, outputs shaped per cluster as the reference's.
  *
  * Emission constants, as the reference kernel reads them:
  *   full: c = logdetCovPlusDdivlamR{j}(rho), P = invCovR{j}(:,:,rho)   (mex.c:785-830)
@@ -27,6 +29,14 @@
  * test double of the mx API (tests/mxshim) so the gateway itself is tested.
  */
 #include "h3m_mex_common.h"
+
+static int call_pairs(void *ctx, const vbhem_base_t *base, const vbhem_cluster_t *clus, int T,
+                      double *LL, double *nu1, double *pr, double *mu, double *Mu, double *xi) {
+  (void)ctx;
+  const char *dev_env = getenv("VBHEM_DEVICE");
+  const int device = dev_env ? atoi(dev_env) : 0;
+  return vbhem_estep_pairs_host(device, base, clus, T, LL, nu1, pr, mu, Mu, xi);
+}
 
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   if ((nrhs != 5) && (nrhs != 7))
@@ -54,7 +64,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "invalid sizes (Kr=%d Kb=%d T=%d maxN=%d maxN2=%d)",
                       Kr, Kb, T, maxN, maxN2);
 
-  /* ---- cluster HMMs (mex.c:433-457): all clusters must have maxN2 states -------- */
+  /* ---- cluster HMMs (mex.c:433-457; N2 per cluster, :436-437) ---------------- */
   int d = -1;
   {
     const mxArray *hr = mxGetCell(h3m_r, 0);
@@ -64,36 +74,13 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     if (!m0) mexErrMsgIdAndTxt("vbhem_mex:invalidinput", "h3m_r{1}.emit{1}.m missing");
     d = (int)mxGetN(m0);
   }
-  const int S = maxN2, SB = maxN;
-  const size_t dd = (covmode == VBHEM_COV_FULL) ? (size_t)d * d : (size_t)d;
   buffers_t b;
   memset(&b, 0, sizeof(b));
-  pack_clusters(&b, h3m_r, Kr, S, d, covmode, logdetR, invCovR);
+  const int S = pack_clusters(&b, h3m_r, Kr, maxN2, d, covmode, logdetR, invCovR);
+  pack_bases(&b, h3m_b, Kb, maxN, d, covmode);
 
-  pack_bases(&b, h3m_b, Kb, SB, d, covmode);
-
-  /* ---- compute on the GPU ---------------------------------------------------- */
-  const size_t np = (size_t)Kb * Kr;
-  b.LL = (double *)mxCalloc(np + 1, sizeof(double));
-  b.nu1 = (double *)mxCalloc(np * S + 1, sizeof(double));
-  b.pr = (double *)mxCalloc(np * S + 1, sizeof(double));
-  b.mu = (double *)mxCalloc(np * S * d + 1, sizeof(double));
-  b.Mu = (double *)mxCalloc(np * S * dd + 1, sizeof(double));
-  b.xi = (double *)mxCalloc(np * S * S + 1, sizeof(double));
-  if (Kb > 0) {
-    vbhem_base_t base = {Kb, SB, d, covmode, b.nstates, b.prior, b.A, b.centres, b.covars};
-    vbhem_cluster_t clus = {Kr, S, b.logA, b.logPi, b.m, b.P, b.c};
-    const char *dev_env = getenv("VBHEM_DEVICE");
-    const int device = dev_env ? atoi(dev_env) : 0;
-    const int st = vbhem_estep_pairs_host(device, &base, &clus, T, b.LL, b.nu1, b.pr, b.mu, b.Mu,
-                                          b.xi);
-    if (st != VBHEM_OK) {
-      free_buffers(&b);
-      mexErrMsgIdAndTxt("vbhem_mex:gpu", "vbhem_estep_pairs_host failed (%d): %s", st,
-                        vbhem_last_error());
-    }
-  }
-
-  scatter_outputs(plhs, &b, Kb, Kr, S, d, covmode);
+  /* ---- compute on the GPU, one call per distinct cluster size ----------------- */
+  run_pairs_grouped(plhs, &b, Kb, Kr, S, d, covmode, T, call_pairs, NULL,
+                    "vbhem_estep_pairs_host");
   free_buffers(&b);
 }

@@ -92,11 +92,13 @@ class Mx:
         return [plhs[k] for k in range(nlhs)], None
 
 
-def matlab_h3m(mx: Mx, base: dict, consts: dict, post: dict | None = None):
-    """(h3m_b.hmm, h3m_r.hmm, extra full-cov args) as MATLAB values."""
+def matlab_h3m(mx: Mx, base: dict, consts: dict, post: dict | None = None, sizes=None):
+    """(h3m_b.hmm, h3m_r.hmm, extra full-cov args) as MATLAB values.  ``sizes``:
+    per-cluster state counts N2[j] <= S (cluster j keeps its first N2[j] states)."""
     cov = base["covmode"]
     N = base["prior"].shape[0]
-    K, S = consts["logPi"].shape
+    K, S0 = consts["logPi"].shape
+    sizes = [S0] * K if sizes is None else [int(x) for x in sizes]
     hb = []
     for i in range(N):
         n = int(base["nstates"][i])
@@ -107,6 +109,7 @@ def matlab_h3m(mx: Mx, base: dict, consts: dict, post: dict | None = None):
                             A=mx.double(base["A"][i, :n, :n]), emit=mx.cell(emit)))
     hr = []
     for j in range(K):
+        S = sizes[j]
         emit = []
         for s in range(S):
             f = dict(m=mx.double(consts["m"][j, s]))
@@ -115,11 +118,18 @@ def matlab_h3m(mx: Mx, base: dict, consts: dict, post: dict | None = None):
                 f.update(W=mx.double(consts["P"][j, s]), v=mx.double(1.0),
                          logLambdaTildePlusDdivlamda=mx.double(consts["c"][j, s]))
             emit.append(mx.struct(**f))
-        hr.append(mx.struct(logATilde=mx.double(consts["logA"][j]),
-                            logPiTilde=mx.double(consts["logPi"][j].reshape(S, 1)),
+        hr.append(mx.struct(logATilde=mx.double(consts["logA"][j, :S, :S]),
+                            logPiTilde=mx.double(consts["logPi"][j, :S].reshape(S, 1)),
                             emit=mx.cell(emit)))
     extra = []
     if cov == 1:
-        extra = [mx.cell([mx.double(consts["c"][j]) for j in range(K)]),
-                 mx.cell([mx.double(np.transpose(consts["P"][j], (1, 2, 0))) for j in range(K)])]
+        extra = [mx.cell([mx.double(consts["c"][j, :sizes[j]]) for j in range(K)]),
+                 mx.cell([mx.double(np.transpose(consts["P"][j, :sizes[j]], (1, 2, 0)))
+                          for j in range(K)])]
     return mx.cell(hb), mx.cell(hr), extra
+
+
+def cluster_consts(consts: dict, j: int, n: int) -> dict:
+    """The E-step constants of cluster j alone, its first n states (K = 1)."""
+    return {k: np.ascontiguousarray(v[j:j + 1, :n, :n] if k == "logA" else v[j:j + 1, :n])
+            for k, v in consts.items() if k in ("logA", "logPi", "m", "P", "c")}

@@ -73,3 +73,52 @@ def test_hyp_learning_cpu(vb):
     # the final run uses the optimised hyperparameters, clipped into range
     for name in ("alpha0", "eta0", "epsilon0", "lambda0"):
         assert o["hyps_min"][name] <= out["vbopt"][name] <= o["hyps_max"][name]
+
+
+def test_hyp_best_only_among_reoptimised(vb, monkeypatch):
+    """vbhem_h3m_c.m:102-105, 157-164: after hyperparameter learning every bound is
+    NaN except those of the unique (re-optimised) trials, so a duplicate trial
+    whose original bound beats the re-optimised one can not win."""
+    from vbhem_amd import cluster, em, hyp
+    base = _exprmt1(vb, N=10)
+    o = vb.default_options(2, 2, 2, **dict(OPT, trials=3, max_iter=6, learn_hyps=1))
+    fake_ll = iter([-100.0, -100.0, -50.0])          # trial bounds: 0 and 1 are duplicates
+
+    real = em.vbhem_h3m_c_trials
+
+    def trials(posts, eng, opt):
+        out = real(posts, eng, opt)
+        out.LLall = np.array([next(fake_ll) for _ in posts])
+        return out
+
+    calls = []
+
+    def fake_hyp(base_, opt_, post, eng):
+        calls.append(post)
+        r = em.vbhem_h3m_c_step_fc(post, eng, dict(opt_, max_iter=2))
+        r.LL = -1e9                                   # re-optimised bound far below the rest
+        return dict(result=r)
+
+    monkeypatch.setattr(em, "vbhem_h3m_c_trials", trials)
+    monkeypatch.setattr(hyp, "vbhem_h3m_c_hyp", fake_hyp)
+    out = cluster.vbhem_h3m_c(base, o, engine_factory=_factory)
+    # unique trials: 0 and 2 (1 duplicates 0); both re-optimised to -1e9
+    assert len(calls) == 2
+    assert np.isnan(out["LLall"][1]) and out["best"] in (0, 2) and out["LL"] == -1e9
+    assert out["hyp"] is not None
+
+
+def test_cluster_vector_k_without_opt(vb):
+    """vbhem_h3m_cluster with a vector of K and opt=None (defaults) runs."""
+    from vbhem_amd import cluster
+    base = _exprmt1(vb, N=8)
+    calls = []
+
+    def fake_c(base_, o, device, engine_factory):
+        calls.append((o["K"], o["S"]))
+        return dict(LL=-float(o["K"]), K=o["K"], S=o["S"])
+
+    import unittest.mock as um
+    with um.patch.object(cluster, "vbhem_h3m_c", fake_c):
+        res = cluster.vbhem_h3m_cluster(None, [1, 2], 2, None, base=base)
+    assert calls == [(1, 2), (2, 2)] and res["model_bestK"] in (1, 2)

@@ -16,12 +16,14 @@ def mx(hem_gateway):
     return Mx(shim, gw)
 
 
-def matlab_vhem(mx: Mx, base: dict, red: dict):
+def matlab_vhem(mx: Mx, base: dict, red: dict, sizes=None):
     """(h3m_b.hmm, h3m_r.hmm as point-estimate HMMs, extra full-cov args) as MATLAB
-    values; the extras are computed as hem_h3m_c_step.m:198-205 does."""
+    values; the extras are computed as hem_h3m_c_step.m:198-205 does.  ``sizes``:
+    per-cluster state counts (the first N2[j] states of each reduced HMM)."""
     cov = base["covmode"]
     N = base["prior"].shape[0]
-    K, S = red["prior"].shape
+    K, S0 = red["prior"].shape
+    sizes = [S0] * K if sizes is None else list(sizes)
     d = base["centres"].shape[2]
     hb = []
     for i in range(N):
@@ -33,16 +35,17 @@ def matlab_vhem(mx: Mx, base: dict, red: dict):
                             A=mx.double(base["A"][i, :n, :n]), emit=mx.cell(emit)))
     hr = []
     for j in range(K):
+        S = sizes[j]
         emit = [mx.struct(centres=mx.double(red["centres"][j, s]),
                           covars=mx.double(red["covars"][j, s]), nin=mx.double(d))
                 for s in range(S)]
-        hr.append(mx.struct(prior=mx.double(red["prior"][j].reshape(S, 1)),
-                            A=mx.double(red["A"][j]), emit=mx.cell(emit)))
+        hr.append(mx.struct(prior=mx.double(red["prior"][j, :S].reshape(S, 1)),
+                            A=mx.double(red["A"][j, :S, :S]), emit=mx.cell(emit)))
     extra = []
     if cov == 1:
         cv = np.asarray(red["covars"])
-        extra = [mx.cell([mx.double(np.log(np.linalg.det(cv[j]))) for j in range(K)]),
-                 mx.cell([mx.double(np.transpose(np.linalg.inv(cv[j]), (1, 2, 0)))
+        extra = [mx.cell([mx.double(np.log(np.linalg.det(cv[j, :sizes[j]]))) for j in range(K)]),
+                 mx.cell([mx.double(np.transpose(np.linalg.inv(cv[j, :sizes[j]]), (1, 2, 0)))
                           for j in range(K)])]
     return mx.cell(hb), mx.cell(hr), extra
 
@@ -110,3 +113,34 @@ def test_vhem_gateway_matches_oracle(mx, vo, cov, ragged, smooth):
             assert rel_err(mu, ref["emit_mu"][i, j]) < RTOL_PAIRS
             assert rel_err(Mu, ref["emit_Mu"][i, j]) < RTOL_PAIRS
             assert rel_err(xi, ref["sum_xi"][i, j]) < RTOL_PAIRS
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cov", [1, 0])
+def test_vhem_gateway_mixed_cluster_sizes(mx, vo, cov):
+    """Reduced HMMs of different sizes: N2[j]-shaped outputs equal the VHEM oracle
+    run on reduced HMM j alone (its first N2[j] states, as given)."""
+    N, K, S, Sb, d, T, smooth = 5, 3, 4, 3, 2, 5, 1.5
+    sizes = [2, 4, 3]
+    cs = make_case(N, K, S, Sb, d, cov, seed=64 + cov, ragged=True, tau=T)
+    base = cs["base"]
+    red = make_reduced(K, S, d, cov, seed=64 + cov)
+    hb, hr, extra = matlab_vhem(mx, base, red, sizes=sizes)
+    out, err = mx.call(6, [hb, hr, mx.double(T), mx.double(smooth), mx.double(Sb),
+                           mx.double(S)] + extra)
+    assert err is None, err
+    LL = mx.to_numpy(out[0])
+    for j, n in enumerate(sizes):
+        rj = {k: np.ascontiguousarray(v[j:j + 1, :n, :n] if k == "A" else v[j:j + 1, :n])
+              for k, v in red.items()}
+        ref = vo.c_vhem_estep_pairs(base, rj, T, smooth)
+        assert rel_err(LL[:, j], ref["LL_elbo"][:, 0]) < RTOL_PAIRS
+        for i in range(N):
+            cell = i + j * N
+            xi = mx.to_numpy(mx.cell_item(out[5], cell))
+            Mu = mx.to_numpy(mx.cell_item(out[4], cell))
+            assert xi.shape == (n, n)
+            assert rel_err(xi, ref["sum_xi"][i, 0]) < RTOL_PAIRS
+            assert rel_err(Mu, ref["emit_Mu"][i, 0]) < RTOL_PAIRS
+            assert rel_err(mx.to_numpy(mx.cell_item(out[1], cell))[0],
+                           ref["sum_nu_1"][i, 0]) < RTOL_PAIRS

@@ -86,7 +86,7 @@ def test_clip_flags(vb):
     assert fl["v0"][0] == 0 and o["v0"] == 5.0
 
 
-@pytest.mark.parametrize("method", ["LBFGS", "BFGS"])
+@pytest.mark.parametrize("method", ["LBFGS", "BFGS", "CG"])
 def test_minimize_rosenbrock(vb, method):
     from vbhem_amd.hyp import minimize
 
@@ -99,6 +99,32 @@ def test_minimize_rosenbrock(vb, method):
     assert np.allclose(x, [1.0, 1.0], atol=1e-6) and fX[-1] < 1e-10
     assert np.all(np.diff(fX) <= 1e-12)          # every accepted line search descends
     assert nls <= 100
+
+
+def test_minimize_bisects_on_any_error(vb):
+    """minimize_new.m:147-155 catches ANY error of the objective during
+    extrapolation and bisects: an exception other than a floating-point one
+    (e.g. a C-ABI error on extreme hyperparameters) must not end the run."""
+    from vbhem_amd.hyp import minimize
+    calls = []
+
+    def F(x):
+        calls.append(float(x[0]))
+        if len(calls) == 5:                      # the 4th extrapolation point fails once
+            raise RuntimeError("vbhem_estep_fused: status -2")
+        return (x[0] - 1.9) ** 2, np.array([2 * (x[0] - 1.9)])
+
+    x, fX, _ = minimize(np.array([-10.0]), F, length=20, method="LBFGS")
+    assert abs(x[0] - 1.9) < 1e-6 and len(calls) > 6
+
+
+def test_minimizer_names(vb):
+    """vbhem_h3m_c_hyp.m:34-52: lbfgs / bfgs / cg, anything else is an error."""
+    from vbhem_amd import hyp
+    opt = dict(minimizer="fminunc", m0=np.zeros(2), W0=1.0, alpha0=1.0, eta0=1.0,
+               epsilon0=1.0, lambda0=1.0, v0=5.0)
+    with pytest.raises(ValueError, match="bad minimizer"):
+        hyp.vbhem_h3m_c_hyp(None, opt, None, None, length=1)
 
 
 def test_minimize_quadratic_exact(vb):

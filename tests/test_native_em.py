@@ -108,3 +108,30 @@ def test_native_em_c4_slice_vs_oracle(vb, vo):
     np.testing.assert_allclose(res.LogLs, ref["LogLs"], rtol=RTOL_NORTH_STAR)
     for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
         assert post_err(getattr(res.post, k), ref["post"][k]) < RTOL_NORTH_STAR, k
+
+
+@pytest.mark.parametrize("name,cov,S", CASES, ids=[c[0] for c in CASES])
+def test_host_iteration_matches_steps(vb, vo, name, cov, S):
+    """vbhem_em_host_iteration (one call: bound, M-step, next prelude) equals the
+    three host steps in sequence, and a NaN bound leaves the posterior untouched."""
+    from vbhem_amd import native_em
+    cs = make_case(8, 3, S, 3, 3, cov, seed=51 + cov, tau=6)
+    vec = packed_stats(vb, vo, cs, cov)
+    P, opt = cs["P"], cs["opt"]
+    hi = native_em.HostIteration(P, opt, cov)
+    L = hi(vec)
+    pre = native_em.prelude(P, cov)
+    assert L == native_em.lower_bound(vec, P, opt, cov, pre)
+    post1 = native_em.mstep(vec, P, opt, cov)
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert np.array_equal(hi.pb.a[k], getattr(post1, k)), k
+    pre1 = native_em.prelude(post1, cov)
+    for k, v in pre1.items():
+        assert np.array_equal(hi.pre[k], v), k
+    bad = vec.copy()
+    K = 3
+    bad[K + K * S + K * S * S] = np.nan          # Lt1
+    before = {k: v.copy() for k, v in hi.pb.a.items()}
+    assert np.isnan(hi(bad))
+    for k, v in before.items():
+        assert np.array_equal(hi.pb.a[k], v, equal_nan=True), k

@@ -195,3 +195,40 @@ def test_fused_into_pinned_host_memory(vb, trials):
                 os.environ["VBHEM_GROUP_BASES"] = old
     with pytest.raises(Exception):
         eng.fused(tN, out=torch.zeros(eng.stats_len, dtype=torch.float64))  # pageable memory
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1200, 2300])
+def test_fused_many_clusters(vb, K):
+    """A single-trial fused call with K in the thousands: the responsibilities'
+    per-wave accumulators (8 B per cluster and wave) and the gate lists' ballot
+    masks pass 64 KB of LDS, so the launches set the dynamic-LDS attribute; the
+    gated result equals the dense schedule's.  Past a CU's 160 KB the call is
+    rejected as unsupported."""
+    from vbhem_amd import _capi, host
+    cs = make_case(40, 2, 2, 2, 2, 1, seed=45, tau=4)
+    c0 = cs["consts"]
+    rng = np.random.default_rng(K)
+    reps = (K + 1) // 2
+    consts = {k: np.concatenate([np.asarray(c0[k])] * reps)[:K] for k in c0}
+    consts["m"] = consts["m"] + rng.normal(0.0, 0.5, consts["m"].shape)
+    logOm = np.full(K, np.log(1.0 / K))
+    tN = _tn(cs)
+    eng = _engine(vb, cs, consts=consts)
+    eng.set_log_omega(logOm)
+    gated = eng.fused(tN).clone()
+    prev = _capi.set_fused_mode(_capi.FUSED_DENSE)
+    try:
+        dense = eng.fused(tN).clone()
+    finally:
+        _capi.set_fused_mode(prev)
+    torch.cuda.synchronize()
+    assert rel_err(gated.cpu().numpy(), dense.cpu().numpy()) < 1e-12
+    st = host.unpack_stats(gated.cpu().numpy(), K, 2, 2, 1)
+    assert abs(st["Nj"].sum() - float(tN.sum())) < 1e-9 * float(tN.sum())
+    if K == 2300:
+        big = {k: np.concatenate([v, v[:2500]]) for k, v in consts.items()}
+        e2 = _engine(vb, cs, consts=big)
+        e2.set_log_omega(np.full(K + 2500, np.log(1.0 / (K + 2500))))
+        with pytest.raises(Exception, match="too many clusters"):
+            e2.fused(tN)
