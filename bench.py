@@ -172,6 +172,8 @@ def main():
     ap.add_argument("--tau", type=int, default=None, help="override tau (experiments only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-sample", action="store_true")
+    ap.add_argument("--parity-seconds", type=float, default=4.0)
     ap.add_argument("--em-iters", type=int, default=10,
                     help="EM iterations timed for the em_iteration block (0: skip)")
     ap.add_argument("--no-shard-sim", action="store_true",
@@ -312,23 +314,33 @@ def main():
     # E-step, the all-reduce, the statistics' copy to the host, the bound, the M-step
     # and the next iteration's psi prelude + constant upload
     def em_iteration(engine, n_total):
+        """Per-iteration cost of the C++ EM loop: two runs of different length, the
+        difference of their times over the difference of their iteration counts
+        (the per-run setup -- posterior upload, workspace, result copies -- cancels)."""
         if args.em_iters <= 0:
             return None
         from vbhem_amd import native_em
         o = dict(opt, minDiff=0.0)          # no early stop: exactly max_iter + 1 iterations
-        native_em.run(post, engine, o, total_N=n_total, allreduce=allreduce, max_iter=1)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        r = native_em.run(post, engine, o, total_N=n_total, allreduce=allreduce,
-                          max_iter=args.em_iters - 1)
-        torch.cuda.synchronize()
-        dt_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
-        return dict(ms=float(dt_.item()) / r.iters * 1e3, iterations=r.iters,
-                    per_s=r.iters / float(dt_.item()))
+
+        def timed(n):
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            r = native_em.run(post, engine, o, total_N=n_total, allreduce=allreduce, max_iter=n)
+            torch.cuda.synchronize()
+            dt_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
+            return float(dt_.item()), r.iters
+
+        timed(1)
+        t_a, n_a = timed(1)
+        t_b, n_b = timed(1 + args.em_iters)
+        ms = (t_b - t_a) / max(1, n_b - n_a) * 1e3
+        return dict(ms=ms, per_s=1e3 / ms, iterations=n_b - n_a,
+                    method=("(t(run of %d iterations) - t(run of %d)) / %d: the per-run setup "
+                            "cancels" % (n_b, n_a, n_b - n_a)))
 
     em_it = em_iteration(eng, N)
     step()   # hat_Z / L_elbo of the bench's own constants again (the EM run moved them)
@@ -500,12 +512,34 @@ def main():
         res["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
                                                   "host_nproc", "host_cpu")}
         res["cpu_baseline_multithread"] = cb["multi"]
-        g = eng.LL[:n].cpu().numpy()
-        r = pr["LL_elbo"]
-        res["parity_sample"] = {"LL_elbo_max_rel_err": float(np.max(np.abs(g - r)) /
-                                                           max(1e-300, np.max(np.abs(r)))),
-                                "pairs": int(n * K)}
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
+    if world == 1 and not args.no_parity_sample:
+        # the checker on bases spread evenly over all N (every base group of a large
+        # run), 16 host threads, ~ --parity-seconds of CPU: L_elbo and hat_Z of the
+        # bench's own E-step (hat_Z of a base depends on its own L_elbo row only)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import vbhem_oracle as vo  # checker only
+        base_np = eng.base.numpy() if hasattr(eng.base, "numpy") else base.numpy()
+        thr = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+        t0p = time.perf_counter()
+        vo.c_estep_pairs(vo.base_subset(base_np, slice(0, 8)), consts, T, nthreads=1)
+        per_base = (time.perf_counter() - t0p) / 8 / max(1, thr)
+        nps = int(min(N, max(16, args.parity_seconds / max(per_base, 1e-9))))
+        idx = np.unique(np.linspace(0, N - 1, nps).astype(np.int64))
+        ref = vo.c_estep_pairs(vo.base_subset(base_np, idx), consts, T, nthreads=thr)
+        hz_ref, _ = vo.c_responsibilities(ref["LL_elbo"], tN.cpu().numpy()[idx], logOm)
+        g = eng.LL.cpu().numpy()[idx]
+        hz = eng.hatZ.cpu().numpy()[idx]
+        ll_err = float(np.max(np.abs(g - ref["LL_elbo"]) /
+                              np.maximum(np.abs(ref["LL_elbo"]), 1e-300)))
+        hz_big = hz_ref > 1e-8
+        hz_err = float(max(np.max(np.abs(hz - hz_ref)[hz_big] / hz_ref[hz_big], initial=0.0),
+                           np.max(np.abs(hz - hz_ref)[~hz_big], initial=0.0)))
+        res["parity_sample"] = {"LL_elbo_max_rel_err": ll_err, "hat_Z_max_err": hz_err,
+                                "pairs": int(idx.size * K), "bases": int(idx.size),
+                                "sample": ("bases evenly spaced over all N (every base group), "
+                                           "oracle/vbhem_oracle.c on %d host threads" % thr),
+                                "tolerance": {"LL_elbo": 1e-10, "hat_Z": 1e-5}}
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

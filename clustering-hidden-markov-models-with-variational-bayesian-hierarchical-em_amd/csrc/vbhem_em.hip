@@ -15,10 +15,12 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
 #include "vbhem_em.h"
+#include "vbhem_em_dev.h"
 
 namespace {
 
@@ -39,10 +41,54 @@ double psi(double x) {
   return acc + std::log(x) - 0.5 * r - series;
 }
 
+// sum_{q=1..d} psi((v + 1 - q) / 2) (step_fc.m:136): the arguments are two chains
+// v/2, v/2 - 1, ... and (v-1)/2, (v-1)/2 - 1, ...; one psi per chain, the rest by
+// psi(x - 1) = psi(x) - 1/(x - 1)
+double psi_sum_half(double v, int d) {
+  double acc = 0.0;
+  for (int c = 0; c < 2 && c < d; ++c) {
+    double x = 0.5 * (v - c), p = psi(x);
+    for (int q = c; q < d; q += 2) {
+      acc += p;
+      x -= 1.0;
+      p -= 1.0 / x;
+    }
+  }
+  return acc;
+}
+
+// sum_{q=1..d} lgamma((v + 1 - q) / 2) (vbhemh3m_lb.m:81-83), the same two chains
+// with lgamma(x - 1) = lgamma(x) - log(x - 1)
+double lgamma_sum_half(double v, int d) {
+  double acc = 0.0;
+  for (int c = 0; c < 2 && c < d; ++c) {
+    double x = 0.5 * (v - c), g = std::lgamma(x);
+    for (int q = c; q < d; q += 2) {
+      acc += g;
+      x -= 1.0;
+      if (q + 2 < d) g -= std::log(x);
+    }
+  }
+  return acc;
+}
+
+// per-thread scratch of the d x d factorisations (no allocation per matrix)
+struct LuScratch {
+  std::vector<double> a, x;
+  std::vector<int> piv;
+  void size(int d) {
+    if ((int)piv.size() < d) {
+      a.resize((size_t)d * d);
+      x.resize((size_t)d);
+      piv.resize((size_t)d);
+    }
+  }
+};
+thread_local LuScratch tl_lu;
+
 // LU with partial pivoting of a d x d row-major matrix (in place); returns det.
-double lu_det(std::vector<double> &a, int d, std::vector<int> &piv) {
+double lu_det(double *a, int d, int *piv) {
   double det = 1.0;
-  piv.resize(d);
   for (int k = 0; k < d; ++k) {
     int p = k;
     for (int r = k + 1; r < d; ++r)
@@ -65,19 +111,22 @@ double lu_det(std::vector<double> &a, int d, std::vector<int> &piv) {
 }
 
 double det_of(const double *m, int d) {
-  std::vector<double> a(m, m + (size_t)d * d);
-  std::vector<int> piv;
-  return lu_det(a, d, piv);
+  LuScratch &s = tl_lu;
+  s.size(d);
+  std::copy(m, m + (size_t)d * d, s.a.begin());
+  return lu_det(s.a.data(), d, s.piv.data());
 }
 
 // inverse through the LU factors (solve for the identity columns)
 void inv_of(const double *m, int d, double *out) {
-  std::vector<double> a(m, m + (size_t)d * d);
-  std::vector<int> piv;
+  LuScratch &s = tl_lu;
+  s.size(d);
+  double *a = s.a.data(), *x = s.x.data();
+  int *piv = s.piv.data();
+  std::copy(m, m + (size_t)d * d, a);
   lu_det(a, d, piv);
   for (int col = 0; col < d; ++col) {
-    std::vector<double> x(d, 0.0);
-    x[col] = 1.0;
+    for (int r = 0; r < d; ++r) x[r] = r == col ? 1.0 : 0.0;
     for (int k = 0; k < d; ++k) std::swap(x[k], x[piv[k]]);
     for (int r = 0; r < d; ++r)
       for (int c = 0; c < r; ++c) x[r] -= a[(size_t)r * d + c] * x[c];
@@ -140,8 +189,7 @@ int vbhem_em_prelude(const vbhem_post_t *post, double *logA, double *logPi, doub
     for (int s = 0; s < S; ++s) {
       const size_t ks = (size_t)k * S + s;
       const double v = post->v[ks];
-      double t1 = 0.0;
-      for (int q = 1; q <= d; ++q) t1 += psi(0.5 * (v + 1.0) - 0.5 * q);
+      const double t1 = psi_sum_half(v, d);
       const double *W = post->W + ks * dd;
       double logdet;
       if (full) {
@@ -192,8 +240,7 @@ int vbhem_em_lower_bound(const vbhem_post_t *post, const vbhem_em_opt_t *opt,
   double logdetW0inv = 0.0;
   if (opt->W0_len == 1) logdetW0inv = d * std::log(W0inv[0]);
   else for (int a = 0; a < d; ++a) logdetW0inv += std::log(W0inv[(size_t)a * d + a]);
-  double sg0 = 0.0;
-  for (int q = 1; q <= d; ++q) sg0 += std::lgamma(0.5 * (v0 + 1 - q));
+  const double sg0 = lgamma_sum_half(v0, d);
   const double logCalpha0 = std::lgamma(K * a0) - K * std::lgamma(a0);
   const double logCeta0 = std::lgamma(S * e0) - S * std::lgamma(e0);
   const double logCepsilon0 = std::lgamma(S * ep0) - S * std::lgamma(ep0);
@@ -233,8 +280,7 @@ int vbhem_em_lower_bound(const vbhem_post_t *post, const vbhem_em_opt_t *opt,
         std::fill(Wf.begin(), Wf.end(), 0.0);
         for (int a = 0; a < d; ++a) Wf[(size_t)a * d + a] = W[a];
       }
-      double sg = 0.0;
-      for (int q = 1; q <= d; ++q) sg += std::lgamma(0.5 * (v + 1 - q));
+      const double sg = lgamma_sum_half(v, d);
       const double logBk = -(v / 2) * std::log(det_of(Wf.data(), d)) - (v * d / 2) * std::log(2.0) -
                            (d * (d - 1) / 4.0) * std::log(kPi) - sg;
       H += -logBk - 0.5 * (v - d - 1) * lLT + 0.5 * v * d;
@@ -353,21 +399,69 @@ size_t vbhem_em_workspace_bytes(const vbhem_base_t *base, int K, int S, int T) {
   if (fused == 0) return 0;
   const size_t consts = (size_t)K * S * S + (size_t)K * S + (size_t)K * S * d + (size_t)K * S * dd +
                         (size_t)K * S + (size_t)K;
-  return (fused + 255) / 256 * 256 + consts * sizeof(double) + 256;
+  // device-side host math (vbhem_em_dev.hip): two posteriors, logLambdaTilde, m0, W0^-1
+  const size_t postn = (size_t)K + 3 * (size_t)K * S + (size_t)K * S * S + (size_t)K * S * d +
+                       (size_t)K * S * dd;
+  const size_t dev = 2 * postn + (size_t)K * S + (size_t)d + (size_t)d * d;
+  return (fused + 255) / 256 * 256 + (consts + dev) * sizeof(double) + 256;
 }
 
-int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
-                 const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
-                 double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
-                 double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
-                 vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
-  if (!base || !post_ok(post) || !opt_ok(opt, post->d) || !LogLs || !iters || !L_final ||
-      !stable || !stats_dev || post->d != base->d || post->covmode != base->covmode)
-    return VBHEM_ERR_ARG;
+namespace {
+
+// the bound's hyperparameter constants (vbhemh3m_lb.m:74-86), as vbhem_em_lower_bound
+void bound_constants(const vbhem_em_opt_t *opt, int K, int S, int d, const std::vector<double> &W0inv,
+                     double &logCalpha0, double &logCeta0, double &logCepsilon0, double &logB0) {
+  double logdetW0inv = 0.0;
+  if (opt->W0_len == 1) logdetW0inv = d * std::log(W0inv[0]);
+  else for (int a = 0; a < d; ++a) logdetW0inv += std::log(W0inv[(size_t)a * d + a]);
+  const double a0 = opt->alpha0, e0 = opt->eta0, ep0 = opt->epsilon0, v0 = opt->v0;
+  logCalpha0 = std::lgamma(K * a0) - K * std::lgamma(a0);
+  logCeta0 = std::lgamma(S * e0) - S * std::lgamma(e0);
+  logCepsilon0 = std::lgamma(S * ep0) - S * std::lgamma(ep0);
+  logB0 = (v0 / 2) * logdetW0inv - (v0 * d / 2) * std::log(2.0) - (d * (d - 1) / 4.0) * std::log(kPi) -
+          lgamma_sum_half(v0, d);
+}
+
+struct PostDev {
+  double *alpha, *eta, *eps, *lam, *v, *m, *W;
+};
+
+PostDev carve_post(double *&p, int K, int S, int d, size_t dd) {
+  PostDev q;
+  q.alpha = p; p += K;
+  q.eta = p; p += (size_t)K * S;
+  q.eps = p; p += (size_t)K * S * S;
+  q.lam = p; p += (size_t)K * S;
+  q.v = p; p += (size_t)K * S;
+  q.m = p; p += (size_t)K * S * d;
+  q.W = p; p += (size_t)K * S * dd;
+  return q;
+}
+
+hipError_t copy_post(const vbhem_post_t *h, const PostDev &q, size_t dd, hipMemcpyKind kind,
+                     hipStream_t st) {
+  const int K = h->K, S = h->S, d = h->d;
+  double *hp[7] = {h->alpha, h->eta, h->epsilon, h->lam, h->v, h->m, h->W};
+  double *dp[7] = {q.alpha, q.eta, q.eps, q.lam, q.v, q.m, q.W};
+  const size_t n[7] = {(size_t)K, (size_t)K * S, (size_t)K * S * S, (size_t)K * S, (size_t)K * S,
+                       (size_t)K * S * d, (size_t)K * S * dd};
+  for (int x = 0; x < 7; ++x) {
+    hipError_t e = kind == hipMemcpyHostToDevice
+                       ? hipMemcpyAsync(dp[x], hp[x], n[x] * sizeof(double), kind, st)
+                       : hipMemcpyAsync(hp[x], dp[x], n[x] * sizeof(double), kind, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// The EM loop with the per-iteration host math in C++ on the host (shapes outside
+// the device kernels: d > 16 or S > 64).
+int em_run_host(const vbhem_base_t *base, const double *tildeN_dev, int T, const vbhem_em_opt_t *opt,
+                vbhem_post_t *post, double *LogLs, int *iters, double *L_final, int *stable,
+                double *stats_dev, double *hatZ_dev, double *LL_dev, void *workspace_dev,
+                hipStream_t st, vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
   const int K = post->K, S = post->S, d = post->d;
   const size_t dd = post->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
-  const size_t need = vbhem_em_workspace_bytes(base, K, S, T);
-  if (need == 0 || !workspace_dev || workspace_bytes < need) return VBHEM_ERR_WORKSPACE;
   vbhem_cluster_t c0 = {K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
   const size_t fused = (vbhem_fused_workspace_bytes(base, &c0, T) + 255) / 256 * 256;
   // device constants: logA | logPi | m | P | c | logOmega (one upload per iteration)
@@ -380,7 +474,6 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
   const double *dlogOmega = dc + nA + nPi + nm + nP + nc;
   const size_t slen = vbhem_stats_len(K, S, d, post->covmode);
   std::vector<double> stats(slen);
-  hipStream_t st = static_cast<hipStream_t>(stream);
   double lastL = -DBL_MAX, L = -INFINITY;
   int it = 0;
   *stable = 1;
@@ -392,9 +485,9 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     hipError_t e = hipMemcpyAsync(dc, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return VBHEM_ERR_HIP;
     rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hatZ_dev, LL_dev,
-                           workspace_dev, fused, stream);
+                           workspace_dev, fused, st);
     if (rc != VBHEM_OK) return rc;
-    if (allreduce && allreduce(stats_dev, slen, stream, allreduce_ctx) != 0) return VBHEM_ERR_HIP;
+    if (allreduce && allreduce(stats_dev, slen, st, allreduce_ctx) != 0) return VBHEM_ERR_HIP;
     e = hipMemcpyAsync(stats.data(), stats_dev, slen * sizeof(double), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return VBHEM_ERR_HIP;
@@ -415,6 +508,112 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     lastL = L;
     if (do_break) break;
   }
+  *iters = it;
+  *L_final = L;
+  return VBHEM_OK;
+}
+
+}  // namespace
+
+int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
+                 const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
+                 double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
+                 double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
+                 vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
+  if (!base || !post_ok(post) || !opt_ok(opt, post->d) || !LogLs || !iters || !L_final ||
+      !stable || !stats_dev || post->d != base->d || post->covmode != base->covmode)
+    return VBHEM_ERR_ARG;
+  const int K = post->K, S = post->S, d = post->d;
+  const size_t dd = post->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
+  const size_t need = vbhem_em_workspace_bytes(base, K, S, T);
+  if (need == 0 || !workspace_dev || workspace_bytes < need) return VBHEM_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!vbhem::em_dev_supported(d, S) || std::getenv("VBHEM_EM_HOST_MATH"))
+    return em_run_host(base, tildeN_dev, T, opt, post, LogLs, iters, L_final, stable, stats_dev,
+                       hatZ_dev, LL_dev, workspace_dev, st, allreduce, allreduce_ctx);
+  vbhem_cluster_t c0 = {K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const size_t fused = (vbhem_fused_workspace_bytes(base, &c0, T) + 255) / 256 * 256;
+  const size_t nA = (size_t)K * S * S, nPi = (size_t)K * S, nm = (size_t)K * S * d,
+               nP = (size_t)K * S * dd, nc = (size_t)K * S;
+  double *dc = reinterpret_cast<double *>(static_cast<char *>(workspace_dev) + fused);
+  vbhem_cluster_t cl = {K, S, dc, dc + nA, dc + nA + nPi, dc + nA + nPi + nm,
+                        dc + nA + nPi + nm + nP};
+  double *dlogOmega = dc + nA + nPi + nm + nP + nc;
+  double *p = dlogOmega + K;
+  PostDev pd[2];
+  pd[0] = carve_post(p, K, S, d, dd);
+  pd[1] = carve_post(p, K, S, d, dd);
+  double *dlLT = p; p += nc;
+  double *dm0 = p; p += d;
+  double *dW0inv = p;
+  // hyperparameters: W0^-1 and the bound's constants once per run
+  std::vector<double> W0inv;
+  w0_inv(opt, d, W0inv);
+  vbhem::EmDevArgs a{};
+  a.K = K; a.S = S; a.d = d; a.covmode = post->covmode; a.NU = (int)vbhem_stats_nu(d, post->covmode);
+  a.stats = stats_dev;
+  a.alpha0 = opt->alpha0; a.eta0 = opt->eta0; a.epsilon0 = opt->epsilon0; a.lambda0 = opt->lambda0;
+  a.v0 = opt->v0;
+  bound_constants(opt, K, S, d, W0inv, a.logCalpha0, a.logCeta0, a.logCepsilon0, a.logB0);
+  a.m0 = dm0; a.W0inv = dW0inv;
+  a.logA = dc; a.logPi = dc + nA; a.cm = dc + nA + nPi; a.P = dc + nA + nPi + nm;
+  a.c = dc + nA + nPi + nm + nP; a.lLT = dlLT; a.logOmega = dlogOmega;
+  hipError_t e = hipMemcpyAsync(dm0, opt->m0, d * sizeof(double), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(dW0inv, W0inv.data(), W0inv.size() * sizeof(double), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = copy_post(post, pd[0], dd, hipMemcpyHostToDevice, st);
+  // the bound of each iteration goes straight to pinned, mapped host memory
+  double *Lh = nullptr, *Ld = nullptr;
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&Lh), sizeof(double), hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&Ld), Lh, 0);
+  auto set_post = [&a](const PostDev &in, const PostDev &out) {
+    a.alpha = in.alpha; a.eta = in.eta; a.eps = in.eps; a.lam = in.lam; a.v = in.v; a.m = in.m;
+    a.W = in.W;
+    a.alpha_o = out.alpha; a.eta_o = out.eta; a.eps_o = out.eps; a.lam_o = out.lam; a.v_o = out.v;
+    a.m_o = out.m; a.W_o = out.W;
+  };
+  int cur = 0;
+  set_post(pd[0], pd[1]);
+  if (e == hipSuccess) e = vbhem::launch_em_dev(a, vbhem::kEmPrelude, nullptr, st);
+  const size_t slen = vbhem_stats_len(K, S, d, post->covmode);
+  double lastL = -DBL_MAX, L = -INFINITY;
+  int it = 0, rc = VBHEM_OK;
+  *stable = 1;
+  while (e == hipSuccess) {
+    rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hatZ_dev, LL_dev,
+                           workspace_dev, fused, st);
+    if (rc != VBHEM_OK) break;
+    if (allreduce && allreduce(stats_dev, slen, st, allreduce_ctx) != 0) {
+      rc = VBHEM_ERR_HIP;
+      break;
+    }
+    // this iteration's bound (its posterior and prelude), then the M-step into the
+    // other posterior buffer and the next prelude (the next E-step's constants)
+    set_post(pd[cur], pd[1 - cur]);
+    e = vbhem::launch_em_dev(a, vbhem::kEmBound, Ld, st);
+    if (e == hipSuccess) e = vbhem::launch_em_dev(a, vbhem::kEmMstepPrelude, nullptr, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) break;
+    L = *Lh;
+    if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, keep the posterior before the M-step
+      L = -INFINITY;
+      *stable = 0;
+      break;
+    }
+    bool do_break = false;
+    if (it > 1 && std::fabs((L - lastL) / lastL) <= opt->minDiff) do_break = true;
+    if (it == opt->max_iter) do_break = true;
+    LogLs[it] = L;
+    ++it;
+    lastL = L;
+    cur = 1 - cur;  // the M-step's posterior
+    if (do_break) break;
+  }
+  if (e == hipSuccess && rc == VBHEM_OK) e = copy_post(post, pd[cur], dd, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && rc == VBHEM_OK) e = hipStreamSynchronize(st);
+  if (Lh) (void)hipHostFree(Lh);
+  if (rc != VBHEM_OK) return rc;
+  if (e != hipSuccess) return VBHEM_ERR_HIP;
   *iters = it;
   *L_final = L;
   return VBHEM_OK;

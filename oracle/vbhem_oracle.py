@@ -193,6 +193,47 @@ def c_statistics(Z, pairs: dict, covmode: int):
     return out
 
 
+def base_subset(base: dict, idx) -> dict:
+    """The base HMMs ``idx`` (an index array or a slice) of a packed base dict."""
+    N = base["prior"].shape[0]
+    return {k: (np.ascontiguousarray(v[idx]) if isinstance(v, np.ndarray) and v.ndim and
+                v.shape[0] == N else v) for k, v in base.items()}
+
+
+def c_fused(base: dict, consts: dict, T: int, tildeN, logOmega, nthreads: int = 1,
+            chunk: int = 4096):
+    """The fused E-step of one EM iteration on the CPU: per-pair recursions
+    (oracle_estep_pairs), responsibilities (vbhem_h3m_c_step_fc.m:270-283) and
+    the gated statistic sums (vbhem_compute_Statistics.m:33-55), with the ELBO
+    partials Lt1 = sum Z .* L_elbo and Lt7 = sum hat_Z .* log(hat_Z)
+    (vbhemh3m_lb.m:90, 107), over chunks of ``chunk`` bases so the per-pair
+    outputs never exist for all N at once (C4 / C5 at full size).  The sums are
+    additive over bases, so chunking changes only their summation order.
+    Returns dict(LL_elbo [N][K], hat_Z [N][K], Nj, N1, M, Nr, Y, SC, Lt1, Lt7)."""
+    N = base["prior"].shape[0]
+    K = consts["logPi"].shape[0]
+    tN = np.asarray(tildeN, dtype=np.float64)
+    LL = np.zeros((N, K))
+    hz = np.zeros((N, K))
+    acc = None
+    Lt1 = Lt7 = 0.0
+    for i0 in range(0, N, chunk):
+        i1 = min(N, i0 + chunk)
+        b = base_subset(base, slice(i0, i1))
+        pr = c_estep_pairs(b, consts, T, nthreads=nthreads)
+        h, Z = c_responsibilities(pr["LL_elbo"], tN[i0:i1], logOmega)
+        st = c_statistics(Z, pr, base["covmode"])
+        LL[i0:i1] = pr["LL_elbo"]
+        hz[i0:i1] = h
+        Lt1 += float((Z * pr["LL_elbo"]).sum())
+        Lt7 += float((h * np.log(h)).sum())
+        acc = st if acc is None else {k: acc[k] + st[k] for k in acc}
+        del pr
+    out = dict(acc or {})
+    out.update(LL_elbo=LL, hat_Z=hz, Lt1=Lt1, Lt7=Lt7)
+    return out
+
+
 # ----------------------------------------------------------------------------
 # numpy restatement of the MATLAB twin (vbhem_hmm_bwd_fwd_fast.m)
 # ----------------------------------------------------------------------------

@@ -139,3 +139,68 @@ def test_c5_slice_vs_oracle(vb, vo):
     """C5 shapes (K = 32, S = Sb = 12, d = 16 full) on 1,000 bases = 32,000 pairs."""
     hz = _fused_vs_oracle(vb, vo, "C5", N=1000, nthreads=16)
     assert hz.shape == (1000, 32)
+
+
+def test_chunked_oracle_matches_whole(vb, vo):
+    """CPU: the chunked fused oracle (vbhem_oracle.c_fused) equals the unchunked
+    pipeline (pairs -> responsibilities -> statistics) up to summation order."""
+    cs = make_case(23, 3, 3, 3, 2, 1, seed=90, tau=5)
+    base, consts = cs["base"], cs["consts"]
+    tN = 100.0 * 23 * base["omega"]
+    logOm, _, _, _ = vo.responsibilities(np.zeros((23, 3)), tN, cs["post"]["alpha"])
+    whole = vo.c_estep_pairs(base, consts, 5)
+    hz, Z = vo.c_responsibilities(whole["LL_elbo"], tN, logOm)
+    st = vo.c_statistics(Z, whole, 1)
+    ch = vo.c_fused(base, consts, 5, tN, logOm, chunk=4)
+    assert np.array_equal(ch["LL_elbo"], whole["LL_elbo"]) and np.array_equal(ch["hat_Z"], hz)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(ch[k], st[k]) < 1e-13, k
+    assert abs(ch["Lt1"] - float((Z * whole["LL_elbo"]).sum())) < 1e-12 * abs(ch["Lt1"])
+
+
+def _full_size_vs_oracle(vb, vo, name, N=None, chunk=4096, nthreads=16):
+    """The fused device E-step against the chunked oracle on EVERY pair: L_elbo
+    (elementwise 1e-10), hat_Z (1e-5), the statistics (1e-9) and the ELBO
+    partials Lt1 / Lt7."""
+    from vbhem_amd.em import tilde_n
+    from vbhem_amd.estep import EStepEngine
+    base, P, opt = vb.synth_workload(name, N=N)
+    cov = base.covmode
+    consts = vb.host.cluster_constants(P, cov)
+    logOm = vb.host.log_omega_tilde(P.alpha)
+    eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+    eng.set_clusters(consts)
+    eng.set_log_omega(logOm)
+    tN = tilde_n(eng, opt["Nv"], base.N)
+    vec = eng.fused(tN).cpu().numpy()
+    LL, hZ = eng.LL.cpu().numpy(), eng.hatZ.cpu().numpy()
+    assert eng.fallback_count() == 0
+    del eng
+    ref = vo.c_fused(base.numpy(), consts, opt["tau"], tN.cpu().numpy(), logOm,
+                     nthreads=nthreads, chunk=chunk)
+    assert elem_err(LL, ref["LL_elbo"]) < RTOL_PAIRS
+    assert hatz_err(hZ, ref["hat_Z"]) < RTOL_NORTH_STAR
+    got = vb.host.unpack_stats(vec, P.K, P.S, base.d, cov)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], ref[k]) < 1e-9, (name, k, stat_err(got[k], ref[k]))
+    for k in ("Lt1", "Lt7"):
+        assert abs(got[k] - ref[k]) <= 1e-9 * abs(ref[k]), (k, got[k], ref[k])
+    return base.N
+
+
+@pytest.mark.gpu
+def test_c4_full_size_vs_oracle(vb, vo):
+    """C4 at its full size (N = 100,000, K = 16: 1.6 M pairs), every pair, every
+    hat_Z entry and every statistic against the oracle (16 host threads)."""
+    assert _full_size_vs_oracle(vb, vo, "C4", chunk=10_000) == 100_000
+
+
+@pytest.mark.gpu
+def test_c5_multigroup_vs_oracle(vb, vo, monkeypatch):
+    """C5 shapes (K = 32, S = Sb = 12, d = 16 full) on 20,000 bases (640,000 pairs)
+    through the multi-group path of the full-size run: VBHEM_GROUP_BASES = 6,000
+    splits the call into 4 base groups (C5 at N = 10^6 runs as 14 groups of
+    <= 74 k), each with its own emission GEMM, backward pass, gate lists and list
+    statistics accumulated into the same slabs."""
+    monkeypatch.setenv("VBHEM_GROUP_BASES", "6000")
+    assert _full_size_vs_oracle(vb, vo, "C5", N=20_000, chunk=1000) == 20_000
