@@ -399,10 +399,13 @@ size_t vbhem_em_workspace_bytes(const vbhem_base_t *base, int K, int S, int T) {
   if (fused == 0) return 0;
   const size_t consts = (size_t)K * S * S + (size_t)K * S + (size_t)K * S * d + (size_t)K * S * dd +
                         (size_t)K * S + (size_t)K;
-  // device-side host math (vbhem_em_dev.hip): two posteriors, logLambdaTilde, m0, W0^-1
+  // device-side host math (vbhem_em_dev.hip): three posteriors (the loop runs one
+  // iteration ahead), logLambdaTilde, log det W, m0, W0^-1, the bound's partial sums,
+  // its ticket, and a second hat_Z / L_elbo pair
   const size_t postn = (size_t)K + 3 * (size_t)K * S + (size_t)K * S * S + (size_t)K * S * d +
                        (size_t)K * S * dd;
-  const size_t dev = 2 * postn + (size_t)K * S + (size_t)d + (size_t)d * d;
+  const size_t dev = 3 * postn + 2 * (size_t)K * S + (size_t)d + (size_t)d * d +
+                     (size_t)K * S * 13 + 1 + 2 * (size_t)base->N * K;
   return (fused + 255) / 256 * 256 + (consts + dev) * sizeof(double) + 256;
 }
 
@@ -420,6 +423,20 @@ void bound_constants(const vbhem_em_opt_t *opt, int K, int S, int d, const std::
   logCepsilon0 = std::lgamma(S * ep0) - S * std::lgamma(ep0);
   logB0 = (v0 / 2) * logdetW0inv - (v0 * d / 2) * std::log(2.0) - (d * (d - 1) / 4.0) * std::log(kPi) -
           lgamma_sum_half(v0, d);
+}
+
+// spin on the sequence word the bound kernel writes to mapped host memory; the
+// stream is queried now and then so a failed launch ends the wait with its error
+hipError_t wait_flag(const int *flag, int seq, hipStream_t st) {
+  for (long n = 0;; ++n) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+    if ((n & 1023) == 1023) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q != hipSuccess && q != hipErrorNotReady) return q;
+      if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? hipSuccess
+                                                                                 : hipErrorUnknown;
+    }
+  }
 }
 
 struct PostDev {
@@ -540,12 +557,17 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
                         dc + nA + nPi + nm + nP};
   double *dlogOmega = dc + nA + nPi + nm + nP + nc;
   double *p = dlogOmega + K;
-  PostDev pd[2];
-  pd[0] = carve_post(p, K, S, d, dd);
-  pd[1] = carve_post(p, K, S, d, dd);
+  PostDev pd[3];
+  for (int x = 0; x < 3; ++x) pd[x] = carve_post(p, K, S, d, dd);
   double *dlLT = p; p += nc;
+  double *dlogdetW = p; p += nc;
   double *dm0 = p; p += d;
-  double *dW0inv = p;
+  double *dW0inv = p; p += (size_t)d * d;
+  double *dpart = p; p += (size_t)K * S * 13;
+  int *dticket = reinterpret_cast<int *>(p); p += 1;
+  // E-step j writes hat_Z / L_elbo into pair j % 2 (the caller's arrays are pair 0):
+  // the speculative E-step of the next iteration keeps this one's
+  double *hz[2] = {hatZ_dev, p}, *ll[2] = {LL_dev, p + (size_t)base->N * K};
   // hyperparameters: W0^-1 and the bound's constants once per run
   std::vector<double> W0inv;
   w0_inv(opt, d, W0inv);
@@ -557,47 +579,64 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
   bound_constants(opt, K, S, d, W0inv, a.logCalpha0, a.logCeta0, a.logCepsilon0, a.logB0);
   a.m0 = dm0; a.W0inv = dW0inv;
   a.logA = dc; a.logPi = dc + nA; a.cm = dc + nA + nPi; a.P = dc + nA + nPi + nm;
-  a.c = dc + nA + nPi + nm + nP; a.lLT = dlLT; a.logOmega = dlogOmega;
+  a.c = dc + nA + nPi + nm + nP; a.lLT = dlLT; a.logOmega = dlogOmega; a.logdetW = dlogdetW;
+  a.part = dpart; a.ticket = dticket;
   hipError_t e = hipMemcpyAsync(dm0, opt->m0, d * sizeof(double), hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(dW0inv, W0inv.data(), W0inv.size() * sizeof(double), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = copy_post(post, pd[0], dd, hipMemcpyHostToDevice, st);
-  // the bound of each iteration goes straight to pinned, mapped host memory
+  if (e == hipSuccess) e = hipMemsetAsync(dticket, 0, sizeof(int), st);
+  // the bound of iteration j goes straight to pinned, mapped host memory (slot j % 2),
+  // followed by a sequence word the host polls: no stream synchronisation per
+  // iteration, and the next E-step is already queued behind the bound
   double *Lh = nullptr, *Ld = nullptr;
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&Lh), sizeof(double), hipHostMallocMapped);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void **>(&Lh), 4 * sizeof(double), hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&Ld), Lh, 0);
+  int *flag_h = Lh ? reinterpret_cast<int *>(Lh + 2) : nullptr;  // two ints after L[2]
+  if (flag_h) flag_h[0] = flag_h[1] = 0;
   auto set_post = [&a](const PostDev &in, const PostDev &out) {
     a.alpha = in.alpha; a.eta = in.eta; a.eps = in.eps; a.lam = in.lam; a.v = in.v; a.m = in.m;
     a.W = in.W;
     a.alpha_o = out.alpha; a.eta_o = out.eta; a.eps_o = out.eps; a.lam_o = out.lam; a.v_o = out.v;
     a.m_o = out.m; a.W_o = out.W;
   };
-  int cur = 0;
   set_post(pd[0], pd[1]);
   if (e == hipSuccess) e = vbhem::launch_em_dev(a, vbhem::kEmPrelude, nullptr, st);
   const size_t slen = vbhem_stats_len(K, S, d, post->covmode);
-  double lastL = -DBL_MAX, L = -INFINITY;
-  int it = 0, rc = VBHEM_OK;
-  *stable = 1;
-  while (e == hipSuccess) {
-    rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hatZ_dev, LL_dev,
+  int rc = VBHEM_OK;
+  // iteration j: E-step (constants of posterior j % 3) -> all-reduce -> bound of
+  // posterior j % 3 + M-step into (j + 1) % 3 + prelude (the constants of E-step j + 1)
+  auto enqueue = [&](int j) -> bool {
+    rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hz[j % 2], ll[j % 2],
                            workspace_dev, fused, st);
-    if (rc != VBHEM_OK) break;
+    if (rc != VBHEM_OK) return false;
     if (allreduce && allreduce(stats_dev, slen, st, allreduce_ctx) != 0) {
       rc = VBHEM_ERR_HIP;
-      break;
+      return false;
     }
-    // this iteration's bound (its posterior and prelude), then the M-step into the
-    // other posterior buffer and the next prelude (the next E-step's constants)
-    set_post(pd[cur], pd[1 - cur]);
-    e = vbhem::launch_em_dev(a, vbhem::kEmBound, Ld, st);
-    if (e == hipSuccess) e = vbhem::launch_em_dev(a, vbhem::kEmMstepPrelude, nullptr, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    set_post(pd[j % 3], pd[(j + 1) % 3]);
+    a.seq = j + 1;
+    a.flag = reinterpret_cast<int *>(Ld + 2) + (j % 2);
+    e = vbhem::launch_em_dev(a, vbhem::kEmIterate, Ld + (j % 2), st);
+    return e == hipSuccess;
+  };
+  double lastL = -DBL_MAX, L = -INFINITY;
+  int it = 0, fin_post = 0, fin_e = 0;
+  *stable = 1;
+  bool ok = e == hipSuccess && enqueue(0);
+  while (ok) {
+    // the next iteration is queued before this one's bound is read (it is discarded
+    // when this one ends the loop; never past max_iter)
+    if (it + 1 <= opt->max_iter && !enqueue(it + 1)) break;
+    e = wait_flag(flag_h + (it % 2), it + 1, st);
     if (e != hipSuccess) break;
-    L = *Lh;
-    if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, keep the posterior before the M-step
+    L = Lh[it % 2];
+    fin_e = it % 2;
+    if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, the posterior before the M-step
       L = -INFINITY;
       *stable = 0;
+      fin_post = it % 3;
       break;
     }
     bool do_break = false;
@@ -606,10 +645,19 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     LogLs[it] = L;
     ++it;
     lastL = L;
-    cur = 1 - cur;  // the M-step's posterior
+    fin_post = it % 3;  // the M-step's posterior
     if (do_break) break;
   }
-  if (e == hipSuccess && rc == VBHEM_OK) e = copy_post(post, pd[cur], dd, hipMemcpyDeviceToHost, st);
+  hipError_t e2 = hipStreamSynchronize(st);  // the discarded speculative iteration drains
+  if (e == hipSuccess) e = e2;
+  if (e == hipSuccess && rc == VBHEM_OK && fin_e == 1 && base->N > 0) {
+    e = hipMemcpyAsync(hatZ_dev, hz[1], (size_t)base->N * K * sizeof(double),
+                       hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(LL_dev, ll[1], (size_t)base->N * K * sizeof(double),
+                         hipMemcpyDeviceToDevice, st);
+  }
+  if (e == hipSuccess && rc == VBHEM_OK) e = copy_post(post, pd[fin_post], dd, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && rc == VBHEM_OK) e = hipStreamSynchronize(st);
   if (Lh) (void)hipHostFree(Lh);
   if (rc != VBHEM_OK) return rc;

@@ -3,23 +3,26 @@
 // vbhem_h3m_c_step_fc.m runs, between two E-steps, the lower bound (vbhemh3m_lb.m:
 // 64-186), the M-step (vbhem_compute_Statistics.m:57-82, vbhem_mstep_component.m:
 // 42-70, :396) and the next iteration's psi prelude (:118-165, 180-191, 271-273).
-// vbhem_em.hip has them in C++ on the host; here the same arithmetic runs as two
-// small kernels on the E-step's stream, so an EM iteration never leaves the GPU:
-// the packed statistics are read where the statistics kernel (and the all-reduce)
-// left them, and the prelude writes the next E-step's cluster constants in place.
-// Only the bound (one double) goes to the host, for the convergence test.
+// vbhem_em.hip has them in C++ on the host; here the same arithmetic is ONE kernel on
+// the E-step's stream, so an EM iteration never leaves the GPU: the packed
+// statistics are read where the statistics kernel (and the all-reduce) left them,
+// the prelude writes the next E-step's cluster constants in place, and only the
+// bound (one double) goes to the host, for the convergence test.
 //
-//   em_step_kernel<DP>   one block per cluster k, one thread per state s:
-//                        [M-step of (k, s)] + prelude of (k, s) (logLambdaTilde, c,
-//                        P = v W, m, the logATilde row), logPiTilde and logOmega
-//   em_bound_kernel<DP>  one block: every (k, s) term of the bound, reduced in a
-//                        fixed order (deterministic), written to host memory
-//
-// d x d determinants and inverses use LU with partial pivoting (as MATLAB's
-// det / inv and vbhem_em.hip) on register arrays padded to DP in {2, 4, 8, 16} with
-// an identity block (exact: the padding neither changes the determinant nor the
-// inverse of the leading block, and never wins a pivot search).  psi is the host
-// routine's recurrence + asymptotic series; lgamma is the device libm's.
+// em_iter_kernel: one WAVEFRONT per cluster state (k, s).  Each does, with its
+// lanes working in parallel:
+//   1. the (k, s) terms of the bound for the current posterior (lgammas over the
+//      lanes, the quadratic forms over lanes = matrix entries), written as partial
+//      sums; the last wave to finish (a ticket counter) reduces all of them in a
+//      fixed order and writes L (deterministic);
+//   2. the M-step of (k, s) into the other posterior buffer: the d x d inverse of
+//      W0^-1 + Nr SC + mult1 dd' by Gauss-Jordan elimination with partial pivoting
+//      in wave-private LDS, lanes = entries of [A | I];
+//   3. the prelude of the new (k, s): logLambdaTilde (psi over the lanes, det W by
+//      the same elimination), c, P = v W, m, its logATilde row, logPiTilde and (one
+//      wave per cluster) logOmega -- the sums over a cluster's states or over all
+//      clusters are recomputed by every wave that needs them, in one fixed order.
+// A prelude-only launch (no bound, no M-step) starts the loop.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -32,148 +35,127 @@ namespace {
 
 constexpr double kPiD = 3.14159265358979323846;
 constexpr double kLn2D = 0.69314718055994530942;
+constexpr int kWaves = 4;  // waves (cluster states) per block
 
+// digamma for x > 0 (the host routine's series): psi(x) = psi(x + n) -
+// sum_{i<n} 1/(x + i) with x + n >= 8, the sum as ONE division of a running
+// numerator / denominator (fp64 division is a long dependent sequence on the GPU),
+// then ln z - 1/(2z) - sum B_2k / (2k z^2k)
 __device__ double psi_dev(double x) {
-  double acc = 0.0;
-  while (x < 8.0) {
-    acc -= 1.0 / x;
+  double num = 0.0, den = 1.0;
+  while (x < 8.0) {  // num / den = sum 1/(x_i) so far
+    num = fma(num, x, den);
+    den *= x;
     x += 1.0;
   }
   const double r = 1.0 / x, r2 = r * r;
   const double series =
       r2 * (1.0 / 12 - r2 * (1.0 / 120 - r2 * (1.0 / 252 - r2 * (1.0 / 240 - r2 * (1.0 / 132 -
       r2 * (691.0 / 32760 - r2 * (1.0 / 12)))))));
-  return acc + log(x) - 0.5 * r - series;
+  return log(x) - 0.5 * r - series - num / den;
 }
 
-// sum_{q=1..d} psi((v + 1 - q) / 2): two chains, psi(x - 1) = psi(x) - 1/(x - 1)
-__device__ double psi_sum_half_dev(double v, int d) {
-  double acc = 0.0;
-  for (int c = 0; c < 2 && c < d; ++c) {
-    double x = 0.5 * (v - c), p = psi_dev(x);
-    for (int q = c; q < d; q += 2) {
-      acc += p;
-      x -= 1.0;
-      p -= 1.0 / x;
-    }
+// log Gamma for x > 0: lgamma(x) = lgamma(x + n) - log(prod_{i<n} (x + i)) with
+// z = x + n >= 10, then Stirling's series (z - 1/2) ln z - z + ln(2 pi)/2 +
+// sum B_2k / (2k (2k - 1) z^(2k-1)) through z^-15 (next term < 3e-18 at z = 10)
+__device__ double lgamma_dev(double x) {
+  double prod = 1.0;
+  while (x < 10.0) {
+    prod *= x;
+    x += 1.0;
   }
-  return acc;
+  const double r = 1.0 / x, r2 = r * r;
+  const double series =
+      r * (1.0 / 12 - r2 * (1.0 / 360 - r2 * (1.0 / 1260 - r2 * (1.0 / 1680 - r2 * (1.0 / 1188 -
+      r2 * (691.0 / 360360 - r2 * (1.0 / 156 - r2 * (3617.0 / 122400))))))));
+  return (x - 0.5) * log(x) - x + 0.91893853320467274178 + series - log(prod);
 }
 
-// sum_{q=1..d} lgamma((v + 1 - q) / 2): two chains, lgamma(x - 1) = lgamma(x) - log(x - 1)
-__device__ double lgamma_sum_half_dev(double v, int d) {
-  double acc = 0.0;
-  for (int c = 0; c < 2 && c < d; ++c) {
-    double x = 0.5 * (v - c), g = lgamma(x);
-    for (int q = c; q < d; q += 2) {
-      acc += g;
-      x -= 1.0;
-      if (q + 2 < d) g -= log(x);
-    }
-  }
-  return acc;
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// LU with partial pivoting in registers (compile-time indices, row swaps as
-// selects); returns det.  a is overwritten by the factors, perm[k] = pivot row.
-template <int DP>
-__device__ __forceinline__ double lu_reg(double (&a)[DP][DP], int (&perm)[DP]) {
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+
+// fixed-order wavefront sum by DPP (row_shr 1, 2, 4, 8, row_bcast15, row_bcast31:
+// the total lands in lane 63), broadcast to every lane; every wave summing the same
+// 64 values gets the same result
+__device__ __forceinline__ double wsum(double v) {
+  v += dpp_d<0x111, 0xf>(v);
+  v += dpp_d<0x112, 0xf>(v);
+  v += dpp_d<0x114, 0xf>(v);
+  v += dpp_d<0x118, 0xf>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
+}
+
+// Gauss-Jordan elimination with partial pivoting of the d x d matrix in g[0 .. d)
+// x [0 .. 2d) (row stride 2d, wave-private LDS), the right half holding I on entry:
+// on exit the right half holds the inverse.  Returns det (every lane).  Lanes own
+// the entries x = lane + 64 j of the d x 2d array.
+__device__ double gauss_jordan(double *g, int d, int lane) {
+  const int w2 = 2 * d, n = d * w2;
   double det = 1.0;
-#pragma unroll
-  for (int k = 0; k < DP; ++k) {
+  for (int k = 0; k < d; ++k) {
+    // pivot: the first row r >= k with the largest |g[r][k]| (every lane scans the
+    // column: broadcast LDS reads, no cross-lane exchange)
     int p = k;
-    double best = fabs(a[k][k]);
-#pragma unroll
-    for (int r = k + 1; r < DP; ++r)
-      if (fabs(a[r][k]) > best) {
-        best = fabs(a[r][k]);
+    double best = fabs(g[k * w2 + k]);
+    for (int r = k + 1; r < d; ++r) {
+      const double t = fabs(g[r * w2 + k]);
+      if (t > best) {
+        best = t;
         p = r;
       }
-    perm[k] = p;
-    if (p != k) det = -det;
+    }
+    const double piv = g[p * w2 + k];
+    det *= (p != k) ? -piv : piv;
+    // new row r of the array: rows k and p swapped, row k divided by the pivot,
+    // every other row minus its column-k multiple of the new row k
+    double nv[8];  // n / 64 <= 8 entries per lane (d <= 16)
 #pragma unroll
-    for (int r = k + 1; r < DP; ++r) {
-      const bool sw = r == p;
-#pragma unroll
-      for (int c = 0; c < DP; ++c) {
-        const double t = a[k][c];
-        a[k][c] = sw ? a[r][c] : t;
-        a[r][c] = sw ? t : a[r][c];
+    for (int j = 0; j < 8; ++j) {
+      const int x = lane + 64 * j;
+      if (x < n) {
+        const int r = x / w2, c = x - r * w2;
+        const double rk = g[p * w2 + c] / piv;                   // new row k
+        if (r == k) {
+          nv[j] = rk;
+        } else {
+          const int src = (r == p) ? k : r;
+          nv[j] = g[src * w2 + c] - g[src * w2 + k] * rk;
+        }
       }
     }
-    const double pk = a[k][k];
-    det *= pk;
-    if (pk != 0.0) {
+    wsync();
 #pragma unroll
-      for (int r = k + 1; r < DP; ++r) {
-        const double f = a[r][k] / pk;
-        a[r][k] = f;
-#pragma unroll
-        for (int c = k + 1; c < DP; ++c) a[r][c] -= f * a[k][c];
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int x = lane + 64 * j;
+      if (x < n) g[x] = nv[j];
     }
+    wsync();
   }
   return det;
-}
-
-// d x d (row-major, stride d) -> DP x DP registers, identity padding
-template <int DP>
-__device__ __forceinline__ void load_pad(double (&a)[DP][DP], const double *m, int d) {
-#pragma unroll
-  for (int r = 0; r < DP; ++r)
-#pragma unroll
-    for (int c = 0; c < DP; ++c)
-      a[r][c] = (r < d && c < d) ? m[r * d + c] : (r == c ? 1.0 : 0.0);
-}
-
-template <int DP>
-__device__ double det_pad(const double *m, int d) {
-  double a[DP][DP];
-  int perm[DP];
-  load_pad<DP>(a, m, d);
-  return lu_reg<DP>(a, perm);
-}
-
-// inverse of the padded matrix in registers (a overwritten), columns solved in turn
-template <int DP>
-__device__ __forceinline__ void inv_reg(double (&a)[DP][DP], double (&out)[DP][DP]) {
-  int perm[DP];
-  lu_reg<DP>(a, perm);
-#pragma unroll
-  for (int col = 0; col < DP; ++col) {
-    double x[DP];
-#pragma unroll
-    for (int r = 0; r < DP; ++r) x[r] = r == col ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < DP; ++k) {
-#pragma unroll
-      for (int r = k + 1; r < DP; ++r) {
-        const bool sw = r == perm[k];
-        const double t = x[k];
-        x[k] = sw ? x[r] : t;
-        x[r] = sw ? t : x[r];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < DP; ++r)
-#pragma unroll
-      for (int c = 0; c < r; ++c) x[r] -= a[r][c] * x[c];
-#pragma unroll
-    for (int r = DP - 1; r >= 0; --r) {
-#pragma unroll
-      for (int c = r + 1; c < DP; ++c) x[r] -= a[r][c] * x[c];
-      x[r] /= a[r][r];
-    }
-#pragma unroll
-    for (int r = 0; r < DP; ++r) out[r][col] = x[r];
-  }
 }
 
 // packed statistics (include/vbhem_estep.h): Nj | N1 | M | Lt1 Lt7 | U
 struct StatsView {
   const double *Nj, *N1, *M, *U;
   double Lt1, Lt7;
-  __device__ StatsView(const double *v, int K, int S, int NU) {
+  __device__ StatsView(const double *v, int K, int S) {
+    Nj = N1 = M = U = nullptr;
+    Lt1 = Lt7 = 0.0;
+    if (!v) return;
     size_t o = 0;
     Nj = v + o; o += K;
     N1 = v + o; o += (size_t)K * S;
@@ -182,257 +164,275 @@ struct StatsView {
     Lt7 = v[o + 1];
     o += 2;
     U = v + o;
-    (void)NU;
   }
 };
 
-constexpr int kStepThreads = 64;   // >= S (S <= 64 on this path)
-constexpr int kBoundThreads = 256;
+// bound partial sums per (k, s), stored quantity-major [13][K S]: 0 Lt51, 1 lLT, 2 v trW, 3 lt10a, 4 H, 5 Lt9, 6 logPi,
+// 7 sum logA row, 8 Lt2, 9 logOmega, 10 Lt8b, 11 lgamma(alpha), 12 alpha
+constexpr int kNQ = 13;
 
-template <int DP>
-__global__ __launch_bounds__(kStepThreads) void em_step_kernel(const EmDevArgs a, int do_mstep) {
-  __shared__ double red[kStepThreads];
-  const int k = blockIdx.x, s = threadIdx.x;
+__global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a, int mode,
+                                                              double *L_out) {
+  __shared__ double glds[kWaves][2 * kEmDevMaxD * kEmDevMaxD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int K = a.K, S = a.S, d = a.d;
+  const int ks = blockIdx.x * kWaves + wave;
+  if (ks >= K * S) return;
+  const int k = ks / S, s = ks - k * S;
   const bool full = a.covmode == 1;
   const int dd = full ? d * d : d;
-  const size_t ks = (size_t)k * S + s;
-  const bool on = s < S;
-  double eta_ks = 0.0, alpha_k = 0.0;
-  double sumA = 0.0;  // sum_k alpha (thread 0)
-  if (do_mstep) {
-    const StatsView st(a.stats, K, S, a.NU);
-    if (on) {
-      // vbhem_compute_Statistics.m:57-82
-      const double *u = st.U + ks * a.NU;
-      const double Nr = u[0] + 1e-50;
-      double y[DP], SC[DP][DP];
-#pragma unroll
-      for (int x = 0; x < DP; ++x) y[x] = x < d ? u[1 + x] / Nr : 0.0;
-#pragma unroll
-      for (int x = 0; x < DP; ++x)
-#pragma unroll
-        for (int z = 0; z < DP; ++z) SC[x][z] = 0.0;
-      if (full) {
-        // packed upper triangle: entry (x, z), x <= z, at 1 + d + x d - x (x - 1) / 2 + (z - x)
-#pragma unroll
-        for (int x = 0; x < DP; ++x)
-#pragma unroll
-          for (int z = 0; z < DP; ++z)
-            if (x < d && z >= x && z < d) {
-              const double ue = u[1 + d + x * d - x * (x - 1) / 2 + (z - x)] / Nr;
-              SC[x][z] = ue - y[x] * y[z];
-              SC[z][x] = ue - y[z] * y[x];
-            }
-      } else {
-#pragma unroll
-        for (int x = 0; x < DP; ++x)
-          if (x < d) SC[x][x] = u[1 + d + x] / Nr - y[x] * y[x];
+  double *g = glds[wave];
+  const bool iterate = mode == kEmIterate;
+  const StatsView st(iterate ? a.stats : nullptr, K, S);
+
+  // ---- 1. bound terms of the current posterior (vbhemh3m_lb.m:64-186) ----
+  if (iterate) {
+    const double v = a.v[ks], lam = a.lam[ks], lLT = a.lLT[ks], l0 = a.lambda0;
+    const double *W = a.W + (size_t)ks * dd, *mk = a.m + (size_t)ks * d;
+    // lanes q < d: lgamma((v + 1 - q) / 2); lanes 32 + s2: the epsilon row
+    double t_sg = 0.0, t_lge = 0.0, t_eps = 0.0, t_ept = 0.0, t_la = 0.0;
+    if (lane < d) t_sg = lgamma_dev(0.5 * (v - lane));
+    if (lane >= 32 && lane - 32 < S) {
+      const int s2 = lane - 32;
+      const double e = a.eps[(size_t)ks * S + s2], la = a.logA[(size_t)ks * S + s2];
+      t_lge = lgamma_dev(e);
+      t_eps = e;
+      t_ept = (e - 1) * la;
+      t_la = la;
+    }
+    // quadratic forms over the lanes = entries (x, z)
+    double t_mwm = 0.0, t_tr = 0.0;
+    for (int x = lane; x < d * d; x += 64) {
+      const int r = x / d, c = x - r * d;
+      const double wrc = full ? W[x] : (r == c ? W[r] : 0.0);
+      const double wcr = full ? W[c * d + r] : wrc;
+      t_mwm += (mk[r] - a.m0[r]) * wrc * (mk[c] - a.m0[c]);
+      t_tr += a.W0inv[x] * wcr;
+    }
+    const double sg = wsum(t_sg), lgp = wsum(t_lge), ps = wsum(t_eps), pt = wsum(t_ept);
+    const double sla = wsum(t_la), mWm = wsum(t_mwm), trW = wsum(t_tr);
+    const double e = a.eta[ks];
+    double es = 0.0, lo = 0.0, al = 0.0;
+    if (s == 0) {
+      es = wsum(lane < S ? a.eta[(size_t)k * S + lane] : 0.0);
+      lo = a.logOmega[k];
+      al = a.alpha[k];
+    }
+    // the remaining lgammas in one parallel round: lane 0 sum(eps row), 1 eta,
+    // 2 sum(eta) (state 0), 3 alpha_k (state 0)
+    const double xg = lane == 0 ? ps : lane == 1 ? e : lane == 2 ? es : al;
+    const double lgx = (lane < 2 || (s == 0 && lane < 4)) ? lgamma_dev(xg) : 0.0;
+    const double lg_ps = __shfl(lgx, 0, 64), lg_e = __shfl(lgx, 1, 64);
+    const double lg_es = __shfl(lgx, 2, 64), lg_al = __shfl(lgx, 3, 64);
+    if (lane < kNQ) {
+      const double logBk = -(v / 2) * a.logdetW[ks] - (v * d / 2) * kLn2D -
+                           (d * (d - 1) / 4.0) * log(kPiD) - sg;
+      double q = 0.0;
+      switch (lane) {
+        case 0: q = d * log(l0 / (2 * kPiD)) + lLT - d * l0 / lam - l0 * v * mWm; break;
+        case 1: q = lLT; break;
+        case 2: q = v * trW; break;
+        case 3: q = lLT + d * log(lam / (2 * kPiD)); break;
+        case 4: q = -logBk - 0.5 * (v - d - 1) * lLT + 0.5 * v * d; break;
+        case 5: q = lg_ps - lgp + pt - lg_e + (e - 1) * a.logPi[ks] + (s == 0 ? lg_es : 0.0); break;
+        case 6: q = a.logPi[ks]; break;
+        case 7: q = sla; break;
+        case 8: q = s == 0 ? (st.Nj[k] + 1e-50) * lo : 0.0; break;
+        case 9: q = s == 0 ? lo : 0.0; break;
+        case 10: q = s == 0 ? (al - 1) * lo : 0.0; break;
+        case 11: q = s == 0 ? lg_al : 0.0; break;
+        default: q = s == 0 ? al : 0.0; break;
       }
-      // vbhem_mstep_component.m:42-70
-      const double l0 = a.lambda0;
-      const double lam = l0 + Nr, v = a.v0 + Nr + 1.0, mult1 = l0 * Nr / (l0 + Nr);
+      a.part[(size_t)lane * K * S + ks] = q;  // quantity-major: one lane sums each below
+    }
+  }
+
+  // ---- 2. M-step of (k, s) (vbhem_compute_Statistics.m:57-82, mstep_component.m:42-70) ----
+  // Every lane keeps what it needs of the new posterior in registers or in its own
+  // LDS entries (no lane reads another lane's global stores): v, lam in all lanes,
+  // m_a in lane a, the epsilon row entry s2 in lanes s2 and 32 + s2, W in the left
+  // half of g (then [W | I] for its determinant).
+  const int w2 = 2 * d;
+  double v, lam, m_l = 0.0, e_l = 0.0, eta_ks, sum_eta = 0.0, alpha_k;
+  if (iterate) {
+    const double *u = st.U + (size_t)ks * a.NU;
+    const double Nr = u[0] + 1e-50, l0 = a.lambda0;
+    lam = l0 + Nr;
+    v = a.v0 + Nr + 1.0;
+    const double mult1 = l0 * Nr / (l0 + Nr);
+    // [Mt | I]: Mt = W0^-1 + Nr SC + mult1 (y - m0)(y - m0)', SC = S_plus_C / Nr - y y'
+    for (int x = lane; x < d * w2; x += 64) {
+      const int r = x / w2, c = x - r * w2;
+      double val;
+      if (c < d) {
+        const double yr = u[1 + r] / Nr, yc = u[1 + c] / Nr;
+        double sc;
+        if (full) {
+          const int lo = r < c ? r : c, hi = r < c ? c : r;
+          sc = u[1 + d + lo * d - lo * (lo - 1) / 2 + (hi - lo)] / Nr - yr * yc;
+        } else {
+          sc = r == c ? u[1 + d + r] / Nr - yr * yr : 0.0;
+        }
+        val = a.W0inv[r * d + c] + Nr * sc + mult1 * (yr - a.m0[r]) * (yc - a.m0[c]);
+      } else {
+        val = (c - d == r) ? 1.0 : 0.0;
+      }
+      g[x] = val;
+    }
+    if (lane < d) {
+      m_l = (l0 * a.m0[lane] + Nr * (u[1 + lane] / Nr)) / (l0 + Nr);
+      a.m_o[(size_t)ks * d + lane] = m_l;
+    }
+    if (lane == 0) {
       a.lam_o[ks] = lam;
       a.v_o[ks] = v;
-      double Mt[DP][DP], tW[DP][DP];
+    }
+    wsync();
+    gauss_jordan(g, d, lane);
+    // W = (tW + tW') / 2, left half of g; right half back to I
+    double nw[4];
 #pragma unroll
-      for (int x = 0; x < DP; ++x) {
-        if (x < d) a.m_o[ks * d + x] = (l0 * a.m0[x] + Nr * y[x]) / (l0 + Nr);
-#pragma unroll
-        for (int z = 0; z < DP; ++z)
-          Mt[x][z] = (x < d && z < d)
-                         ? a.W0inv[x * d + z] + Nr * SC[x][z] +
-                               mult1 * (y[x] - a.m0[x]) * (y[z] - a.m0[z])
-                         : (x == z ? 1.0 : 0.0);
+    for (int j = 0; j < 4; ++j) {
+      const int x = lane + 64 * j;
+      if (x < d * d) {
+        const int r = x / d, c = x - r * d;
+        nw[j] = (g[r * w2 + d + c] + g[c * w2 + d + r]) / 2;
       }
-      inv_reg<DP>(Mt, tW);
-      double *W = a.W_o + ks * dd;
+    }
+    wsync();
+    double *Wo = a.W_o + (size_t)ks * dd;
 #pragma unroll
-      for (int x = 0; x < DP; ++x) {
-        if (full) {
+    for (int j = 0; j < 4; ++j) {
+      const int x = lane + 64 * j;
+      if (x < d * d) {
+        const int r = x / d, c = x - r * d;
+        g[r * w2 + c] = full ? nw[j] : (r == c ? nw[j] : 0.0);
+        g[r * w2 + d + c] = r == c ? 1.0 : 0.0;
+        if (full) Wo[x] = nw[j];
+        else if (r == c) Wo[r] = nw[j];
+      }
+    }
+    eta_ks = a.eta0 + st.N1[ks];
+    if (lane < S) sum_eta = a.eta0 + st.N1[(size_t)k * S + lane];
+    const int s2 = lane & 31;
+    if (s2 < S) {
+      e_l = a.epsilon0 + (S > 1 ? st.M[(size_t)ks * S + s2] : 1e-12);
+      if (lane < 32) a.eps_o[(size_t)ks * S + s2] = e_l;
+    }
+    if (lane == 0) a.eta_o[ks] = eta_ks;
+    alpha_k = a.alpha0 + (st.Nj[k] + 1e-50);
+    if (s == 0 && lane == 0) a.alpha_o[k] = alpha_k;
+  } else {
+    v = a.v[ks];
+    lam = a.lam[ks];
+    eta_ks = a.eta[ks];
+    if (lane < S) sum_eta = a.eta[(size_t)k * S + lane];
+    if (lane < d) m_l = a.m[(size_t)ks * d + lane];
+    if ((lane & 31) < S) e_l = a.eps[(size_t)ks * S + (lane & 31)];
+    alpha_k = a.alpha[k];
+    const double *W = a.W + (size_t)ks * dd;
+    for (int x = lane; x < d * w2; x += 64) {
+      const int r = x / w2, c = x - r * w2;
+      g[x] = c < d ? (full ? W[r * d + c] : (r == c ? W[r] : 0.0)) : ((c - d == r) ? 1.0 : 0.0);
+    }
+  }
+  wsync();
+  sum_eta = wsum(lane < S ? sum_eta : 0.0);  // the cluster's eta (lanes < S hold them)
+
+  // ---- 3. prelude of (k, s) (step_fc.m:118-165, 180-191, 271-273) ----
+  double t_psi = 0.0;
+  if (lane < d) t_psi = psi_dev(0.5 * (v - lane));
+  const double t1 = wsum(t_psi);
+  const double es = wsum(lane >= 32 && lane - 32 < S ? e_l : 0.0);
+  // P = v W and the diagonal's logs from g's left half, before the elimination
+  for (int x = lane; x < dd; x += 64) {
+    const int r = full ? x / d : x, c = full ? x - r * d : x;
+    a.P[(size_t)ks * dd + x] = v * g[r * w2 + c];
+  }
+  double logdet;
+  if (full) {
+    wsync();
+    logdet = log(gauss_jordan(g, d, lane));
+  } else {
+    logdet = wsum(lane < d ? log(g[lane * w2 + lane]) : 0.0);
+  }
+  const double lLT = t1 + d * kLn2D + logdet;
+  if (lane < d) a.cm[(size_t)ks * d + lane] = m_l;
+  // psi of the epsilon row (lanes 32 + s2), of its sum (lane 0), of eta (lane 1) and
+  // of the cluster's eta sum (lane 2)
+  double pl = 0.0;
+  if (lane >= 32 && lane - 32 < S) pl = psi_dev(e_l);
+  else if (lane == 0) pl = psi_dev(es);
+  else if (lane == 1) pl = psi_dev(eta_ks);
+  else if (lane == 2) pl = psi_dev(sum_eta);
+  const double pes = __shfl(pl, 0, 64), pet = __shfl(pl, 1, 64), pst = __shfl(pl, 2, 64);
+  if (lane >= 32 && lane - 32 < S) a.logA[(size_t)ks * S + (lane - 32)] = pl - pes;
+  if (lane == 0) {
+    a.lLT[ks] = lLT;
+    a.logdetW[ks] = logdet;
+    a.c[ks] = -lLT + d / lam;
+    a.logPi[ks] = pet - pst;
+  }
+  if (s == 0) {
+    // logOmega[k] = psi(alpha_k) - psi(sum alpha): the sum as lane-strided partials
+    // added in lane order (the same arithmetic in every wave)
+    double t = 0.0;
+    for (int j = lane; j < K; j += 64)
+      t += iterate ? a.alpha0 + (st.Nj[j] + 1e-50) : a.alpha[j];
+    const double sa = wsum(t);
+    if (lane == 0) a.logOmega[k] = psi_dev(alpha_k) - psi_dev(sa);
+  }
+
+  // ---- the bound: the last wave reduces every (k, s)'s partial sums ----
+  if (iterate) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    int last = 0;
+    if (lane == 0) last = atomicAdd(a.ticket, 1) == K * S - 1;
+    last = __shfl(last, 0, 64);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      // lane x < 13 sums quantity x over every (k, s) in order
+      double t = 0.0;
+      if (lane < kNQ)
+        for (int j = 0; j < K * S; ++j) t += a.part[(size_t)lane * K * S + j];
+      double q[kNQ];
 #pragma unroll
-          for (int z = 0; z < DP; ++z)
-            if (x < d && z < d) W[x * d + z] = (tW[x][z] + tW[z][x]) / 2;
-        } else if (x < d) {
-          W[x] = (tW[x][x] + tW[x][x]) / 2;
+      for (int x = 0; x < kNQ; ++x) {
+        const int lo = __builtin_amdgcn_readlane(__double2loint(t), x);
+        const int hi = __builtin_amdgcn_readlane(__double2hiint(t), x);
+        q[x] = __hiloint2double(hi, lo);
+      }
+      if (lane == 0) {
+        const double a0 = a.alpha0, e0 = a.eta0, ep0 = a.epsilon0, v0 = a.v0;
+        const double Lt3 = K * a.logCeta0 + (e0 - 1) * q[6];
+        const double Lt4 = (double)K * S * a.logCepsilon0 + (ep0 - 1) * q[7];
+        const double Lt5 =
+            0.5 * q[0] + (double)K * S * a.logB0 + 0.5 * (v0 - d - 1) * q[1] - 0.5 * q[2];
+        const double Lt6 = a.logCalpha0 + (a0 - 1) * q[9];
+        const double Lt8 = (lgamma_dev(q[12]) - q[11]) + q[10];
+        const double Lt10 = 0.5 * q[3] - 0.5 * d * S * K - q[4];
+        *L_out = st.Lt1 + q[8] + Lt3 + Lt4 + Lt5 + Lt6 - st.Lt7 - Lt8 - q[5] - Lt10;
+        *a.ticket = 0;  // ready for the next launch
+        if (a.flag) {   // the host polls this word (mapped memory) instead of syncing
+          __threadfence_system();
+          __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
-      eta_ks = a.eta0 + st.N1[ks];
-      a.eta_o[ks] = eta_ks;
-      for (int s2 = 0; s2 < S; ++s2)
-        a.eps_o[ks * S + s2] = a.epsilon0 + (S > 1 ? st.M[ks * S + s2] : 1e-12);
     }
-    alpha_k = a.alpha0 + (st.Nj[k] + 1e-50);
-    if (s == 0) {
-      a.alpha_o[k] = alpha_k;
-      for (int j = 0; j < K; ++j) sumA += a.alpha0 + (st.Nj[j] + 1e-50);
-    }
-  } else {
-    if (on) eta_ks = a.eta[ks];
-    alpha_k = a.alpha[k];
-    if (s == 0)
-      for (int j = 0; j < K; ++j) sumA += a.alpha[j];
   }
-  // every write of this thread's posterior entries is its own: read back below
-  const double *pv = do_mstep ? a.v_o : a.v, *plam = do_mstep ? a.lam_o : a.lam;
-  const double *pm = do_mstep ? a.m_o : a.m, *pW = do_mstep ? a.W_o : a.W;
-  const double *peps = do_mstep ? a.eps_o : a.eps;
-  if (on) {
-    // psi prelude (step_fc.m:118-165, 180-191)
-    const double v = pv[ks];
-    const double t1 = psi_sum_half_dev(v, d);
-    const double *W = pW + ks * dd;
-    double logdet = 0.0;
-    if (full) {
-      logdet = log(det_pad<DP>(W, d));
-    } else {
-      for (int x = 0; x < d; ++x) logdet += log(W[x]);
-    }
-    const double lLT = t1 + d * kLn2D + logdet;
-    a.lLT[ks] = lLT;
-    a.c[ks] = -lLT + d / plam[ks];
-    for (int x = 0; x < dd; ++x) a.P[ks * dd + x] = v * W[x];
-    for (int x = 0; x < d; ++x) a.cm[ks * d + x] = pm[ks * d + x];
-    const double *eps = peps + ks * S;
-    double es = 0.0;
-    for (int s2 = 0; s2 < S; ++s2) es += eps[s2];
-    const double pes = psi_dev(es);
-    for (int s2 = 0; s2 < S; ++s2) a.logA[ks * S + s2] = psi_dev(eps[s2]) - pes;
-  }
-  red[s] = eta_ks;
-  __syncthreads();
-  if (s == 0) {
-    double ets = 0.0;
-    for (int x = 0; x < S; ++x) ets += red[x];
-    red[0] = ets;
-    a.logOmega[k] = psi_dev(alpha_k) - psi_dev(sumA);
-  }
-  __syncthreads();
-  if (on) a.logPi[ks] = psi_dev(eta_ks) - psi_dev(red[0]);
-}
-
-// fixed-order block reduction of NQ partial sums (blockDim = kBoundThreads)
-template <int NQ>
-__device__ void block_sum(double (&q)[NQ], double *lds) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int x = 0; x < NQ; ++x) lds[x * kBoundThreads + t] = q[x];
-  __syncthreads();
-  for (int off = kBoundThreads / 2; off > 0; off >>= 1) {
-    if (t < off)
-#pragma unroll
-      for (int x = 0; x < NQ; ++x) lds[x * kBoundThreads + t] += lds[x * kBoundThreads + t + off];
-    __syncthreads();
-  }
-#pragma unroll
-  for (int x = 0; x < NQ; ++x) q[x] = lds[x * kBoundThreads];
-}
-
-// vbhemh3m_lb.m:64-186 (value), the same terms as vbhem_em_lower_bound
-template <int DP>
-__global__ __launch_bounds__(kBoundThreads) void em_bound_kernel(const EmDevArgs a, double *L_out) {
-  constexpr int NQ = 13;
-  __shared__ double lds[NQ * kBoundThreads];
-  const int K = a.K, S = a.S, d = a.d, t = threadIdx.x;
-  const bool full = a.covmode == 1;
-  const int dd = full ? d * d : d;
-  const StatsView st(a.stats, K, S, a.NU);
-  const double l0 = a.lambda0, const2 = d * log(l0 / (2 * kPiD));
-  // partial sums: 0 Lt51, 1 sum lLT, 2 sum v trW, 3 lt10a, 4 H, 5 Lt9, 6 sum logPi,
-  // 7 sum logA, 8 Lt2, 9 sum logOmega, 10 Lt8b, 11 sum lgamma(alpha), 12 sum alpha
-  double q[NQ];
-#pragma unroll
-  for (int x = 0; x < NQ; ++x) q[x] = 0.0;
-  for (int ks = t; ks < K * S; ks += kBoundThreads) {
-    const int k = ks / S, s = ks - k * S;
-    const double v = a.v[ks], lam = a.lam[ks], lLT = a.lLT[ks];
-    const double *W = a.W + (size_t)ks * dd;
-    double detW;
-    if (full) {
-      detW = det_pad<DP>(W, d);
-    } else {
-      detW = 1.0;
-      for (int x = 0; x < d; ++x) detW *= W[x];
-    }
-    const double sg = lgamma_sum_half_dev(v, d);
-    const double logBk = -(v / 2) * log(detW) - (v * d / 2) * kLn2D -
-                         (d * (d - 1) / 4.0) * log(kPiD) - sg;
-    q[4] += -logBk - 0.5 * (v - d - 1) * lLT + 0.5 * v * d;
-    double mWm = 0.0, trW = 0.0;
-    const double *mk = a.m + (size_t)ks * d;
-    for (int x = 0; x < d; ++x)
-      for (int z = 0; z < d; ++z) {
-        const double wxz = full ? W[x * d + z] : (x == z ? W[x] : 0.0);
-        const double wzx = full ? W[z * d + x] : (x == z ? W[x] : 0.0);
-        mWm += (mk[x] - a.m0[x]) * wxz * (mk[z] - a.m0[z]);
-        trW += a.W0inv[x * d + z] * wzx;
-      }
-    q[0] += const2 + lLT - d * l0 / lam - l0 * v * mWm;
-    q[1] += lLT;
-    q[2] += v * trW;
-    q[3] += lLT + d * log(lam / (2 * kPiD));
-    // Lt9: the epsilon row s of cluster k, eta entry s (and lgamma(sum eta) at s = 0)
-    const double *er = a.eps + (size_t)ks * S;
-    double ps = 0.0, lgp = 0.0, pt = 0.0, sla = 0.0;
-    for (int s2 = 0; s2 < S; ++s2) {
-      ps += er[s2];
-      lgp += lgamma(er[s2]);
-      pt += (er[s2] - 1) * a.logA[(size_t)ks * S + s2];
-      sla += a.logA[(size_t)ks * S + s2];
-    }
-    q[5] += lgamma(ps) - lgp + pt;
-    const double e = a.eta[ks];
-    q[5] += -lgamma(e) + (e - 1) * a.logPi[ks];
-    if (s == 0) {
-      double es = 0.0;
-      for (int s2 = 0; s2 < S; ++s2) es += a.eta[(size_t)k * S + s2];
-      q[5] += lgamma(es);
-    }
-    q[6] += a.logPi[ks];
-    q[7] += sla;
-  }
-  for (int k = t; k < K; k += kBoundThreads) {
-    const double lo = a.logOmega[k], al = a.alpha[k];
-    q[8] += (st.Nj[k] + 1e-50) * lo;
-    q[9] += lo;
-    q[10] += (al - 1) * lo;
-    q[11] += lgamma(al);
-    q[12] += al;
-  }
-  block_sum<NQ>(q, lds);
-  if (t == 0) {
-    const double a0 = a.alpha0, e0 = a.eta0, ep0 = a.epsilon0, v0 = a.v0;
-    const double Lt3 = K * a.logCeta0 + (e0 - 1) * q[6];
-    const double Lt4 = (double)K * S * a.logCepsilon0 + (ep0 - 1) * q[7];
-    const double Lt5 = 0.5 * q[0] + (double)K * S * a.logB0 + 0.5 * (v0 - d - 1) * q[1] - 0.5 * q[2];
-    const double Lt6 = a.logCalpha0 + (a0 - 1) * q[9];
-    const double Lt8 = (lgamma(q[12]) - q[11]) + q[10];
-    const double Lt10 = 0.5 * q[3] - 0.5 * d * S * K - q[4];
-    *L_out = st.Lt1 + q[8] + Lt3 + Lt4 + Lt5 + Lt6 - st.Lt7 - Lt8 - q[5] - Lt10;
-  }
-}
-
-template <int DP>
-hipError_t launch_em_dev(const EmDevArgs &a, int mode, double *L_out, hipStream_t st) {
-  if (mode == kEmBound) {
-    hipLaunchKernelGGL(em_bound_kernel<DP>, dim3(1), dim3(kBoundThreads), 0, st, a, L_out);
-  } else {
-    hipLaunchKernelGGL(em_step_kernel<DP>, dim3(a.K), dim3(kStepThreads), 0, st, a,
-                       mode == kEmMstepPrelude ? 1 : 0);
-  }
-  return hipGetLastError();
 }
 
 }  // namespace
 
-bool em_dev_supported(int d, int S) { return d >= 1 && d <= kEmDevMaxD && S >= 1 && S <= kStepThreads; }
+bool em_dev_supported(int d, int S) { return d >= 1 && d <= kEmDevMaxD && S >= 1 && S <= 32; }
 
 hipError_t launch_em_dev(const EmDevArgs &a, int mode, double *L_out, hipStream_t st) {
-  if (!em_dev_supported(a.d, a.S)) return hipErrorInvalidValue;
-  if (a.d <= 2) return launch_em_dev<2>(a, mode, L_out, st);
-  if (a.d <= 4) return launch_em_dev<4>(a, mode, L_out, st);
-  if (a.d <= 8) return launch_em_dev<8>(a, mode, L_out, st);
-  return launch_em_dev<16>(a, mode, L_out, st);
+  if (!em_dev_supported(a.d, a.S) || (mode == kEmIterate && (!L_out || !a.ticket || !a.part)))
+    return hipErrorInvalidValue;
+  const int nw = a.K * a.S;
+  hipLaunchKernelGGL(em_iter_kernel, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, st, a,
+                     mode, L_out);
+  return hipGetLastError();
 }
 
 }  // namespace vbhem

@@ -79,7 +79,15 @@ size_t vbhem_em_workspace_bytes(const vbhem_base_t *base, int K, int S, int T);
  * stats_dev [vbhem_stats_len], hatZ_dev / LL_dev [N][K]).  `post` (host) holds the
  * initial posteriors and receives the final ones; LogLs [max_iter + 1] receives the
  * lower bound of every iteration (before its M-step); *iters, *L_final, *stable as
- * in vbhem_h3m_c_step_fc.m:311-374 (L = -inf and no M-step when the bound is NaN). */
+ * in vbhem_h3m_c_step_fc.m:311-374 (L = -inf and no M-step when the bound is NaN).
+ * hatZ_dev / LL_dev receive the last accepted E-step's hat_Z and L_elbo.
+ * For d <= 16 and S <= 32 the per-iteration host math (bound, M-step, prelude) runs
+ * on the device (vbhem_em_dev.hip) and the loop keeps the next iteration queued
+ * while it reads this one's bound (one iteration ahead: a converging run computes
+ * one E-step it then discards, so stats_dev holds the statistics of the last E-step
+ * RUN); otherwise, or with VBHEM_EM_HOST_MATH set, the host math runs in C++ on the
+ * host between synchronous E-steps.  The all-reduce callback always reduces
+ * stats_dev, once per E-step run, in the same order on every rank. */
 int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
                  const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
                  double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
