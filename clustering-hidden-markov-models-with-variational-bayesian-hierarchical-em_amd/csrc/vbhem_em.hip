@@ -29,6 +29,7 @@ constexpr double kPi = 3.14159265358979323846;
 // digamma for x > 0: psi(x) = psi(x + n) - sum_{k<n} 1/(x + k), then the
 // asymptotic expansion ln x - 1/(2x) - sum B_2k / (2k x^2k) at x >= 8.
 double psi(double x) {
+  if (!(x > 0.0 && x < INFINITY)) return x == INFINITY ? x : std::nan("");
   double acc = 0.0;
   while (x < 8.0) {
     acc -= 1.0 / x;

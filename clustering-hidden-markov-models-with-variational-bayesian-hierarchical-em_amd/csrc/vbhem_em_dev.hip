@@ -42,6 +42,7 @@ constexpr int kWaves = 4;  // waves (cluster states) per block
 // numerator / denominator (fp64 division is a long dependent sequence on the GPU),
 // then ln z - 1/(2z) - sum B_2k / (2k z^2k)
 __device__ double psi_dev(double x) {
+  if (!(x > 0.0 && x < INFINITY)) return x == INFINITY ? x : __builtin_nan("");
   double num = 0.0, den = 1.0;
   while (x < 8.0) {  // num / den = sum 1/(x_i) so far
     num = fma(num, x, den);
@@ -59,6 +60,7 @@ __device__ double psi_dev(double x) {
 // z = x + n >= 10, then Stirling's series (z - 1/2) ln z - z + ln(2 pi)/2 +
 // sum B_2k / (2k (2k - 1) z^(2k-1)) through z^-15 (next term < 3e-18 at z = 10)
 __device__ double lgamma_dev(double x) {
+  if (!(x > 0.0 && x < INFINITY)) return x == INFINITY ? x : __builtin_nan("");
   double prod = 1.0;
   while (x < 10.0) {
     prod *= x;
@@ -99,50 +101,42 @@ __device__ __forceinline__ double wsum(double v) {
   return __hiloint2double(hi, lo);
 }
 
-// Gauss-Jordan elimination with partial pivoting of the d x d matrix in g[0 .. d)
-// x [0 .. 2d) (row stride 2d, wave-private LDS), the right half holding I on entry:
-// on exit the right half holds the inverse.  Returns det (every lane).  Lanes own
-// the entries x = lane + 64 j of the d x 2d array.
-__device__ double gauss_jordan(double *g, int d, int lane) {
-  const int w2 = 2 * d, n = d * w2;
+// Gauss-Jordan elimination of the d x d matrix in g[0 .. d) x [0 .. cols) (row
+// stride 2d, wave-private LDS).  cols = 2d with I in the right half on entry: on exit
+// the right half holds the inverse; cols = d: the left half only (for the
+// determinant).  Returns det (every lane).  Both matrices it is used on are
+// symmetric positive definite (Mt = W0^-1 + Nr SC + mult1 dd', and W), so the
+// diagonal pivots are positive and need no row exchanges (the host path's LU
+// pivots as MATLAB does; the results agree to rounding).  Lanes own the entries
+// x = lane + 64 j of the d x cols array (row / column computed once); per step every
+// lane reads the pivot, its row's multiplier and the pivot row's entry of its column
+// (three independent LDS reads), one reciprocal, one fma per entry.
+__device__ __forceinline__ double gauss_jordan(double *g, int d, int cols, int lane) {
+  const int w2 = 2 * d, n = d * cols;
+  int er[8], ec[8];  // n / 64 <= 8 entries per lane (d <= 16); er < 0: no entry
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int x = lane + 64 * j;
+    er[j] = x < n ? x / cols : -1;
+    ec[j] = x < n ? x - er[j] * cols : 0;
+  }
   double det = 1.0;
   for (int k = 0; k < d; ++k) {
-    // pivot: the first row r >= k with the largest |g[r][k]| (every lane scans the
-    // column: broadcast LDS reads, no cross-lane exchange)
-    int p = k;
-    double best = fabs(g[k * w2 + k]);
-    for (int r = k + 1; r < d; ++r) {
-      const double t = fabs(g[r * w2 + k]);
-      if (t > best) {
-        best = t;
-        p = r;
-      }
-    }
-    const double piv = g[p * w2 + k];
-    det *= (p != k) ? -piv : piv;
-    // new row r of the array: rows k and p swapped, row k divided by the pivot,
-    // every other row minus its column-k multiple of the new row k
-    double nv[8];  // n / 64 <= 8 entries per lane (d <= 16)
+    const double piv = g[k * w2 + k], rp = 1.0 / piv;
+    double nv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int x = lane + 64 * j;
-      if (x < n) {
-        const int r = x / w2, c = x - r * w2;
-        const double rk = g[p * w2 + c] / piv;                   // new row k
-        if (r == k) {
-          nv[j] = rk;
-        } else {
-          const int src = (r == p) ? k : r;
-          nv[j] = g[src * w2 + c] - g[src * w2 + k] * rk;
-        }
+      if (er[j] >= 0) {
+        const int r = er[j], c = ec[j];
+        const double rk = g[k * w2 + c] * rp;  // new pivot row
+        nv[j] = r == k ? rk : fma(-g[r * w2 + k], rk, g[r * w2 + c]);
       }
     }
+    det *= piv;
     wsync();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int x = lane + 64 * j;
-      if (x < n) g[x] = nv[j];
-    }
+    for (int j = 0; j < 8; ++j)
+      if (er[j] >= 0) g[er[j] * w2 + ec[j]] = nv[j];
     wsync();
   }
   return det;
@@ -171,35 +165,68 @@ struct StatsView {
 // 7 sum logA row, 8 Lt2, 9 logOmega, 10 Lt8b, 11 lgamma(alpha), 12 alpha
 constexpr int kNQ = 13;
 
+#ifdef EMDEV_TIMING
+__device__ long long emdev_t[8][1024];  // [phase][wave]: s_memrealtime (100 MHz)
+#define EMDEV_MARK(ph)                                                  \
+  if (lane == 0 && ks < 1024) emdev_t[ph][ks] = __builtin_amdgcn_s_memrealtime()
+#else
+#define EMDEV_MARK(ph)
+#endif
+
 __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a, int mode,
                                                               double *L_out) {
   __shared__ double glds[kWaves][2 * kEmDevMaxD * kEmDevMaxD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int K = a.K, S = a.S, d = a.d;
-  const int ks = blockIdx.x * kWaves + wave;
+  const int ks = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wave);  // wave-uniform
   if (ks >= K * S) return;
   const int k = ks / S, s = ks - k * S;
   const bool full = a.covmode == 1;
   const int dd = full ? d * d : d;
   double *g = glds[wave];
   const bool iterate = mode == kEmIterate;
-  const StatsView st(iterate ? a.stats : nullptr, K, S);
+  // (the view is built in both modes: a.stats is always a valid buffer, so a load
+  // the compiler hoists out of an `iterate ? stats : posterior` select cannot fault)
+  const StatsView st(a.stats, K, S);
+  EMDEV_MARK(0);
 
   // ---- 1. bound terms of the current posterior (vbhemh3m_lb.m:64-186) ----
   if (iterate) {
     const double v = a.v[ks], lam = a.lam[ks], lLT = a.lLT[ks], l0 = a.lambda0;
     const double *W = a.W + (size_t)ks * dd, *mk = a.m + (size_t)ks * d;
-    // lanes q < d: lgamma((v + 1 - q) / 2); lanes 32 + s2: the epsilon row
-    double t_sg = 0.0, t_lge = 0.0, t_eps = 0.0, t_ept = 0.0, t_la = 0.0;
-    if (lane < d) t_sg = lgamma_dev(0.5 * (v - lane));
+    // the epsilon row on lanes 32 + s2 (and its sum), eta, the cluster's eta sum and
+    // alpha_k first, so that every lgamma of the (k, s) terms is one parallel round:
+    // lanes q < d lgamma((v + 1 - q) / 2), lanes 32 + s2 lgamma(eps), lanes 16..19
+    // lgamma of sum(eps row), eta, sum(eta) and alpha_k (the last two for state 0)
+    double t_eps = 0.0, t_ept = 0.0, t_la = 0.0;
     if (lane >= 32 && lane - 32 < S) {
       const int s2 = lane - 32;
-      const double e = a.eps[(size_t)ks * S + s2], la = a.logA[(size_t)ks * S + s2];
-      t_lge = lgamma_dev(e);
-      t_eps = e;
-      t_ept = (e - 1) * la;
+      const double la = a.logA[(size_t)ks * S + s2];
+      t_eps = a.eps[(size_t)ks * S + s2];
+      t_ept = (t_eps - 1) * la;
       t_la = la;
     }
+    const double e = a.eta[ks];
+    double es = 0.0, lo = 0.0, al = 0.0;
+    if (s == 0) {
+      es = wsum(lane < S ? a.eta[(size_t)k * S + lane] : 0.0);
+      lo = a.logOmega[k];
+      al = a.alpha[k];
+    }
+    const double ps = wsum(t_eps);
+    double xg = 0.0;
+    bool lg_on = false;
+    if (lane < d) {
+      xg = 0.5 * (v - lane);
+      lg_on = true;
+    } else if (lane >= 32 && lane - 32 < S) {
+      xg = t_eps;
+      lg_on = true;
+    } else if (lane >= 16 && lane < 20) {
+      xg = lane == 16 ? ps : lane == 17 ? e : lane == 18 ? es : al;
+      lg_on = lane < 18 || s == 0;
+    }
+    const double lgx = lg_on ? lgamma_dev(xg) : 0.0;
     // quadratic forms over the lanes = entries (x, z)
     double t_mwm = 0.0, t_tr = 0.0;
     for (int x = lane; x < d * d; x += 64) {
@@ -209,21 +236,10 @@ __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a,
       t_mwm += (mk[r] - a.m0[r]) * wrc * (mk[c] - a.m0[c]);
       t_tr += a.W0inv[x] * wcr;
     }
-    const double sg = wsum(t_sg), lgp = wsum(t_lge), ps = wsum(t_eps), pt = wsum(t_ept);
-    const double sla = wsum(t_la), mWm = wsum(t_mwm), trW = wsum(t_tr);
-    const double e = a.eta[ks];
-    double es = 0.0, lo = 0.0, al = 0.0;
-    if (s == 0) {
-      es = wsum(lane < S ? a.eta[(size_t)k * S + lane] : 0.0);
-      lo = a.logOmega[k];
-      al = a.alpha[k];
-    }
-    // the remaining lgammas in one parallel round: lane 0 sum(eps row), 1 eta,
-    // 2 sum(eta) (state 0), 3 alpha_k (state 0)
-    const double xg = lane == 0 ? ps : lane == 1 ? e : lane == 2 ? es : al;
-    const double lgx = (lane < 2 || (s == 0 && lane < 4)) ? lgamma_dev(xg) : 0.0;
-    const double lg_ps = __shfl(lgx, 0, 64), lg_e = __shfl(lgx, 1, 64);
-    const double lg_es = __shfl(lgx, 2, 64), lg_al = __shfl(lgx, 3, 64);
+    const double sg = wsum(lane < d ? lgx : 0.0), lgp = wsum(lane >= 32 ? lgx : 0.0);
+    const double pt = wsum(t_ept), sla = wsum(t_la), mWm = wsum(t_mwm), trW = wsum(t_tr);
+    const double lg_ps = __shfl(lgx, 16, 64), lg_e = __shfl(lgx, 17, 64);
+    const double lg_es = __shfl(lgx, 18, 64), lg_al = __shfl(lgx, 19, 64);
     if (lane < kNQ) {
       const double logBk = -(v / 2) * a.logdetW[ks] - (v * d / 2) * kLn2D -
                            (d * (d - 1) / 4.0) * log(kPiD) - sg;
@@ -247,13 +263,14 @@ __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a,
     }
   }
 
+  EMDEV_MARK(1);
   // ---- 2. M-step of (k, s) (vbhem_compute_Statistics.m:57-82, mstep_component.m:42-70) ----
   // Every lane keeps what it needs of the new posterior in registers or in its own
   // LDS entries (no lane reads another lane's global stores): v, lam in all lanes,
   // m_a in lane a, the epsilon row entry s2 in lanes s2 and 32 + s2, W in the left
   // half of g (then [W | I] for its determinant).
   const int w2 = 2 * d;
-  double v, lam, m_l = 0.0, e_l = 0.0, eta_ks, sum_eta = 0.0, alpha_k;
+  double v, lam, m_l = 0.0, e_l = 0.0, eta_ks, sum_eta = 0.0, alpha_k, det_mt = 1.0;
   if (iterate) {
     const double *u = st.U + (size_t)ks * a.NU;
     const double Nr = u[0] + 1e-50, l0 = a.lambda0;
@@ -288,7 +305,9 @@ __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a,
       a.v_o[ks] = v;
     }
     wsync();
-    gauss_jordan(g, d, lane);
+    EMDEV_MARK(2);
+    det_mt = gauss_jordan(g, d, 2 * d, lane);
+    EMDEV_MARK(3);
     // W = (tW + tW') / 2, left half of g; right half back to I
     double nw[4];
 #pragma unroll
@@ -337,52 +356,66 @@ __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a,
     }
   }
   wsync();
+  EMDEV_MARK(4);
   sum_eta = wsum(lane < S ? sum_eta : 0.0);  // the cluster's eta (lanes < S hold them)
 
   // ---- 3. prelude of (k, s) (step_fc.m:118-165, 180-191, 271-273) ----
-  double t_psi = 0.0;
-  if (lane < d) t_psi = psi_dev(0.5 * (v - lane));
-  const double t1 = wsum(t_psi);
   const double es = wsum(lane >= 32 && lane - 32 < S ? e_l : 0.0);
+  double sa = 0.0;  // sum_k alpha (state 0's wave): lane-strided partials, one DPP sum
+  if (s == 0) {
+    double t = 0.0;
+    for (int j = lane; j < K; j += 64)
+      t += iterate ? a.alpha0 + (st.Nj[j] + 1e-50) : a.alpha[j];
+    sa = wsum(t);
+  }
+  // every psi of (k, s) in one parallel round: lanes q < d psi((v + 1 - q) / 2),
+  // lanes 32 + s2 the epsilon row, lanes 16..20 psi of sum(eps row), eta, sum(eta),
+  // alpha_k and sum(alpha) (the last two for state 0)
+  double xp = 0.0;
+  bool p_on = false;
+  if (lane < d) {
+    xp = 0.5 * (v - lane);
+    p_on = true;
+  } else if (lane >= 32 && lane - 32 < S) {
+    xp = e_l;
+    p_on = true;
+  } else if (lane >= 16 && lane < 21) {
+    xp = lane == 16 ? es : lane == 17 ? eta_ks : lane == 18 ? sum_eta : lane == 19 ? alpha_k : sa;
+    p_on = lane < 19 || s == 0;
+  }
+  const double pl = p_on ? psi_dev(xp) : 0.0;
+  const double t1 = wsum(lane < d ? pl : 0.0);
+  const double pes = __shfl(pl, 16, 64), pet = __shfl(pl, 17, 64), pst = __shfl(pl, 18, 64);
+  const double pal = __shfl(pl, 19, 64), psa = __shfl(pl, 20, 64);
   // P = v W and the diagonal's logs from g's left half, before the elimination
   for (int x = lane; x < dd; x += 64) {
     const int r = full ? x / d : x, c = full ? x - r * d : x;
     a.P[(size_t)ks * dd + x] = v * g[r * w2 + c];
   }
   double logdet;
-  if (full) {
+  if (full && iterate) {
+    // W = (inv(Mt) + inv(Mt)') / 2: log det W = -log det Mt (the M-step's
+    // elimination; the symmetrisation moves it by rounding only)
+    logdet = -log(det_mt);
+  } else if (full) {
     wsync();
-    logdet = log(gauss_jordan(g, d, lane));
+    logdet = log(gauss_jordan(g, d, d, lane));
   } else {
     logdet = wsum(lane < d ? log(g[lane * w2 + lane]) : 0.0);
   }
+  EMDEV_MARK(5);
   const double lLT = t1 + d * kLn2D + logdet;
   if (lane < d) a.cm[(size_t)ks * d + lane] = m_l;
-  // psi of the epsilon row (lanes 32 + s2), of its sum (lane 0), of eta (lane 1) and
-  // of the cluster's eta sum (lane 2)
-  double pl = 0.0;
-  if (lane >= 32 && lane - 32 < S) pl = psi_dev(e_l);
-  else if (lane == 0) pl = psi_dev(es);
-  else if (lane == 1) pl = psi_dev(eta_ks);
-  else if (lane == 2) pl = psi_dev(sum_eta);
-  const double pes = __shfl(pl, 0, 64), pet = __shfl(pl, 1, 64), pst = __shfl(pl, 2, 64);
   if (lane >= 32 && lane - 32 < S) a.logA[(size_t)ks * S + (lane - 32)] = pl - pes;
   if (lane == 0) {
     a.lLT[ks] = lLT;
     a.logdetW[ks] = logdet;
     a.c[ks] = -lLT + d / lam;
     a.logPi[ks] = pet - pst;
-  }
-  if (s == 0) {
-    // logOmega[k] = psi(alpha_k) - psi(sum alpha): the sum as lane-strided partials
-    // added in lane order (the same arithmetic in every wave)
-    double t = 0.0;
-    for (int j = lane; j < K; j += 64)
-      t += iterate ? a.alpha0 + (st.Nj[j] + 1e-50) : a.alpha[j];
-    const double sa = wsum(t);
-    if (lane == 0) a.logOmega[k] = psi_dev(alpha_k) - psi_dev(sa);
+    if (s == 0) a.logOmega[k] = pal - psa;
   }
 
+  EMDEV_MARK(6);
   // ---- the bound: the last wave reduces every (k, s)'s partial sums ----
   if (iterate) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -391,17 +424,17 @@ __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a,
     last = __shfl(last, 0, 64);
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      // lane x < 13 sums quantity x over every (k, s) in order
-      double t = 0.0;
-      if (lane < kNQ)
-        for (int j = 0; j < K * S; ++j) t += a.part[(size_t)lane * K * S + j];
+      // every lane sums its strided share of each quantity (independent loads),
+      // then one fixed-order DPP sum per quantity
       double q[kNQ];
 #pragma unroll
-      for (int x = 0; x < kNQ; ++x) {
-        const int lo = __builtin_amdgcn_readlane(__double2loint(t), x);
-        const int hi = __builtin_amdgcn_readlane(__double2hiint(t), x);
-        q[x] = __hiloint2double(hi, lo);
+      for (int x = 0; x < kNQ; ++x) q[x] = 0.0;
+      for (int j = lane; j < K * S; j += 64) {  // the 13 loads of a round in flight together
+#pragma unroll
+        for (int x = 0; x < kNQ; ++x) q[x] += a.part[(size_t)x * K * S + j];
       }
+#pragma unroll
+      for (int x = 0; x < kNQ; ++x) q[x] = wsum(q[x]);
       if (lane == 0) {
         const double a0 = a.alpha0, e0 = a.eta0, ep0 = a.epsilon0, v0 = a.v0;
         const double Lt3 = K * a.logCeta0 + (e0 - 1) * q[6];
@@ -413,6 +446,7 @@ __global__ __launch_bounds__(64 * kWaves) void em_iter_kernel(const EmDevArgs a,
         const double Lt10 = 0.5 * q[3] - 0.5 * d * S * K - q[4];
         *L_out = st.Lt1 + q[8] + Lt3 + Lt4 + Lt5 + Lt6 - st.Lt7 - Lt8 - q[5] - Lt10;
         *a.ticket = 0;  // ready for the next launch
+        EMDEV_MARK(7);
         if (a.flag) {   // the host polls this word (mapped memory) instead of syncing
           __threadfence_system();
           __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
