@@ -598,7 +598,9 @@ size_t vbhem_prepare_base_bytes(const vbhem_base_t *base) {
       (base->covmode != VBHEM_COV_DIAG && base->covmode != VBHEM_COV_FULL))
     return 0;
   if (vbhem::emission_kdp(base->d, base->covmode) / 4 > vbhem::kUMaxKq) return 0;
-  return vbhem::u_doubles((long long)base->N * base->SB, base->d, base->covmode) * sizeof(double);
+  // the emission GEMM's operand U, then its statistics copy Us (vbhem_internal.h)
+  return (vbhem::u_doubles((long long)base->N * base->SB, base->d, base->covmode) +
+          vbhem::us_doubles(base->N, base->SB, base->d, base->covmode)) * sizeof(double);
 }
 
 int vbhem_prepare_base(const vbhem_base_t *base, double *U_dev, size_t bytes, void *stream) {
@@ -617,6 +619,10 @@ int vbhem_prepare_base(const vbhem_base_t *base, double *U_dev, size_t bytes, vo
   ua.U = U_dev; ua.z = nullptr;  // shift = mean of the valid base means
   hipError_t e = vbhem::launch_u_prep(ua, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "u_prep_kernel");
+  e = vbhem::launch_us_build(ua, U_dev + vbhem::u_doubles((long long)base->N * base->SB, base->d,
+                                                         base->covmode),
+                             static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "us_build_kernel");
   return VBHEM_OK;
 }
 
@@ -799,10 +805,12 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     sa.assign = gated && g0 == 0;
     // the emission GEMM's operand for this group (prepared, or built by run_fb)
     sa.U = nullptr;
+    sa.Us = nullptr;
     if (ctx.split.ok && ctx.use_u) {
       sa.ukdp = ctx.em.kdp;
       if (base->U) {
         sa.U = base->U; sa.uz = base->U; sa.u_col0 = 0;
+        sa.Us = base->U + vbhem::u_doubles((long long)base->N * SB, base->d, base->covmode);
       } else if (ctx.u_ws) {
         sa.U = ctx.u_ws; sa.uz = ctx.em.shift; sa.u_col0 = (long long)g0 * SB / 16 * 16;
       }

@@ -525,6 +525,44 @@ __global__ __launch_bounds__(kUThreads) void u_prep_kernel(UPrepArgs p) {
   }
 }
 
+// us_build_kernel: the statistics copy Us (vbhem_internal.h), one thread per entry
+// (grid-stride), the same moment arithmetic as u_prep_kernel.
+__global__ __launch_bounds__(kUThreads) void us_build_kernel(UPrepArgs p, double *Us) {
+  __shared__ double zs[kUHead];
+  const int tid = threadIdx.x, d = p.d, SB = p.SB;
+  const bool full = p.covmode == kCovFull;
+  const int NPF = full ? d * (d + 1) / 2 : d, NU = 1 + d + NPF;
+  const int SBP = us_sbp(SB), NUP = us_nup(NU);
+  const int dd = full ? d * d : d;
+  for (int a = tid; a < d; a += kUThreads) zs[a] = p.U[a];
+  __syncthreads();
+  const long long n = (long long)p.N * SBP * NUP;
+  for (long long x = (long long)blockIdx.x * kUThreads + tid; x < n; x += (long long)gridDim.x * kUThreads) {
+    const long long i = x / (SBP * NUP);
+    const int r = (int)(x - i * (SBP * NUP)), b = r / NUP, f = r - b * NUP;
+    double u = 0.0;
+    if (b < SB && f < NU) {
+      const long long col = i * SB + b;
+      const double *mu = p.centres + (size_t)col * d;
+      if (f == 0) {
+        u = 1.0;
+      } else if (f <= d) {
+        u = mu[f - 1] - zs[f - 1];
+      } else {
+        const double *C = p.covars + (size_t)col * dd;
+        const int e = f - 1 - d;
+        int a = e, bb = e;
+        if (full) packed_ab(e, d, a, bb);
+        const double ma = mu[a] - zs[a], mb = mu[bb] - zs[bb];
+        if (!full) u = fma(ma, ma, C[a]);
+        else if (a == bb) u = fma(ma, ma, C[a * d + a]);
+        else u = fma(2.0 * ma, mb, C[a * d + bb] + C[bb * d + a]);
+      }
+    }
+    Us[x] = u;
+  }
+}
+
 template <int KQB, int RC, int NTW, bool EXACT, bool PF = false>
 __global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
@@ -683,6 +721,15 @@ hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st) {
   }
   if (ntile > 0 && a.i_end > a.i_begin)
     hipLaunchKernelGGL(u_prep_kernel, dim3((unsigned)ntile), dim3(kUThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_us_build(const UPrepArgs &a, double *Us, hipStream_t st) {
+  if (a.d < 1 || a.d > kUHead || a.N < 0) return hipErrorInvalidValue;
+  const long long n = (long long)us_doubles(a.N, a.SB, a.d, a.covmode);
+  if (n == 0) return hipSuccess;
+  const long long nb = std::min<long long>((n + kUThreads - 1) / kUThreads, 16384);
+  hipLaunchKernelGGL(us_build_kernel, dim3((unsigned)nb), dim3(kUThreads), 0, st, a, Us);
   return hipGetLastError();
 }
 

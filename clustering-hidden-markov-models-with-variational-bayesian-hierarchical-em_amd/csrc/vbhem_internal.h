@@ -121,6 +121,7 @@ struct StatsArgs {
   long long u_col0;      // first column of U
   int ukdp;              // k-extent of U (multiple of 4)
   int nzero;             // stats_list_u_kernel with assign: slabs [gridDim.x, nzero) get zeros
+  const double *Us;      // the statistics copy of the prepared operand (us_doubles), or null
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).
@@ -203,6 +204,21 @@ struct UPrepArgs {
                               // mean of the valid base means of [0, N) into the head first
 };
 hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st);
+// The statistics copy of the base-set operand (vbhem_prepare_base, right after U in
+// the same buffer): per base i an [SBP][NUP] block (SBP = SB rounded up to 4, NUP =
+// NU rounded up to 16) of the statistic features f of every base state b:
+// 1 | mu'_a (d) | packed Sigma + mu' mu'^T (as U, off-diagonals Sigma_ab + Sigma_ba +
+// 2 mu'_a mu'_b), mu' = mu - z, zero past SB and NU.  stats_list_m_kernel's MFMA B
+// operand: 16 features of one state are one 128-byte segment, a base's block is
+// contiguous (the tile order of U splits it over two 16-column tiles' half lines).
+__host__ __device__ inline int us_sbp(int SB) { return (SB + 3) / 4 * 4; }
+__host__ __device__ inline int us_nup(int NU) { return (NU + 15) / 16 * 16; }
+__host__ __device__ inline int us_nu(int d, int covmode) { return 1 + d + (covmode == kCovFull ? d * (d + 1) / 2 : d); }
+inline size_t us_doubles(long long N, int SB, int d, int covmode) {
+  return (size_t)N * us_sbp(SB) * us_nup(us_nu(d, covmode));
+}
+// builds Us for bases [0, a.N) with the shift in a.U's head (after launch_u_prep)
+hipError_t launch_us_build(const UPrepArgs &a, double *Us, hipStream_t st);
 hipError_t launch_emission_prep(const EmissionArgs &a, hipStream_t st);
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st);
 

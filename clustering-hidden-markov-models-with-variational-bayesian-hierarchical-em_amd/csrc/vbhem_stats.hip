@@ -1081,6 +1081,193 @@ __global__ __launch_bounds__(64 * kSuWaves) void stats_list_u_kernel(const Stats
   su_output(p, red, zs, c, nch, j, tid);
 }
 
+// ---------------------------------------------------------------------------
+// stats_list_m_kernel<NTW, G, KSM, NXR, PD>: the gated sums on the MFMA pipe, from the
+// statistics copy Us of the prepared operand.  For cluster j the emission moments are
+//   acc[s][f] = sum over the gated pairs (i, j) and base states b of
+//               (Z tnu)(s, b) * Us(i, b, f)
+// i.e. one (16 x 4) x (4 x 16) v_mfma_f64_16x16x4f64 per k-slice of four base states
+// and 16-feature tile: A = Z tnu (lane: state s = lane & 15, base state 4 kk + lane / 16;
+// zero past S / SB), B = 16 consecutive features of one base state's row of Us (one
+// 128-byte segment per lane quarter).  Block (c, j) = part c of cluster j's list, as
+// stats_list_u_kernel.  Its 4 waves are G pair groups x 4 / G tile groups: wave w takes
+// the part's pairs w % G, + G, ... and the feature tiles w / G + (4 / G) t, t < NTW,
+// plus the sum_nu_1 | sum_xi entries lane + 64 (w / G + (4 / G) r).  The next PD - 1
+// pairs' operands are in flight while a pair's MFMAs run (a register ring; the kernel is
+// bound by memory latency, not by the MFMA pipe); no LDS in the loop.  The
+// pair groups' sums are added in group order at the end (bit-reproducible).  Output
+// as stats_list_u_kernel (shifted back by z).
+// ---------------------------------------------------------------------------
+constexpr int kSmWaves = 4;
+static_assert(kSmWaves == kSuWaves, "su_output's thread stride");
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int NTW, int G, int KSM, int NXR, int PD>
+__global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const StatsArgs p) {
+  extern __shared__ double lds[];
+  constexpr int TG = kSmWaves / G;  // tile groups; NXR: sum_nu_1 | sum_xi chunks of 64 per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pg = wave % G, tg = wave / G;
+  const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU;
+  const int SBP = us_sbp(SB), NUP = us_nup(NU), ntile = NUP / 16, KSL = SBP / 4;
+  const int OT = S * SB, NX = S + S * S;
+  // block -> (cluster j, part c of its list, parts nch): the gated pairs of all clusters
+  // in parts of about P = total / (blocks - K) pairs, at most p.nzero (the slab count)
+  // parts per cluster, at least one (an empty cluster's block writes its zeros)
+  __shared__ int sm_map[3];
+  if (wave == 0) {
+    int total = 0;
+    for (int x = lane; x < K; x += 64) total += p.list_tot[x];
+    for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
+    const int nb = (int)gridDim.x, P = max(1, (total + max(1, nb - K) - 1) / max(1, nb - K));
+    int pre = 0, jj = -1, cc = 0, np = 1;
+    for (int x0 = 0; x0 < K && jj < 0; x0 += 64) {
+      const int x = x0 + lane;
+      int parts = 0;
+      if (x < K) {
+        const int t = p.list_tot[x], Pj = max(P, (t + p.nzero - 1) / p.nzero);
+        parts = max(1, (t + Pj - 1) / Pj);
+      }
+      int inc = parts;  // inclusive prefix over the lanes
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+      }
+      const int b0 = pre + inc - parts;  // this cluster's first block
+      const bool hit = x < K && (int)blockIdx.x >= b0 && (int)blockIdx.x < b0 + parts;
+      const unsigned long long m = __ballot(hit);
+      if (m) {
+        const int src = __builtin_ctzll(m);
+        jj = __shfl(x, src, 64);
+        cc = (int)blockIdx.x - __shfl(b0, src, 64);
+        np = __shfl(parts, src, 64);
+      }
+      pre += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) {
+      sm_map[0] = jj;
+      sm_map[1] = cc;
+      sm_map[2] = np;
+    }
+  }
+  __syncthreads();
+  const int j = sm_map[0], c = sm_map[1], nch = sm_map[2];
+  if (j < 0) return;  // past the last part (block-uniform)
+  double *red = lds;                                  // [S][NU] | [S] | [S][S]
+  double *zs = red + (size_t)S * NU + S + S * S;      // [d]
+  for (int a = tid; a < d; a += 64 * kSmWaves) zs[a] = p.uz[a];
+  const int kl = lane >> 4, cl = lane & 15;
+  dbl4 acc[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double ax[NXR];
+#pragma unroll
+  for (int r = 0; r < NXR; ++r) ax[r] = 0.0;
+  const int tot = p.list_tot[j];
+  const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
+  const int *lst = p.list + (size_t)j * p.list_cap;
+  // one pair's operands: A values per k-slice, B values per (tile, k-slice), its Z and
+  // its sum_nu_1 / sum_xi entries; a ring of PD of them (PD - 1 pairs' loads in flight
+  // while a pair's MFMAs run)
+  struct Ops {
+    double ta[KSM], ub[NTW][KSM], xv[NXR], z;
+  };
+  Ops buf[PD];
+  auto load = [&](int i, Ops &o) {
+    // wave-uniform bases (SGPRs), 32-bit lane offsets: saddr loads, no 64-bit address
+    // arithmetic per lane
+    const size_t lp = (size_t)(i - p.i_buf0) * K + j;
+    o.z = p.Z[lp];
+    const double *us = p.Us + (size_t)i * SBP * NUP;
+    const double *tp = p.tnu + lp * OT, *n1p = p.nu1 + lp * S, *xp = p.xi + lp * S * S;
+    // lane-varying bounds by clamped (always valid) loads and a select, not branches
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk) {
+      if (kk < KSL) {  // wave-uniform
+        const int b = 4 * kk + kl;
+        const bool ok = cl < S && b < SB;
+        const double v = tp[ok ? (unsigned)(cl * SB + b) : 0u];
+        o.ta[kk] = ok ? v : 0.0;
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          const int ft = tg + TG * t;
+          if (ft < ntile) o.ub[t][kk] = us[(unsigned)(b * NUP + 16 * ft + cl)];  // b < SBP: in the block
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NXR; ++r) {
+      const int x = lane + 64 * (tg + TG * r);
+      const double v1 = n1p[x < S ? (unsigned)x : 0u];
+      const double v2 = xp[x >= S && x < NX ? (unsigned)(x - S) : 0u];
+      o.xv[r] = x < S ? v1 : x < NX ? v2 : 0.0;
+    }
+  };
+  auto compute = [&](const Ops &o) {
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk) {
+      if (kk < KSL) {
+        const double av = o.z * o.ta[kk];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+          if (tg + TG * t < ntile) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, o.ub[t][kk], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NXR; ++r) ax[r] = fma(o.z, o.xv[r], ax[r]);
+  };
+  // this wave's pairs: n0 + pg + G k, k < cnt; their bases fetched 64 at a time, one
+  // per lane, for the load cursor
+  const int nf = n0 + pg;
+  const int cnt = nf < n1 ? (n1 - nf + G - 1) / G : 0;
+  int il = 0;
+  auto base_of = [&](int k) -> int {  // k: the load cursor (ascending)
+    if ((k & 63) == 0) il = k + lane < cnt ? lst[nf + G * (k + lane)] : 0;
+    return __builtin_amdgcn_readlane(il, k & 63);
+  };
+#pragma unroll
+  for (int u = 0; u < PD - 1; ++u)
+    if (u < cnt) load(base_of(u), buf[u]);
+  for (int k0 = 0; k0 < cnt; k0 += PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int k = k0 + u;
+      if (k < cnt) {  // wave-uniform
+        if (k + PD - 1 < cnt) load(base_of(k + PD - 1), buf[(u + PD - 1) % PD]);
+        compute(buf[u]);
+      }
+    }
+  }
+  // the pair groups' sums into the block's LDS record in group order, then su_output
+  for (int g = 0; g < G; ++g) {
+    if (pg == g) {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+        const int f = 16 * (tg + TG * t) + cl;
+        if (tg + TG * t < ntile && f < NU)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int s2 = kl + 4 * v;
+            if (s2 < S) {
+              double *r = red + (size_t)s2 * NU + f;
+              *r = g == 0 ? acc[t][v] : *r + acc[t][v];
+            }
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < NXR; ++r) {
+        const int x = lane + 64 * (tg + TG * r);
+        if (x < NX) {
+          double *o = red + (size_t)S * NU + x;
+          *o = g == 0 ? ax[r] : *o + ax[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  su_output(p, red, zs, c, nch, j, tid);
+}
+
 // stats_list_g_kernel<LG, SM>: stats_list_u_kernel for small moment vectors
 // (NU <= LG <= 32, e.g. d = 2 diag: NU = 5): a wavefront is 64 / LG lane groups, each
 // taking its own pair (group g of wave w: pairs w G + g, + 4 G, ...), so a pair
@@ -1254,6 +1441,58 @@ static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st
   return hipGetLastError();
 }
 
+template <int NTW, int G, int KSM, int NXR>
+static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double);
+  const char *ep = std::getenv("VBHEM_SM_PD");  // A/B: prefetch ring depth
+  const int pd = ep ? std::atoi(ep) : 2;
+  auto *fn = pd >= 4 ? &stats_list_m_kernel<NTW, G, KSM, NXR, 4> : &stats_list_m_kernel<NTW, G, KSM, NXR, 2>;
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
+  if (e != hipSuccess) return e;
+  // one generation of resident blocks (the kernel is latency-bound: a second round of
+  // blocks repeats every block's start-up chain; C4: 1024 blocks 0.177 ms per step of
+  // statistics, 2048 0.211, 4096 0.188 at the ring depth 2), at least one per cluster,
+  // at most the slab count per cluster (grid.x is the cap from launch_stats_list)
+  long long nb = (long long)resident_per_cu(reinterpret_cast<const void *>(fn), 64 * kSmWaves, lds) *
+                 device_cus();
+  if (const char *ev = std::getenv("VBHEM_SU_BLOCKS")) nb = std::atoll(ev);  // A/B
+  nb = std::min<long long>(std::max<long long>(nb, a.K + 1), grid.x);
+  hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(64 * kSmWaves), lds, st, a);
+  return hipGetLastError();
+}
+
+// the sum_nu_1 | sum_xi chunks per wave: ceil(ceil((S + S^2) / 64) / tile groups)
+template <int NTW, int G, int KSM>
+static hipError_t launch_sm_x(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  constexpr int TG = kSmWaves / G;
+  const int nxr = ((a.S + a.S * a.S + 63) / 64 + TG - 1) / TG;
+  if (nxr <= 1) return launch_sm<NTW, G, KSM, 1>(a, grid, st);
+  if (nxr <= 2) return launch_sm<NTW, G, KSM, 2>(a, grid, st);
+  if (nxr <= 3) return launch_sm<NTW, G, KSM, 3>(a, grid, st);
+  return launch_sm<NTW, G, KSM, 5>(a, grid, st);
+}
+
+// stats_list_m_kernel's variant: 4 pair groups (every wave all feature tiles) up to 4
+// tiles (NU <= 64), 2 groups up to 8 tiles, else one group of 4 tile groups
+template <int KSM>
+static hipError_t launch_sm_k(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  const int nt = us_nup(a.NU) / 16;
+  if (const char *eg = std::getenv("VBHEM_SM_G")) {  // A/B: fewer pair groups up to 4 tiles
+    const int g = std::atoi(eg);
+    if (nt <= 4 && g == 1) return launch_sm_x<1, 1, KSM>(a, grid, st);
+    if (nt <= 4 && g == 2) return launch_sm_x<2, 2, KSM>(a, grid, st);
+  }
+  switch (nt) {
+    case 1: return launch_sm_x<1, 4, KSM>(a, grid, st);
+    case 2: return launch_sm_x<2, 4, KSM>(a, grid, st);
+    case 3: return launch_sm_x<3, 4, KSM>(a, grid, st);
+    case 4: return launch_sm_x<4, 4, KSM>(a, grid, st);
+    case 5: case 6: return launch_sm_x<3, 2, KSM>(a, grid, st);
+    case 7: case 8: return launch_sm_x<4, 2, KSM>(a, grid, st);
+    default: return launch_sm_x<3, 1, KSM>(a, grid, st);
+  }
+}
+
 template <int LG, int SM>
 static hipError_t launch_sg(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
   const int OT = a.S * a.SB, KP = a.ukdp + 1;
@@ -1295,28 +1534,41 @@ static hipError_t launch_su_s(const StatsArgs &a, const dim3 &grid, hipStream_t 
 hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st) {
   const int NO = a.S + a.S * a.S + a.S * a.NU;
   const dim3 grid(nchunk, a.K);
-  // on the prepared operand when the call has one (S <= 16: the split kernel's range)
-  // (NU > 64, e.g. d = 16 full at C5: the covariance gather of stats_list_kernel
-  // measured 2 % faster, 1.74 vs 1.78 ms per 100 k-base step; VBHEM_STATS_U=1 forces it)
+  const bool no_u = std::getenv("VBHEM_NO_STATS_U") != nullptr;
+  // blocks of the list kernels on the prepared operand: the per-block cost (wave
+  // reduction, slab writes) grows with the output count NO: at most ~4M block outputs
+  // per launch (C4: 512 x 16 blocks of 432, C5: 64 x 32 of 1992 -- measured: 16384
+  // blocks of 1992 ran 1.3x slower than 2048), and at most 4096 blocks in all (C4: 256
+  // parts per cluster instead of 512, statistics 0.245 -> 0.231 ms; 3072 blocks 0.243,
+  // 6144 0.235)
+  const long long NOb = (long long)a.S + (long long)a.S * a.S + (long long)a.S * a.NU;
+  long long cap = (4ll << 20) / (NOb * std::max(1, a.K));
+  cap = std::min<long long>(cap, 4096 / std::max(1, a.K));
+  if (const char *ev = std::getenv("VBHEM_SU_BLOCKS"))  // A/B
+    cap = std::atoi(ev) / std::max(1, a.K);
+  const int nb = (int)std::max(1ll, std::min((long long)nchunk, cap));
+  const dim3 g2(nb, a.K);
+  StatsArgs b = a;
+  b.nzero = nchunk;
+  const int lg = a.U ? sg_lanes(a) : 0;
+  // the MFMA kernel on the statistics copy Us (prepared base sets; S <= 16 rows of one
+  // MFMA tile, SB <= 16, at most 12 feature tiles over 4 waves); the grouped kernel
+  // keeps the small moment vectors (NU <= 32) unless VBHEM_STATS_M=1
+  if (a.Us && !no_u && a.S <= 16 && a.SB <= 16 && us_nup(a.NU) <= 12 * 16 &&
+      !std::getenv("VBHEM_NO_STATS_M") && (lg == 0 || std::getenv("VBHEM_STATS_M"))) {
+    // one 1-D grid over all clusters' gated pairs (balanced parts; the block maps
+    // itself to (cluster, part)); slabs: b.nzero = nchunk; g1.x = the block cap
+    const dim3 g1((unsigned)std::min<long long>((long long)nchunk * a.K, 1ll << 30));
+    return us_sbp(a.SB) <= 8 ? launch_sm_k<2>(b, g1, st) : launch_sm_k<4>(b, g1, st);
+  }
+  // on the prepared operand's tile layout when the call has one (S <= 16: the split
+  // kernel's range) (NU > 64, e.g. d = 16 full at C5: the covariance gather of
+  // stats_list_kernel measured 2 % faster, 1.74 vs 1.78 ms per 100 k-base step;
+  // VBHEM_STATS_U=1 forces it)
   const bool su = a.NU <= 64 || std::getenv("VBHEM_STATS_U");
-  if (a.U && su && a.S <= 16 && a.SB <= a.S && a.NU <= 3 * 64 && !std::getenv("VBHEM_NO_STATS_U")) {
-    StatsArgs b = a;
-    b.nzero = nchunk;
-    // the per-block cost (wave reduction, slab writes) grows with the output count NO:
-    // at most ~4M block outputs per launch (C4: 512 x 16 blocks of 432, C5: 64 x 32 of
-    // 1992 -- measured: 16384 blocks of 1992 ran 1.3x slower than 2048)
-    const long long NOb = (long long)a.S + (long long)a.S * a.S + (long long)a.S * a.NU;
-    long long cap = (4ll << 20) / (NOb * std::max(1, a.K));
-    // and at most 4096 blocks in all (C4: 256 parts per cluster instead of 512,
-    // statistics 0.245 -> 0.231 ms; 3072 blocks 0.243, 6144 0.235)
-    cap = std::min<long long>(cap, 4096 / std::max(1, a.K));
-    if (const char *ev = std::getenv("VBHEM_SU_BLOCKS"))  // A/B
-      cap = std::atoi(ev) / std::max(1, a.K);
-    const int nb = (int)std::max(1ll, std::min((long long)nchunk, cap));
-    const dim3 g2(nb, a.K);
+  if (a.U && su && a.S <= 16 && a.SB <= a.S && a.NU <= 3 * 64 && !no_u) {
     // the grouped kernel runs 64 / LG pairs per wave at once: half the blocks (C3,
     // 80 per cluster: statistics 0.047 -> 0.043 ms; with 156 it was 0.057)
-    const int lg = sg_lanes(a);
     const dim3 gg(std::getenv("VBHEM_SU_BLOCKS") ? nb : std::max(1, nb / 2), a.K);
     switch (lg) {
       case 8: return launch_sg_s<8>(b, gg, st);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile bench.py on the GPU box: kernel trace + stats, then separate PMC passes.
-# Usage: scripts/profile.sh TAG [bench args...]
+# Usage: scripts/profile.sh TAG [bench args...]   (PASSES=trace: the kernel trace only)
 set -o pipefail
 TAG=${1:-run}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -13,7 +13,8 @@ run() {  # name, extra rocprof args
   timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline $ARGS > $OUT/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc"; return $rc
 }
-run trace --kernel-trace --stats &&
+run trace --kernel-trace --stats || exit $?
+[ "$PASSES" = trace ] && exit 0
 run pmc1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE &&
 run pmc2 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_WAIT_INST_LDS &&
 run pmc3 --pmc FETCH_SIZE &&

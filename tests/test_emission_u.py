@@ -29,6 +29,8 @@ SHAPES = {
     "full_d8_rows": (12, 20, 8, 6, 8, 1, {}),      # K*S = 160 > 128: two W' chunks
     "full_d16": (6, 8, 12, 12, 16, 1, dict(tau=6)),  # k-steps 38 (C5 shape), 12 row chunks
     "diag_d12": (10, 6, 5, 4, 12, 0, {}),          # k-steps 6
+    # statistics only: > 64 gated pairs per cluster (one block per cluster walks them)
+    "full_d4_long": (300, 3, 4, 4, 4, 1, {}),
 }
 
 
@@ -102,16 +104,31 @@ def test_prepared_operand_layout(vb):
     kq = (4 * 5 // 2 + 4 + 3) // 4
     ncols = 7 * 3
     ntile = (ncols + 15) // 16
-    assert U.size == 64 + ntile * kq * 64
+    nu = 1 + 4 + 4 * 5 // 2        # statistic features: 1 | mu' | packed Sigma + mu'mu'
+    sbp, nup = 4, 16               # Us block per base: [SB -> 4][NU -> 16]
+    nt = 64 + ntile * kq * 64
+    assert U.size == nt + 7 * sbp * nup
     assert int(eng.lib.vbhem_prepare_base_bytes(ctypes.byref(eng._bt))) == U.size * 8
     # columns past the end of the base set are zero in every k-step
-    tiles = U[64:].reshape(ntile, kq, 4, 16)
+    tiles = U[64:nt].reshape(ntile, kq, 4, 16)
     last = ncols - 16 * (ntile - 1)
     assert np.all(tiles[-1, :, :, last:] == 0.0)
+    # the statistics copy: per base state the ones column, mu' = mu - z, and the packed
+    # second moments as in U's k-steps; zero rows / columns past SB and NU
+    Us = U[nt:].reshape(7, sbp, nup)
+    z = U[:4]
+    assert np.all(Us[:, 3:, :] == 0.0) and np.all(Us[:, :, nu:] == 0.0)
+    assert np.all(Us[:, :3, 0] == 1.0)
+    mu = b["centres"] - z                       # [N][SB][d]
+    np.testing.assert_allclose(Us[:, :3, 1:5], mu, rtol=0, atol=1e-12)
+    ut = tiles.transpose(0, 3, 1, 2).reshape(ntile * 16, kq * 4)[:ncols]   # [col][e]
+    npf = 10
+    np.testing.assert_array_equal(Us[:, :3, 5:nu].reshape(ncols, npf), ut[:, :npf])
+    np.testing.assert_array_equal(Us[:, :3, 1:5].reshape(ncols, 4), ut[:, npf:npf + 4])
     del _capi
 
 
-@pytest.mark.parametrize("name", ["full_d8", "full_d16", "diag_d12", "full_d2_face"])
+@pytest.mark.parametrize("name", ["full_d8", "full_d16", "diag_d12", "full_d2_face", "full_d4_long"])
 @pytest.mark.parametrize("prepare", [True, False])
 def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     """Gated statistics from the prepared operand (stats_list_u_kernel, and
@@ -130,10 +147,15 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     # covariance path (NU > 64)
     # VBHEM_NO_STATS_G=1: the one-pair-per-wave kernel where the grouped one (small NU)
     # is the default
-    for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1"},
-                {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K)},
-                {"VBHEM_STATS_U": "1", "VBHEM_NO_STATS_G": "1"}):
-        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U", "VBHEM_NO_STATS_G"):
+    # VBHEM_STATS_M=1: the MFMA kernel on the statistics copy Us where the default picks
+    # the grouped kernel (small NU); VBHEM_NO_STATS_M=1: the older prepared-operand kernels
+    no_m = {"VBHEM_NO_STATS_M": "1"}
+    for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1", **no_m},
+                {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K), **no_m},
+                {"VBHEM_STATS_U": "1", "VBHEM_NO_STATS_G": "1", **no_m},
+                {}, {"VBHEM_STATS_M": "1"}, {"VBHEM_STATS_M": "1", "VBHEM_SU_BLOCKS": str(K)}):
+        for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U", "VBHEM_NO_STATS_G",
+                  "VBHEM_NO_STATS_M", "VBHEM_STATS_M"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
