@@ -781,6 +781,10 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   // gated schedule its kernels write (not add to) every entry of slabs [0, nslab_used)
   auto chunks = [&w](int nb) { return std::min(w.nslab, (nb + kChunkMinBases - 1) / kChunkMinBases); };
   const int nslab_used = std::max(1, chunks(std::min(base->N, w.group)));
+  // the MFMA statistics kernel: at most 128 parts per cluster (stats_final_kernel then
+  // sums 128 slabs of the N1 / M / U columns instead of every chunk's: C4 28 -> 7 MB)
+  sa.nzero_m = std::min(nslab_used, 128);
+  int stats_slabs = nslab_used;
   hipError_t e = hipSuccess;
   if (!gated || base->N == 0) {
     e = hipMemsetAsync(w.slabs, 0, sizeof(double) * (size_t)nslab_used * w.slab_len, st);
@@ -827,15 +831,18 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
                        w.group, w.flags, w.scratch, LL_elbo_dev, st);
       if (rc != VBHEM_OK) return rc;
       ev0 = timing_on(st) ? timing_event(st) : nullptr;
-      e = vbhem::launch_stats_list(sa, nchunk, sl_lds, st);
+      int ss = nchunk;
+      e = vbhem::launch_stats_list(sa, nchunk, sl_lds, st, &ss);
       if (e != hipSuccess) return hip_fail(e, "stats_list_kernel");
+      if (g0 == 0) stats_slabs = ss;  // later groups add into [0, ss) with ss <= this
     } else {
       e = vbhem::launch_stats(sa, nchunk, ngroups, slds, st);
       if (e != hipSuccess) return hip_fail(e, "stats_kernel");
     }
     if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
-  e = vbhem::launch_stats_final(w.slabs, nslab_used, w.slab_len, stats_dev, st);
+  e = vbhem::launch_stats_final(w.slabs, nslab_used, stats_slabs, w.slab_len, sa.KT, S, sa.SL,
+                                stats_dev, st);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
   return VBHEM_OK;
 }

@@ -122,6 +122,7 @@ struct StatsArgs {
   int ukdp;              // k-extent of U (multiple of 4)
   int nzero;             // stats_list_u_kernel with assign: slabs [gridDim.x, nzero) get zeros
   const double *Us;      // the statistics copy of the prepared operand (us_doubles), or null
+  int nzero_m;           // stats_list_m_kernel: at most this many parts (slabs) per cluster (0: nzero)
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).
@@ -287,8 +288,13 @@ bool plan_stats_list(StatsArgs &a, size_t &lds);
 hipError_t launch_gate_list(const StatsArgs &a, int nchunk, hipStream_t st);
 size_t gate_list_lds(int K);  // dynamic LDS of gate_list_kernel for K clusters
 size_t resp_lds(int K, int KT);  // dynamic LDS of resp_kernel / resp_trials_kernel
-hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st);
-hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
-                              hipStream_t st);
+// *stats_slabs (optional): the slabs [0, n) holding this launch's N1 / M / U entries
+hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st,
+                             int *stats_slabs = nullptr);
+// sums slabs [0, nslab) of the Nj / Lt1 / Lt7 columns (resp_kernel's per-chunk partials)
+// and slabs [0, nslab_stats) of the N1 / M / U columns (KT clusters x S states per
+// section of SL doubles)
+hipError_t launch_stats_final(const double *slabs, int nslab, int nslab_stats, int slab_len, int KT,
+                              int S, int SL, double *out, hipStream_t st);
 
 }  // namespace vbhem

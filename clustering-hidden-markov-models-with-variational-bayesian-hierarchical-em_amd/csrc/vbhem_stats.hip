@@ -752,11 +752,16 @@ __global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
 // partials are added in fixed order -- deterministic; ~slab_len/16 blocks (C4:
 // 506) keep every CU's loads in flight (32-column blocks left it latency-bound).
 constexpr int kFinalCols = 16, kFinalParts = 16;
-__global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab,
-                                                          int slab_len, double *out) {
+__global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab_all,
+                                                          int nslab_stats, int slab_len, int KT,
+                                                          int S, int SL, double *out) {
   __shared__ double part[kFinalParts][kFinalCols];
   const int c = threadIdx.x % kFinalCols, pp = threadIdx.x / kFinalCols;
   const int x = blockIdx.x * kFinalCols + c;
+  // resp_kernel's columns (Nj, Lt1, Lt7) have a partial in every chunk's slab; the
+  // gated statistics' only in their kernel's parts
+  const int xs = x % SL, lt = KT * (1 + S + S * S);
+  const int nslab = (xs < KT || (xs >= lt && xs < lt + 2)) ? nslab_all : nslab_stats;
   double acc = 0.0;
   if (x < slab_len) {
     int k = pp;
@@ -1531,7 +1536,9 @@ static hipError_t launch_su_s(const StatsArgs &a, const dim3 &grid, hipStream_t 
   return launch_su<FPL, 16>(a, grid, st);
 }
 
-hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st) {
+hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st,
+                             int *stats_slabs) {
+  if (stats_slabs) *stats_slabs = nchunk;
   const int NO = a.S + a.S * a.S + a.S * a.NU;
   const dim3 grid(nchunk, a.K);
   const bool no_u = std::getenv("VBHEM_NO_STATS_U") != nullptr;
@@ -1552,12 +1559,15 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   b.nzero = nchunk;
   const int lg = a.U ? sg_lanes(a) : 0;
   // the MFMA kernel on the statistics copy Us (prepared base sets; S <= 16 rows of one
-  // MFMA tile, SB <= 16, at most 12 feature tiles over 4 waves); the grouped kernel
-  // keeps the small moment vectors (NU <= 32) unless VBHEM_STATS_M=1
+  // MFMA tile, SB <= 16, at most 12 feature tiles over 4 waves); also for the small
+  // moment vectors of the grouped kernel (C3: statistics 0.039 -> 0.032 ms per step)
   if (a.Us && !no_u && a.S <= 16 && a.SB <= 16 && us_nup(a.NU) <= 12 * 16 &&
-      !std::getenv("VBHEM_NO_STATS_M") && (lg == 0 || std::getenv("VBHEM_STATS_M"))) {
+      !std::getenv("VBHEM_NO_STATS_M")) {
     // one 1-D grid over all clusters' gated pairs (balanced parts; the block maps
-    // itself to (cluster, part)); slabs: b.nzero = nchunk; g1.x = the block cap
+    // itself to (cluster, part)); at most nzero_m parts per cluster, so the slabs past
+    // them hold none of its N1 / M / U entries (stats_final_kernel reads only those)
+    if (a.nzero_m > 0) b.nzero = std::min(a.nzero_m, nchunk);
+    if (stats_slabs) *stats_slabs = b.nzero;
     const dim3 g1((unsigned)std::min<long long>((long long)nchunk * a.K, 1ll << 30));
     return us_sbp(a.SB) <= 8 ? launch_sm_k<2>(b, g1, st) : launch_sm_k<4>(b, g1, st);
   }
@@ -1590,10 +1600,11 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   return hipGetLastError();
 }
 
-hipError_t launch_stats_final(const double *slabs, int nslab, int slab_len, double *out,
-                              hipStream_t st) {
+hipError_t launch_stats_final(const double *slabs, int nslab, int nslab_stats, int slab_len, int KT,
+                              int S, int SL, double *out, hipStream_t st) {
+  if (nslab_stats < 1 || nslab_stats > nslab || SL < 1 || slab_len % SL != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + kFinalCols - 1) / kFinalCols), dim3(256),
-                     0, st, slabs, nslab, slab_len, out);
+                     0, st, slabs, nslab, nslab_stats, slab_len, KT, S, SL, out);
   return hipGetLastError();
 }
 

@@ -147,15 +147,16 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     # covariance path (NU > 64)
     # VBHEM_NO_STATS_G=1: the one-pair-per-wave kernel where the grouped one (small NU)
     # is the default
-    # VBHEM_STATS_M=1: the MFMA kernel on the statistics copy Us where the default picks
-    # the grouped kernel (small NU); VBHEM_NO_STATS_M=1: the older prepared-operand kernels
+    # default (prepared): the MFMA kernel on the statistics copy Us, also with one block
+    # per cluster (> 64 pairs per wave: the list-base refetch); VBHEM_NO_STATS_M=1: the
+    # older prepared-operand kernels
     no_m = {"VBHEM_NO_STATS_M": "1"}
     for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1", **no_m},
                 {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K), **no_m},
                 {"VBHEM_STATS_U": "1", "VBHEM_NO_STATS_G": "1", **no_m},
-                {}, {"VBHEM_STATS_M": "1"}, {"VBHEM_STATS_M": "1", "VBHEM_SU_BLOCKS": str(K)}):
+                {}, {"VBHEM_SU_BLOCKS": str(K + 1)}, {"VBHEM_SM_PD": "4"}):
         for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U", "VBHEM_NO_STATS_G",
-                  "VBHEM_NO_STATS_M", "VBHEM_STATS_M"):
+                  "VBHEM_NO_STATS_M", "VBHEM_SM_PD"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
