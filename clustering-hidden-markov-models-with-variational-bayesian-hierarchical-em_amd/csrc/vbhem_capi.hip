@@ -355,7 +355,9 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   if (const char *ev = std::getenv("VBHEM_NSLAB")) maxslab = std::max(1, std::min(8192, std::atoi(ev)));
   w.nslab = std::min<int>(w.group, maxslab);
   w.slab_len = R * (int)vbhem_stats_len(K / R, S, b->d, b->covmode);
-  w.flags = cv.take<int>(vbhem::kFlagHead + g * K);
+  // flagged-pair list: with the fallback folded into the consumers the backward pass's
+  // entries stay while the gate-list pass appends its own (at most g K + g K)
+  w.flags = cv.take<int>(vbhem::kFlagHead + 2 * g * K);
   w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   w.nu1 = cv.take<double>(g * K * S);
   w.xi = cv.take<double>(g * K * S * S);
@@ -460,7 +462,7 @@ unsigned list_grid(const vbhem::SplitArgs &a, size_t lds) {
 int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1, double *xi,
                 double *tnu, const double *Ebuf, long long e_ld, const int *list,
                 const int *list_tot, int list_cap, int *flags, double *scratch, double *LL,
-                hipStream_t st) {
+                hipStream_t st, bool fold = false) {
   if (i_end <= i_begin) return VBHEM_OK;
   // flags[0] is zero here: the backward pass's fb_exact_kernel reset it
   if (!c.split.lds_l) return fail(VBHEM_ERR_UNSUPPORTED, "gate-list pass does not fit LDS");
@@ -475,6 +477,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   hipError_t e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_l), c.split.lds_l, st);
   if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
   if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
+  if (fold) return VBHEM_OK;  // the statistics kernel takes the flagged pairs (StatsArgs::fold)
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin; a.i_end = i_end; a.i_buf0 = i_buf0;
   a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
@@ -489,7 +492,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
 // output from the exact kernel.
 int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, double *nu1,
            double *xi, double *tnu, double *Ebuf, long long e_ld, int *flags, double *scratch,
-           hipStream_t st, int mode = vbhem::kFbDense) {
+           hipStream_t st, int mode = vbhem::kFbDense, vbhem::FbArgs *fold = nullptr) {
   if (i_end <= i_begin) return VBHEM_OK;
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin;
@@ -571,6 +574,10 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   if (ev0) {
     g_timing.fb.emplace_back(ev0, timing_event(st));
     g_timing.fb_pairs.push_back((long long)(i_end - i_begin) * a.K);
+  }
+  if (fold) {  // resp_kernel takes the flagged pairs (StatsArgs::fold): no exact launch
+    *fold = a;
+    return VBHEM_OK;
   }
   e = vbhem::launch_fb_exact(a, scratch, exact_stride(a.S, a.SB, a.T), kExactThreads, st);
   if (e != hipSuccess) return hip_fail(e, "fb_exact_kernel");
@@ -799,12 +806,25 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
                          gated ? w.Atg : nullptr,
                          clus->logA);
   if (rc != VBHEM_OK) return rc;
+  // the exact fallback folded into resp_kernel and the statistics kernel (one base
+  // group, one trial: two fb_exact_kernel launches less per E-step)
+  // (the statistics kernel needs a block, and so a scratch slot, per cluster: K below
+  // the slot count)
+  const bool fold = gated && R == 1 && base->N <= w.group && ctx.split.ok && K < kExactThreads &&
+                    !std::getenv("VBHEM_NO_FOLD_EXACT");
+  sa.fold = 0;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);
     const long long e_ld = (long long)w.group * SB;
     rc = run_fb(ctx, g0, g1, g0, LL_elbo_dev, w.nu1, w.xi, w.tnu, w.E, e_ld, w.flags, w.scratch,
-                st, gated ? vbhem::kFbBackward : vbhem::kFbDense);
+                st, gated ? vbhem::kFbBackward : vbhem::kFbDense, fold ? &sa.fx : nullptr);
     if (rc != VBHEM_OK) return rc;
+    if (fold) {
+      sa.fold = 1;
+      sa.xscratch = w.scratch;
+      sa.xstride = (long long)exact_stride(S, SB, T);
+      sa.xslots = kExactThreads;
+    }
     sa.i_begin = g0; sa.i_end = g1; sa.i_buf0 = g0;
     sa.assign = gated && g0 == 0;
     // the emission GEMM's operand for this group (prepared, or built by run_fb)
@@ -828,7 +848,7 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
       if (e != hipSuccess) return hip_fail(e, "gate_list_kernel");
       if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
       rc = run_fb_list(ctx, g0, g1, g0, w.nu1, w.xi, w.tnu, w.E, e_ld, w.list, w.list_tot,
-                       w.group, w.flags, w.scratch, LL_elbo_dev, st);
+                       w.group, w.flags, w.scratch, LL_elbo_dev, st, fold);
       if (rc != VBHEM_OK) return rc;
       ev0 = timing_on(st) ? timing_event(st) : nullptr;
       int ss = nchunk;

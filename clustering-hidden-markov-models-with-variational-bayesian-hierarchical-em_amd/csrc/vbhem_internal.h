@@ -123,6 +123,14 @@ struct StatsArgs {
   int nzero;             // stats_list_u_kernel with assign: slabs [gridDim.x, nzero) get zeros
   const double *Us;      // the statistics copy of the prepared operand (us_doubles), or null
   int nzero_m;           // stats_list_m_kernel: at most this many parts (slabs) per cluster (0: nzero)
+  // the exact fallback folded into resp_kernel (the backward pass's flagged pairs of each
+  // block's bases) and stats_list_m_kernel (the gate-list pass's flagged pairs of each
+  // block's part) instead of two fb_exact_kernel launches (fold = 1; one base group)
+  int fold;
+  FbArgs fx;                 // the exact recursion's arguments (outputs, flag counter / list)
+  double *xscratch;          // its scratch: xslots slots of xstride doubles
+  long long xstride;
+  int xslots;
 };
 
 // fb_split_kernel (one base-state column per LPC lanes; S <= kSplitMaxS, SB <= S).
@@ -274,7 +282,10 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 // inputs; pairs whose cluster constants or emissions are not finite (a diverged
 // EM trial) are not flagged: their L_elbo is written as NaN, as the reference's
 // arithmetic would produce, and they cost the fallback nothing.
-constexpr int kFlagHead = 3;
+//   [3] the first entry of the gate-list pass (written by resp_kernel when the fallback
+//       is folded into the consumers: resp_kernel takes [0, [3]), stats_list_m_kernel
+//       the rest)
+constexpr int kFlagHead = 4;
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
 constexpr int kExactBlock = 256;   // fb_exact_kernel: threads per block
 constexpr int kExactBlocks = 8;    // fb_exact_kernel: blocks (grid-stride over the list)

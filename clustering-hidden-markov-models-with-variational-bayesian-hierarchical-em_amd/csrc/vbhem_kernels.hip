@@ -32,6 +32,7 @@
 #include <cstdint>
 
 #include "vbhem_internal.h"
+#include "vbhem_exact.h"
 
 namespace vbhem {
 
@@ -380,112 +381,8 @@ __global__ __launch_bounds__(kExactBlock) void fb_exact_kernel(const FbArgs p, d
   // nothing flagged (the usual case): every block reads 0 -- nobody writes the
   // counter while it is 0 -- so all leave at once, with no reset to do
   if (cnt == 0) return;
-  const int S = p.S, SB = p.SB, d = p.d, T = p.T;
   double *w = scratch + (size_t)gt * scratch_stride;
-  double *E = w, *L = E + S * SB, *Ln = L + S * SB, *lt = Ln + S * SB, *nu = lt + S * SB,
-         *tn = nu + S * SB, *ls = tn + S * SB, *Th = ls + SB;  // Th [T][S][S][SB]
-  for (int idx = gt; idx < cnt; idx += nt) {
-    const int pair = p.flag_list[idx];
-    const int i = pair / p.K, j = pair - (pair / p.K) * p.K;
-    const size_t lp = (size_t)(i - p.i_buf0) * p.K + j;
-    const double *Ab = p.A + (size_t)i * SB * SB;
-    const double *pb = p.prior + (size_t)i * SB;
-    const double *la = p.logA + (size_t)j * S * S;
-    const double *lpj = p.logPi + (size_t)j * S;
-    for (int s = 0; s < S; ++s)
-      for (int be = 0; be < SB; ++be) {
-        const double *mm = p.m + ((size_t)j * S + s) * d;
-        const double *mu = p.centres + ((size_t)i * SB + be) * d;
-        double ell = d * kLog2Pi + p.c[(size_t)j * S + s];
-        if (p.covmode == kCovFull) {
-          const double *P = p.P + ((size_t)j * S + s) * d * d;
-          const double *C = p.covars + ((size_t)i * SB + be) * d * d;
-          for (int k = 0; k < d * d; ++k) ell += P[k] * C[k];
-          for (int c2 = 0; c2 < d; ++c2) {
-            double col = 0.0;
-            for (int r = 0; r < d; ++r) col += (mu[r] - mm[r]) * P[r * d + c2];
-            ell += col * (mu[c2] - mm[c2]);
-          }
-        } else {
-          const double *P = p.P + ((size_t)j * S + s) * d;
-          const double *C = p.covars + ((size_t)i * SB + be) * d;
-          for (int r = 0; r < d; ++r) {
-            const double x = mu[r] - mm[r];
-            ell += P[r] * C[r];
-            ell += P[r] * (x * x);
-          }
-        }
-        E[s * SB + be] = p.smooth != 1.0 ? (-0.5 * ell) / p.smooth : -0.5 * ell;
-        L[s * SB + be] = 0.0;
-      }
-    for (int t = T - 1; t >= 1; --t) {
-      for (int rho = 0; rho < S; ++rho) {
-        for (int s = 0; s < S; ++s)
-          for (int be = 0; be < SB; ++be) lt[s * SB + be] = la[rho * S + s] + E[s * SB + be] + L[s * SB + be];
-        for (int be = 0; be < SB; ++be) {
-          double mv = lt[be];
-          for (int s = 1; s < S; ++s) mv = fmax(mv, lt[s * SB + be]);
-          double acc = 0.0;
-          for (int s = 0; s < S; ++s) acc += exp(lt[s * SB + be] - mv);
-          ls[be] = mv + log(acc);
-          for (int s = 0; s < S; ++s)
-            Th[(((size_t)t * S + rho) * S + s) * SB + be] = exp(lt[s * SB + be] - ls[be]);
-        }
-        for (int g = 0; g < SB; ++g) {
-          double acc = 0.0;
-          for (int be = 0; be < SB; ++be) acc += Ab[g * SB + be] * ls[be];
-          Ln[rho * SB + g] = acc;
-        }
-      }
-      for (int k = 0; k < S * SB; ++k) L[k] = Ln[k];
-    }
-    double LLv = 0.0;
-    for (int s = 0; s < S; ++s)
-      for (int be = 0; be < SB; ++be) lt[s * SB + be] = lpj[s] + E[s * SB + be] + L[s * SB + be];
-    for (int be = 0; be < SB; ++be) {
-      double mv = lt[be];
-      for (int s = 1; s < S; ++s) mv = fmax(mv, lt[s * SB + be]);
-      double acc = 0.0;
-      for (int s = 0; s < S; ++s) acc += exp(lt[s * SB + be] - mv);
-      const double l1 = mv + log(acc);
-      LLv += pb[be] * l1;
-      for (int s = 0; s < S; ++s) nu[s * SB + be] = pb[be] * exp(lt[s * SB + be] - l1);
-    }
-    p.LL[pair] = LLv;
-    for (int s = 0; s < S; ++s) {
-      double acc = 0.0;
-      for (int be = 0; be < SB; ++be) acc += nu[s * SB + be];
-      p.nu1[lp * S + s] = acc;
-    }
-    for (int k = 0; k < S * SB; ++k) tn[k] = nu[k];
-    double *xi = p.xi + lp * S * S;
-    for (int k = 0; k < S * S; ++k) xi[k] = 0.0;
-    for (int t = 1; t < T; ++t) {
-      double *foo = Ln;
-      for (int rho = 0; rho < S; ++rho)
-        for (int g = 0; g < SB; ++g) {
-          double acc = 0.0;
-          for (int be = 0; be < SB; ++be) acc += nu[rho * SB + be] * Ab[be * SB + g];
-          foo[rho * SB + g] = acc;
-        }
-      for (int s = 0; s < S; ++s) {
-        for (int rho = 0; rho < S; ++rho) {
-          double acc = 0.0;
-          for (int g = 0; g < SB; ++g)
-            acc += foo[rho * SB + g] * Th[(((size_t)t * S + rho) * S + s) * SB + g];
-          xi[rho * S + s] += acc;
-        }
-        for (int g = 0; g < SB; ++g) {
-          double acc = 0.0;
-          for (int rho = 0; rho < S; ++rho)
-            acc += foo[rho * SB + g] * Th[(((size_t)t * S + rho) * S + s) * SB + g];
-          nu[s * SB + g] = acc;
-        }
-      }
-      for (int k = 0; k < S * SB; ++k) tn[k] += nu[k];
-    }
-    for (int k = 0; k < S * SB; ++k) p.tnu[lp * S * SB + k] = tn[k];
-  }
+  for (int idx = gt; idx < cnt; idx += nt) exact_pair(p, p.flag_list[idx], w);
   __syncthreads();  // every thread of this block has read the count
   if (threadIdx.x == 0) {
     const int done = atomicAdd(p.flag_count + 2, 1);

@@ -32,6 +32,7 @@
 #include <cstdlib>
 
 #include "vbhem_internal.h"
+#include "vbhem_exact.h"
 
 namespace vbhem {
 
@@ -97,9 +98,24 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   int *gcnt = reinterpret_cast<int *>(accLt + 2 * NW);  // [K] gated pairs of this chunk
   for (int x = tid; x < NW * BPW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
   for (int x = tid; x < K; x += kRespThreads) gcnt[x] = 0;
-  __syncthreads();
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
+  if (p.fold && tid == 0) {
+    // the folded fallback (vbhem_internal.h, kFlagHead): the backward pass's flagged
+    // pairs of this block's bases get their exact L_elbo (and other outputs) before any
+    // of them is read; block 0 records where the gate-list pass's entries will start
+    int *fc = p.fx.flag_count;
+    const int cnt = __atomic_load_n(fc, __ATOMIC_RELAXED);
+    if (blockIdx.x == 0) fc[3] = cnt;
+    if (cnt > 0) {
+      double *w = p.xscratch + (size_t)(blockIdx.x % p.xslots) * p.xstride;
+      for (int x = 0; x < cnt; ++x) {
+        const int pair = p.fx.flag_list[x], i = pair / K;
+        if (i >= b0 && i < b1) exact_pair(p.fx, pair, w);
+      }
+    }
+  }
+  __syncthreads();
   double l1 = 0.0, l7 = 0.0;
   if (K <= G) {
     // one cluster per lane: the next base's tilde_N and L_elbo are loaded while
@@ -1171,6 +1187,23 @@ __global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const Stats
   const int tot = p.list_tot[j];
   const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
   const int *lst = p.list + (size_t)j * p.list_cap;
+  if (p.fold) {
+    // the folded fallback: the gate-list pass's flagged pairs of this part (cluster j,
+    // bases lst[n0] .. lst[n1 - 1]) get their exact outputs before they are read
+    const int *fc = p.fx.flag_count;
+    const int c1 = fc[3], cnt = __atomic_load_n(fc, __ATOMIC_RELAXED);
+    if (cnt > c1) {  // block-uniform
+      if (tid == 0 && n0 < n1) {
+        const int ilo = lst[n0], ihi = lst[n1 - 1];
+        double *w = p.xscratch + (size_t)(blockIdx.x % p.xslots) * p.xstride;
+        for (int x = c1; x < cnt; ++x) {
+          const int pair = p.fx.flag_list[x], i = pair / K;
+          if (pair - i * K == j && i >= ilo && i <= ihi) exact_pair(p.fx, pair, w);
+        }
+      }
+      __syncthreads();
+    }
+  }
   // one pair's operands: A values per k-slice, B values per (tile, k-slice), its Z and
   // its sum_nu_1 / sum_xi entries; a ring of PD of them (PD - 1 pairs' loads in flight
   // while a pair's MFMAs run)
@@ -1462,6 +1495,7 @@ static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st
                  device_cus();
   if (const char *ev = std::getenv("VBHEM_SU_BLOCKS")) nb = std::atoll(ev);  // A/B
   nb = std::min<long long>(std::max<long long>(nb, a.K + 1), grid.x);
+  if (a.fold) nb = std::min<long long>(nb, a.xslots);  // one fallback scratch slot per block
   hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(64 * kSmWaves), lds, st, a);
   return hipGetLastError();
 }
@@ -1570,6 +1604,12 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
     if (stats_slabs) *stats_slabs = b.nzero;
     const dim3 g1((unsigned)std::min<long long>((long long)nchunk * a.K, 1ll << 30));
     return us_sbp(a.SB) <= 8 ? launch_sm_k<2>(b, g1, st) : launch_sm_k<4>(b, g1, st);
+  }
+  // the other kernels do not fold the fallback: the exact kernel first (it redoes the
+  // backward pass's entries too, which resp_kernel already fixed: same values)
+  if (a.fold) {
+    hipError_t e = launch_fb_exact(a.fx, a.xscratch, (size_t)a.xstride, kExactBlock * kExactBlocks, st);
+    if (e != hipSuccess) return e;
   }
   // on the prepared operand's tile layout when the call has one (S <= 16: the split
   // kernel's range) (NU > 64, e.g. d = 16 full at C5: the covariance gather of

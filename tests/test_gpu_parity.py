@@ -168,6 +168,36 @@ def test_exact_fallback_fused(vb, vo, fused_mode):
         assert stat_err(got[k], st[k]) < 1e-9, k
 
 
+@pytest.mark.parametrize("N,K", [(4, 1), (300, 2)])
+@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}, {"VBHEM_NO_STATS_M": "1"}])
+def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
+    """The adversarial cluster wins every base (the other cluster's emissions are far
+    worse), so its pairs are flagged by the backward pass AND are gated: the gate-list
+    pass flags them again.  Default: both passes' fallbacks folded into resp_kernel and
+    the MFMA statistics kernel (several resp chunks and statistics parts at N = 300);
+    VBHEM_NO_FOLD_EXACT: two fb_exact_kernel launches; VBHEM_NO_STATS_M: folded into
+    resp_kernel, the exact kernel before the other statistics kernels."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cs, consts = adversarial_case(1, N=N, K=K)
+    if K > 1:
+        consts["c"][1:] = 1.0e4
+    base, T = cs["base"], cs["T"]
+    S, d = consts["logPi"].shape[1], base["centres"].shape[2]
+    pairs = vo.c_estep_pairs(base, consts, T)
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    assert (Z[:, 0] > 1e-8).all()  # the flagged cluster is gated for every base
+    st = vo.c_statistics(Z, pairs, 1)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
+    assert eng.fallback_count() >= 2 * N  # both passes flagged cluster 0 of every base
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, k
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
 def test_host_pointer_entry_point(vb, vo, capi_lib):
     """vbhem_estep_pairs_host (what the MEX gateway calls): host arrays in/out."""
     from vbhem_amd import _capi
