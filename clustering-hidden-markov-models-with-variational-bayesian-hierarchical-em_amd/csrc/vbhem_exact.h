@@ -12,7 +12,7 @@ namespace vbhem {
 
 constexpr double kExactLog2Pi = 1.8378770664093454835606594728112353;  // log(2*pi)
 
-static __device__ __attribute__((noinline)) void exact_pair(const FbArgs &p, int pair, double *w) {
+static __device__ __forceinline__ void exact_pair(const FbArgs &p, int pair, double *w) {
   const int S = p.S, SB = p.SB, d = p.d, T = p.T;
   double *E = w, *L = E + S * SB, *Ln = L + S * SB, *lt = Ln + S * SB, *nu = lt + S * SB,
          *tn = nu + S * SB, *ls = tn + S * SB, *Th = ls + SB;  // Th [T][S][S][SB]

@@ -154,9 +154,9 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1", **no_m},
                 {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K), **no_m},
                 {"VBHEM_STATS_U": "1", "VBHEM_NO_STATS_G": "1", **no_m},
-                {}, {"VBHEM_SU_BLOCKS": str(K + 1)}, {"VBHEM_SM_PD": "4"}):
+                {}, {"VBHEM_SU_BLOCKS": str(K + 1)}, {"VBHEM_SM_G": "1"}):
         for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U", "VBHEM_NO_STATS_G",
-                  "VBHEM_NO_STATS_M", "VBHEM_SM_PD"):
+                  "VBHEM_NO_STATS_M", "VBHEM_SM_G"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
