@@ -338,7 +338,15 @@ def main():
         t_a, n_a = timed(1)
         t_b, n_b = timed(1 + args.em_iters)
         ms = (t_b - t_a) / max(1, n_b - n_a) * 1e3
-        return dict(ms=ms, per_s=1e3 / ms, iterations=n_b - n_a,
+        # the loop's per-iteration math kernel (bound + M-step + next prelude on the
+        # device), timed with events in one more run
+        _capi.timing_read()
+        _capi.timing_enable(True)
+        timed(1 + args.em_iters)
+        _capi.timing_enable(False)
+        tm = _capi.timing_read()
+        math_ms = tm["em_math_ms"] / tm["em_math_launches"] if tm["em_math_launches"] else None
+        return dict(ms=ms, per_s=1e3 / ms, iterations=n_b - n_a, math_kernel_ms=math_ms,
                     method=("(t(run of %d iterations) - t(run of %d)) / %d: the per-run setup "
                             "cancels" % (n_b, n_a, n_b - n_a)))
 
@@ -495,10 +503,14 @@ def main():
         "emission_kernel_ms": tkb["em_ms"] / max(1, tkb["em_launches"]),
         "stats_kernels_ms_per_step": tkb["stats_ms"] / bd_steps,
         "breakdown_steps": bd_steps,
-        "host_mstep_ms": host_ms,
-        "host_mstep_note": ("per-iteration host math of the C++ EM loop "
-                            "(vbhem_em_host_iteration: bound, M-step, next psi prelude), "
-                            "replicated on every rank; host_math_python_ms: the Python path"),
+        "host_mstep_ms": em_it["math_kernel_ms"] if em_it else None,
+        "host_mstep_note": ("the per-iteration math of the EM loop (vbhem_em_run: bound, M-step, "
+                            "next psi prelude) as the loop runs it: one device kernel on the "
+                            "E-step stream, replicated on every rank, HIP-event timed; "
+                            "host_math_cpp_ms: the same math in C++ on the host "
+                            "(vbhem_em_host_iteration, the loop's path for d > 16 or S > 64), "
+                            "host_math_python_ms: the Python path"),
+        "host_math_cpp_ms": host_ms,
         "host_math_python_ms": host_py_ms,
         "em_iteration": em_it,
         "shard_sim": shard_sim,

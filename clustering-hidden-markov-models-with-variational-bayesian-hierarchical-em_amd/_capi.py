@@ -96,6 +96,8 @@ EXPORTS = {
                                             ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_timing_read_gated": (_c_int, [ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_longlong)]),
+    "vbhem_timing_read_em_math": (_c_int, [ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_set_fused_mode": (_c_int, [_c_int]),
     "vbhem_em_prelude": (_c_int, [ctypes.POINTER(PostT), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "vbhem_em_lower_bound": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp, _vp,
@@ -170,9 +172,13 @@ def timing_read() -> dict:
     gf, ng = ctypes.c_double(), ctypes.c_longlong()
     check(lib().vbhem_timing_read_gated(ctypes.byref(gf), ctypes.byref(ng)),
           "vbhem_timing_read_gated")
+    mm, nm = ctypes.c_double(), ctypes.c_longlong()
+    check(lib().vbhem_timing_read_em_math(ctypes.byref(mm), ctypes.byref(nm)),
+          "vbhem_timing_read_em_math")
     return dict(fb_ms=fb.value, fb_launches=nf.value, fb_pairs=npairs.value,
                 stats_ms=st.value, stats_launches=ns.value, em_ms=em.value, em_launches=ne.value,
-                gated_fwd_ms=gf.value, gated_fwd_launches=ng.value)
+                gated_fwd_ms=gf.value, gated_fwd_launches=ng.value, em_math_ms=mm.value,
+                em_math_launches=nm.value)
 
 
 FUSED_GATED, FUSED_DENSE = 0, 1

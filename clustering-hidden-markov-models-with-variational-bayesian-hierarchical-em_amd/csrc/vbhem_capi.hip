@@ -38,7 +38,7 @@ thread_local std::string g_err;
 // are recycled through a per-thread pool (no create/destroy per launch).
 struct TimingState {
   int level = 0;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em, gf;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> fb, stats, em, gf, emd;  // emd: EM-loop math kernel
   std::vector<long long> fb_pairs;
   std::vector<hipEvent_t> pool;
   ~TimingState() {
@@ -80,6 +80,18 @@ hipEvent_t timing_event(hipStream_t st) {
 void timing_recycle(hipEvent_t ev) {
   if (ev) g_timing.pool.push_back(ev);
 }
+
+}  // namespace
+
+// EM-loop math kernel timing (vbhem_em.hip), same events and levels as the E-step's
+namespace vbhem {
+void *timing_begin(hipStream_t st) { return timing_on(st) ? timing_event(st) : nullptr; }
+void timing_end_em_math(void *ev0, hipStream_t st) {
+  if (ev0) g_timing.emd.emplace_back(static_cast<hipEvent_t>(ev0), timing_event(st));
+}
+}  // namespace vbhem
+
+namespace {
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
@@ -384,6 +396,7 @@ struct FbCtx {
   // the backward-only pass on fb_bwd2_kernel (S <= 8): LDS bytes, pairs per block
   size_t bwd2_lds = 0;
   int bwd2_ppb = 0, bwd2_nwb = 0;
+  bool bwd4 = false;  // S = 8, SB <= 8: fb_bwd4_kernel (MFMA contractions) instead
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
   // emission_u_kernel: on the prepared operand (base->U) or one built per call in u_ws
@@ -433,6 +446,7 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
       c.bwd2_nwb = vbhem::bwd2_waves(cl->S);
       c.bwd2_lds = vbhem::bwd2_lds(cl->S, c.bwd2_nwb);
       c.bwd2_ppb = vbhem::bwd2_ppb(cl->S, c.bwd2_nwb);
+      c.bwd4 = vbhem::bwd4_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD4");
     }
   }
   return VBHEM_OK;
@@ -546,7 +560,16 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
     const unsigned ntile = (unsigned)((i_end - i_begin + sp.ppb - 1) / sp.ppb);
     unsigned grid = ntile * (unsigned)ca.K;
-    if (mode == vbhem::kFbBackward && c.bwd2_lds) {
+    if (mode == vbhem::kFbBackward && c.bwd4) {
+      // fb_bwd4_kernel, persistent: NB blocks per cluster (x8 when possible)
+      const int ppb = vbhem::bwd4_ppb();
+      const unsigned nt4 = (unsigned)((i_end - i_begin + ppb - 1) / ppb);
+      const unsigned all = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::bwd4_resident_blocks()));
+      unsigned nb = std::max(1u, std::min(nt4, all / (unsigned)ca.K));
+      if (nb >= 8) nb = nb / 8 * 8;
+      e = vbhem::launch_bwd4(ca, (unsigned)ca.K * nb, st);
+      if (e != hipSuccess) return hip_fail(e, "fb_bwd4_kernel");
+    } else if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
       ca.nwb = c.bwd2_nwb;
       const unsigned nt2 = (unsigned)((i_end - i_begin + c.bwd2_ppb - 1) / c.bwd2_ppb);
@@ -931,6 +954,10 @@ static int drain_events(std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, doubl
   if (ms_out) *ms_out = t;
   if (n_out) *n_out = n;
   return rc;
+}
+
+int vbhem_timing_read_em_math(double *ms, long long *launches) {
+  return drain_events(g_timing.emd, ms, launches, "vbhem_timing_read_em_math");
 }
 
 int vbhem_timing_read_gated(double *fwd_ms, long long *fwd_launches) {

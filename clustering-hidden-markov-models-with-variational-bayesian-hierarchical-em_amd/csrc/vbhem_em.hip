@@ -21,6 +21,7 @@
 
 #include "vbhem_em.h"
 #include "vbhem_em_dev.h"
+#include "vbhem_internal.h"
 
 namespace {
 
@@ -619,7 +620,9 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     set_post(pd[j % 3], pd[(j + 1) % 3]);
     a.seq = j + 1;
     a.flag = reinterpret_cast<int *>(Ld + 2) + (j % 2);
+    void *t0 = vbhem::timing_begin(st);
     e = vbhem::launch_em_dev(a, vbhem::kEmIterate, Ld + (j % 2), st);
+    vbhem::timing_end_em_math(t0, st);
     return e == hipSuccess;
   };
   double lastL = -DBL_MAX, L = -INFINITY;

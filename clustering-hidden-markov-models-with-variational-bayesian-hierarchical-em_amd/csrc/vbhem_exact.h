@@ -88,7 +88,11 @@ static __device__ __forceinline__ void exact_pair(const FbArgs &p, int pair, dou
     p.nu1[lp * S + s] = acc;
   }
   for (int k = 0; k < S * SB; ++k) tn[k] = nu[k];
-  double *xi = p.xi + lp * S * S;
+  // sum_xi accumulates in the thread's own scratch (Theta's slice t = 0, never used
+  // by the recursion) and is stored once at the end: a pair listed twice in one
+  // fallback launch (flagged by both passes) is then two threads storing the same
+  // values, never two threads adding into the same output
+  double *xi = Th;
   for (int k = 0; k < S * S; ++k) xi[k] = 0.0;
   for (int t = 1; t < T; ++t) {
     double *foo = Ln;
@@ -115,6 +119,7 @@ static __device__ __forceinline__ void exact_pair(const FbArgs &p, int pair, dou
     for (int k = 0; k < S * SB; ++k) tn[k] += nu[k];
   }
   for (int k = 0; k < S * SB; ++k) p.tnu[lp * S * SB + k] = tn[k];
+  for (int k = 0; k < S * S; ++k) p.xi[lp * S * S + k] = xi[k];
 }
 
 }  // namespace vbhem

@@ -1,0 +1,432 @@
+// vbhem_fb_bwd4.hip -- the gated schedule's backward-only pass (K2 backward
+// recursion, mex.c:915-1015, and K3 termination, mex.c:1020-1080, writing L_elbo)
+// for S = 8 cluster states and SB <= 8 base states, with both per-step contractions
+// on the fp64 matrix cores (v_mfma_f64_4x4x4f64, 4 blocks of 4x4x4 per instruction).
+//
+// Per pair and step (the factorised recursion of fb_bwd2_kernel):
+//   G  = exp(V - M)            M[b] = column maximum over the cluster states
+//   Z  = A' G                  A' = exp(logA - amax), the cluster's transitions
+//   sv = M + log Z
+//   V  = Ef + sv Ab^T          Ab = the base's transitions, Ef = E + amax rowsum(Ab)
+// A wavefront holds QPW quads of 4 pairs (4 consecutive bases of one cluster); the
+// 4 pairs of a quad are the 4 blocks of every MFMA, so no operand is padded.  With
+//   P layout:  X[i][j] of block (I, J) in lane 16 (i - 4I) + 4 pair + (j - 4J)
+//   Q layout:  X[i][j] of block (I, J) in lane 16 (j - 4J) + 4 pair + (i - 4I)
+// an MFMA takes A in Q, B in P and returns D in P (scripts/ubench_valu.hip probes
+// the lane maps), and the recursion closes without any data movement:
+//   Z^T = G^T A'^T : A = G (V's P layout read as G^T in Q), B = A'^T (constant),
+//                    D = Z^T in P = Z in Q
+//   V   = sv Ab^T + Ef : A = sv (Z's Q layout), B = Ab^T (per pair, loaded once),
+//                    C = Ef, D = V in P.
+// Per element and step the VALU keeps the exp and the log (7 + 8 fp64 operations,
+// table-driven with LDS tables) and a share of the column maxima; the 16 fmas of
+// the two contractions go to the matrix cores (4 MFMAs per 64 elements).
+//
+// Column maxima without fp64 work.  The exp's range reduction s = V * 2048/ln2 +
+// (1.5 2^52 + 2^31) leaves n + 2^31 (n = round(V 2048/ln2)) in the low word of s as
+// an unsigned integer whose order is V's; the column maximum m is an integer max of
+// those words (two v_permlane swaps reduce the four lane rows of both column blocks
+// at once), the shift by M = m ln2/2048 is an integer subtraction inside the exp's
+// exponent arithmetic, and M comes back in the log's integer exponent: log Z + M =
+// (k 2048 + m) ln2/2048 + log(mantissa).  The maxima reach the Q layout of the log
+// by one ds_bpermute per column block.  This needs |V| < 2^31 ln2/2048 (7.3e5);
+// pairs whose inputs could exceed 7e5 over T steps (|V| <= T (max |E| + log S) for
+// row sums <= 1) go to the exact fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "vbhem_internal.h"
+#include "vbhem_log_table.h"
+
+#ifndef VBHEM_BWD4_WAVES
+#define VBHEM_BWD4_WAVES 4   // waves per SIMD
+#endif
+#ifndef VBHEM_BWD4_QPW
+#define VBHEM_BWD4_QPW 1     // quads (of 4 pairs) per wavefront
+#endif
+
+namespace vbhem {
+
+namespace {
+
+constexpr int kQPW = VBHEM_BWD4_QPW;
+constexpr int kWaves = VBHEM_BWD4_WAVES;
+constexpr int kNWB = 4;             // waves per block; kWaves blocks per CU
+constexpr int kPPW = 4 * kQPW;      // pairs per wavefront (one tile)
+// underflow guard of the column sums Z (as fb_bwd2_kernel): Z < 2^-665
+constexpr int kZMinHi = 0x16600000;
+constexpr double kInvLn2N = 2954.639443740597;        // 2048 / ln 2
+constexpr double kLn2N = 0x1.62e42fefa39efp-12;       // ln 2 / 2048 (2048 kLn2N = ln 2 exactly)
+constexpr double kShiftU = 0x1.8p52 + 2147483648.0;   // low word of s = n + 2^31
+constexpr unsigned kBias = 1010u * 2048u;             // exp: 2^(-1010) folded into the table
+constexpr unsigned kWq0 = 0u - 2147483648u - 1023u * 2048u;  // log: m + 2^31 -> m - 1023*2048
+constexpr double kVMax = 7.0e5;                       // |V| limit of the integer maxima
+alignas(16) __device__ const double kExpTab4[2048] = VBHEM_EXP2048_TABLE_INIT;
+alignas(16) __device__ const double kLogTab4[2 * 1024] = VBHEM_LOG12_TABLE_INIT;
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// s = V 2048/ln2 + 1.5 2^52 + 2^31: n + 2^31 in the low word (exact for |V| < 7.3e5)
+__device__ __forceinline__ double red_s(double v) { return fma(v, kInvLn2N, kShiftU); }
+__device__ __forceinline__ unsigned lo_u(double x) { return (unsigned)__double2loint(x); }
+
+// exp(V - m ln2/2048) for wp = m + 2^31 - kBias, N elements stage by stage (the
+// chains interleave: the kernel's latency is hidden by ILP, not by more waves):
+// d = max(0, n - m + kBias) (the clamp sends anything below exp(-700) to
+// ~exp(-700)); 2^(d/2048 - 1010) from the table (scaled by 2^-1010) and the
+// exponent add, exp(r) as a cubic, |r| <= ln2/4096
+template <int N>
+__device__ __forceinline__ void exp_m_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
+                                        const unsigned (&wp)[N], const double *etab) {
+  double r[N], t[N];
+  unsigned d[N];
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    d[x] = __builtin_elementwise_sub_sat(lo_u(s[x]), wp[x]);
+    t[x] = *reinterpret_cast<const double *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((d[x] << 3) & 0x3ff8u), 8));
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) r[x] = fma(-(s[x] - kShiftU), kLn2N, v[x]);
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double q = fma(r[x], 1.0 / 6.0, 0.5);
+    const double pp = fma(q, r[x] * r[x], r[x]);
+    const double m = fma(t[x], pp, t[x]);
+    // hi(m) + (d >> 11) << 20 as shift + shift-add: the shifted value is laundered
+    // through an empty asm so the combiner cannot merge the two shifts into a
+    // shift-and-mask (three ops).  No instruction is written in asm here: the
+    // compiler's hazard recognizer does not see operands of inline asm, and a VALU
+    // read of an MFMA result needs wait states it would not insert.
+    unsigned e = d[x] >> 11;
+    asm("" : "+v"(e));
+    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
+  }
+}
+
+// log(Z) + m ln2/2048 for wq = m - 1023*2048 (int32), N elements stage by stage:
+// Z = 2^e zz, zz in [1, 2), 1024 intervals {1/(2c), -log(1/c)}, log1p(r) to r^4 in
+// s = r/2; (e 2048 + m) ln2/2048 is one fma against the table constant (the
+// integer sum is exact)
+template <int N>
+__device__ __forceinline__ void log_m_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
+                                        const double *ltab) {
+  double zz[N], ic[N], w[N];
+  // exponent word of 1.0 in a register the combiner cannot see through: the
+  // mantissa insert below becomes one v_bfi_b32
+  unsigned one_hi = 0x3ff00000u;
+  asm("" : "+v"(one_hi));
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const unsigned hi = (unsigned)__double2hiint(z[x]);
+    // zz = mantissa with exponent 0, kk = (hi >> 20) 2048 + wq (shift + shift-add)
+    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
+    unsigned ex = hi >> 20;
+    asm("" : "+v"(ex));
+    const int kk = (int)(ex << 11) + wq[x];
+    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    const double2 e = *reinterpret_cast<const double2 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 6) & 0x3ff0u), 16));
+    ic[x] = e.x;
+    w[x] = fma((double)kk, kLn2N, e.y);
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double sh = fma(zz[x], ic[x], -0.5);
+    const double s2 = sh * sh;
+    double q = fma(sh, -2.0, 4.0 / 3.0);
+    q = fma(q, sh, -1.0);
+    y[x] = fma(fma(q, s2, sh), 2.0, w[x]);
+  }
+}
+
+// column maxima of a quad's two column blocks: x0 / x1 = this lane row's maximum of
+// block J = 0 / 1; the result's lane row r holds block J = r & 1 (over all 4 rows)
+__device__ __forceinline__ unsigned colmax_rows(unsigned x0, unsigned x1) {
+  const auto a = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
+  const unsigned u = max((unsigned)a[0], (unsigned)a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return max((unsigned)b[0], (unsigned)b[1]);
+}
+// row r holds block r & 1 -> block 0 / block 1 in every row
+__device__ __forceinline__ void split_rows(unsigned w, unsigned &w0, unsigned &w1) {
+  const auto a = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  w0 = a[0];
+  w1 = a[1];
+}
+// the same row reduction as sums of doubles (the termination's column sums)
+__device__ __forceinline__ double colsum_rows(double x0, double x1) {
+  const auto al = __builtin_amdgcn_permlane16_swap(lo_u(x0), lo_u(x1), false, false);
+  const auto ah = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x0),
+                                                   (unsigned)__double2hiint(x1), false, false);
+  const double u = __hiloint2double((int)ah[0], (int)al[0]) + __hiloint2double((int)ah[1], (int)al[1]);
+  const auto bl = __builtin_amdgcn_permlane32_swap(lo_u(u), lo_u(u), false, false);
+  const auto bh = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(u),
+                                                   (unsigned)__double2hiint(u), false, false);
+  return __hiloint2double((int)bh[0], (int)bl[0]) + __hiloint2double((int)bh[1], (int)bl[1]);
+}
+
+__device__ __forceinline__ double shfl_xor_d(double x, int m) {
+  const int l = (int)__lane_id() ^ m;
+  const int lo = __builtin_amdgcn_ds_bpermute(l << 2, __double2loint(x));
+  const int hi = __builtin_amdgcn_ds_bpermute(l << 2, __double2hiint(x));
+  return __hiloint2double(hi, lo);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64 * kNWB) __attribute__((amdgpu_waves_per_eu(kWaves)))
+void fb_bwd4_kernel(const SplitArgs p) {
+  constexpr int S = 8;
+  __shared__ __attribute__((aligned(16))) double etab[2048];      // 2^(i/2048 - 1010)
+  __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];  // {1/(2c), -log(1/c)}
+  __shared__ double amax[S], lpi[S];
+  const int tid = threadIdx.x;
+  for (int x = tid; x < 2048; x += 64 * kNWB) {
+    etab[x] = kExpTab4[x] * 0x1p-1010;
+    ltab[x] = kLogTab4[x];
+  }
+  const int SB = p.SB, K = p.K, T = p.T;
+  // persistent: NB blocks per cluster; XCD-aware when NB % 8 == 0 (as fb_bwd2_kernel)
+  const int bk = blockIdx.x, NB = (int)gridDim.x / K;
+  int j, t0;
+  if (NB % 8 == 0) {
+    const int rr = bk / 8;
+    j = rr % K;
+    t0 = (rr / K) * 8 + bk % 8;
+  } else {
+    j = bk % K;
+    t0 = bk / K;
+  }
+  j = __builtin_amdgcn_readfirstlane(j);
+  if (tid < S) {
+    const double *la = p.logA + ((size_t)j * S + tid) * S;
+    double mx = la[0];
+    for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
+    amax[tid] = mx;
+    lpi[tid] = p.logPi[(size_t)j * S + tid];
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane >> 4, b = (lane >> 2) & 3, c = lane & 3;
+  // B operand of Z^T = G^T A'^T, block (K, I'): A'[4I' + c][4K + r]
+  double AT[2][2];
+#pragma unroll
+  for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) AT[k2][i2] = p.Atg[(size_t)j * S * S + (4 * i2 + c) * S + 4 * k2 + r];
+  // A operand of the amax fold (rows amax[sigma], Q layout: sigma = 4I + c)
+  const double amQ[2] = {amax[c], amax[4 + c]};
+  const double lpP[2] = {lpi[r], lpi[4 + r]};  // P layout: sigma = 4I + r
+  bool cl_nf = false;
+#pragma unroll
+  for (int x = 0; x < S; ++x) cl_nf |= isnan(amax[x]) || isnan(lpi[x]);
+  // ds_bpermute sources of the log's column maxima (Q layout: column 4J + r)
+  const int qsrc0 = (0 * 16 + 4 * b + r) << 2, qsrc1 = (1 * 16 + 4 * b + r) << 2;
+  const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
+  const double vlim = kVMax / (double)T - 3.0;
+
+  const int ntile = (p.i_end - p.i_begin + kPPW - 1) / kPPW;
+  for (int tile = wave * NB + t0; tile < ntile; tile += NB * kNWB) {
+    const int i0 = p.i_begin + tile * kPPW;
+    double Ef[kQPW][2][2], V[kQPW][2][2], AbT[kQPW][2][2];
+    bool rbad[kQPW], nfb[kQPW];
+    int zmin[kQPW];
+#pragma unroll
+    for (int q = 0; q < kQPW; ++q) {
+      const int i = i0 + 4 * q + b;
+      const int ic = i < p.i_end ? i : p.i_end - 1;
+      // B operand of V = sv Ab^T + Ef, block (J', J): Ab[4J + c][4J' + r] (zero past SB)
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int be = 4 * jj + c, bp = 4 * j2 + r;
+          const double a = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
+          AbT[q][j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+        }
+      double mabs = 0.0, rs = 0.0;
+      bool nf = false;
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int be = 4 * jj + c;
+          const double e = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
+                               (be < SB ? be : SB - 1)];
+          V[q][i2][jj] = e;
+          // Ef = E + amax[sigma] sum_b' Ab[beta][b'] on the matrix cores
+          Ef[q][i2][jj] = mfma4(amQ[i2], AbT[q][1][jj], mfma4(amQ[i2], AbT[q][0][jj], e));
+          mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[q][i2][jj])));
+          nf |= !isfinite(Ef[q][i2][jj]);
+        }
+      // row sums of Ab (P layout, column 4J + c): the |V| bound assumes <= 1
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) rs = fmax(rs, mfma4(1.0, AbT[q][1][jj], mfma4(1.0, AbT[q][0][jj], 0.0)));
+      rbad[q] = !(mabs < vlim) || rs > 1.0 + 1e-6;
+      nfb[q] = nf;
+      zmin[q] = 0x7fffffff;
+    }
+
+    // ---- K2: backward recursion, t = T-1 .. 1 ----
+    // each phase over all quads of the wavefront before the next one, so the
+    // independent quads sit next to each other in the dependency chain of a step
+    // (column maxima -> exp -> MFMA -> log -> MFMA)
+    for (int t = T - 1; t >= 1; --t) {
+      double s[kQPW][2][2];
+      unsigned wp[kQPW][2];
+      int mq[kQPW][2];
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q) {
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) s[q][i2][jj] = red_s(V[q][i2][jj]);
+        const unsigned w = colmax_rows(max(lo_u(s[q][0][0]), lo_u(s[q][1][0])),
+                                       max(lo_u(s[q][0][1]), lo_u(s[q][1][1])));
+        const int wq = (int)(w + kWq0);
+        mq[q][0] = __builtin_amdgcn_ds_bpermute(qsrc0, wq);
+        mq[q][1] = __builtin_amdgcn_ds_bpermute(qsrc1, wq);
+        split_rows(w - kBias, wp[q][0], wp[q][1]);
+      }
+      constexpr int NE = 4 * kQPW;  // elements per lane: (q, I, J) flattened
+      double G[kQPW][2][2];
+      {
+        double vv[NE], sf[NE], gg[NE];
+        unsigned wpf[NE];
+#pragma unroll
+        for (int x = 0; x < NE; ++x) {
+          vv[x] = V[x / 4][(x / 2) % 2][x % 2];
+          sf[x] = s[x / 4][(x / 2) % 2][x % 2];
+          wpf[x] = wp[x / 4][x % 2];
+        }
+        exp_m_n<NE>(gg, vv, sf, wpf, etab);
+#pragma unroll
+        for (int x = 0; x < NE; ++x) G[x / 4][(x / 2) % 2][x % 2] = gg[x];
+      }
+      // Z^T block (J, I') = sum_K G^T(J, K) A'^T(K, I'); G^T(J, K) is V's block (K, J)
+      double Z[kQPW][2][2];
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int i2 = 0; i2 < 2; ++i2) Z[q][jj][i2] = mfma4(G[q][0][jj], AT[0][i2], 0.0);
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int i2 = 0; i2 < 2; ++i2) Z[q][jj][i2] = mfma4(G[q][1][jj], AT[1][i2], Z[q][jj][i2]);
+      double sv[kQPW][2][2];
+      {
+        double zf[NE], yf[NE];
+        int wqf[NE];
+#pragma unroll
+        for (int x = 0; x < NE; ++x) {
+          zf[x] = Z[x / 4][(x / 2) % 2][x % 2];
+          wqf[x] = mq[x / 4][(x / 2) % 2];
+        }
+#pragma unroll
+        for (int q = 0; q < kQPW; ++q)
+          zmin[q] = min(zmin[q], min(min(__double2hiint(zf[4 * q]), __double2hiint(zf[4 * q + 1])),
+                                     min(__double2hiint(zf[4 * q + 2]), __double2hiint(zf[4 * q + 3]))));
+        log_m_n<NE>(yf, zf, wqf, ltab);
+#pragma unroll
+        for (int x = 0; x < NE; ++x) sv[x / 4][(x / 2) % 2][x % 2] = yf[x];
+      }
+      // V block (I, J) = Ef + sum_J' sv(I, J') Ab^T(J', J); sv(I, J') is Z^T's block (J', I)
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q)
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) V[q][i2][jj] = mfma4(sv[q][0][i2], AbT[q][0][jj], Ef[q][i2][jj]);
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q)
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) V[q][i2][jj] = mfma4(sv[q][1][i2], AbT[q][1][jj], V[q][i2][jj]);
+    }
+
+    // ---- K3: termination, L_elbo = sum_beta prior_beta log sum_sigma exp(lpi + E + L) ----
+#pragma unroll
+    for (int q = 0; q < kQPW; ++q) {
+      const int i = i0 + 4 * q + b;
+      const int ic = i < p.i_end ? i : p.i_end - 1;
+      double W[2][2], s[2][2];
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          // (a state of zero initial probability: lpi = -inf, kept in the integer range)
+          W[i2][jj] = fmax(lpP[i2] + V[q][i2][jj], -7.2e5);
+          s[i2][jj] = red_s(W[i2][jj]);
+        }
+      const unsigned w = colmax_rows(max(lo_u(s[0][0]), lo_u(s[1][0])), max(lo_u(s[0][1]), lo_u(s[1][1])));
+      unsigned wp[2];
+      split_rows(w - kBias, wp[0], wp[1]);
+      double ev[2][2];
+      {
+        const double wf[4] = {W[0][0], W[0][1], W[1][0], W[1][1]};
+        const double sf[4] = {s[0][0], s[0][1], s[1][0], s[1][1]};
+        const unsigned wpf[4] = {wp[0], wp[1], wp[0], wp[1]};
+        double ef[4];
+        exp_m_n<4>(ef, wf, sf, wpf, etab);
+        ev[0][0] = ef[0]; ev[0][1] = ef[1]; ev[1][0] = ef[2]; ev[1][1] = ef[3];
+      }
+      // row r: column 4 (r & 1) + c, the layout of w
+      const double zs = colsum_rows(ev[0][0] + ev[1][0], ev[0][1] + ev[1][1]);
+      double lse1[1];
+      {
+        const double zsf[1] = {zs};
+        const int wqf[1] = {(int)(w + kWq0)};
+        log_m_n<1>(lse1, zsf, wqf, ltab);
+      }
+      const double lse = lse1[0];
+      const int be = 4 * (r & 1) + c;
+      const double pr = be < SB ? p.prior[(size_t)ic * SB + be] : 0.0;
+      double y = r < 2 ? pr * lse : 0.0;
+      const bool bad = zmin[q] < kZMinHi || !isfinite(y) || rbad[q];
+      y += shfl_xor_d(y, 1);
+      y += shfl_xor_d(y, 2);
+      y += shfl_xor_d(y, 16);
+      const bool pbad = (__ballot(bad) & pmask) != 0;
+      const bool pnf = cl_nf || (__ballot(nfb[q]) & pmask) != 0;
+      if (lane == 4 * b && r == 0 && i < p.i_end) {
+        const size_t pair = (size_t)i * K + j;
+        if (pbad && !pnf) {
+          // underflow or range with finite inputs: the exact kernel recomputes the pair
+          const int slot = atomicAdd(p.flag_count, 1);
+          atomicAdd(p.flag_count + 1, 1);
+          p.flag_list[slot] = (int)pair;
+          p.LL[pair] = y;
+        } else {
+          p.LL[pair] = (pbad && pnf) ? __builtin_nan("") : y;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+bool bwd4_supported(int S, int SB) { return S == 8 && SB >= 1 && SB <= 8; }
+int bwd4_waves() { return kNWB; }
+int bwd4_ppb() { return kNWB * kPPW; }
+int bwd4_resident_blocks() {
+  return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd4_kernel), 64 * kNWB, 0);
+}
+
+hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st) {
+  if (!bwd4_supported(a.S, a.SB) || !a.Atg) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fb_bwd4_kernel, dim3(grid), dim3(64 * kNWB), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace vbhem

@@ -272,6 +272,18 @@ int bwd2_ppb(int S, int nwb);     // pairs per block
 int bwd2_resident_blocks(int S, int nwb, size_t lds);
 hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
 
+// kernel timing hooks for code outside vbhem_capi.hip (null when timing is off)
+void *timing_begin(hipStream_t st);
+void timing_end_em_math(void *ev0, hipStream_t st);
+
+// fb_bwd4_kernel (vbhem_fb_bwd4.hip): the backward-only pass for S = 8, SB <= 8 with
+// both contractions on v_mfma_f64_4x4x4f64; SplitArgs fields as fb_bwd2_kernel
+bool bwd4_supported(int S, int SB);
+int bwd4_waves();            // waves per block
+int bwd4_ppb();              // pairs per block (one tile per wavefront)
+int bwd4_resident_blocks();  // per CU
+hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st);
+
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
 // Fallback bookkeeping in the workspace's int array `flags`:
 //   [0] pairs flagged by the current pass (consumed and reset by fb_exact_kernel)

@@ -237,6 +237,10 @@ int vbhem_timing_read_emission(double *em_ms, long long *em_launches);
 /* Summed time and launch count of the gated forward pass (fb_split_kernel in
  * list mode; VBHEM_FUSED_GATED only) since the last call. */
 int vbhem_timing_read_gated(double *fwd_ms, long long *fwd_launches);
+/* Summed time and launch count of the EM loop's per-iteration math kernel
+ * (vbhem_em_run's bound + M-step + next prelude on the device, em_dev_kernel) since
+ * the last call; recorded while vbhem_timing_enable(1) is on. */
+int vbhem_timing_read_em_math(double *ms, long long *launches);
 
 const char *vbhem_last_error(void);
 const char *vbhem_version(void);
