@@ -421,7 +421,10 @@ def main():
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
     lpc = 1 if S <= 4 else 2 if S <= 8 else 4      # split_lpc (dense / list modes)
     lpc_bwd = 1 if S <= 8 else 2                    # split_lpc_bwd (backward mode)
-    if gated and S <= 16 and not os.environ.get("VBHEM_NO_BWD2"):
+    if gated and S == 8 and Sb <= 8 and not os.environ.get("VBHEM_NO_BWD4") \
+            and not os.environ.get("VBHEM_NO_BWD2"):
+        kname = "vbhem::fb_bwd4_kernel"   # MFMA contractions (S = 8)
+    elif gated and S <= 16 and not os.environ.get("VBHEM_NO_BWD2"):
         kname = f"vbhem::fb_bwd2_kernel<{S}>"
     else:
         kname = (f"vbhem::fb_split_kernel<{S}, {lpc_bwd if gated else lpc}, {1 if gated else 0}>"
