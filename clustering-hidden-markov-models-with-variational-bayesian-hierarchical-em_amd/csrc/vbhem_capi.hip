@@ -397,6 +397,7 @@ struct FbCtx {
   size_t bwd2_lds = 0;
   int bwd2_ppb = 0, bwd2_nwb = 0;
   bool bwd4 = false;  // S = 8, SB <= 8: fb_bwd4_kernel (MFMA contractions) instead
+  bool list4 = false;  // S = 8, SB <= 8, T = 10: fb_list4_kernel for the gate-list pass
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
   // emission_u_kernel: on the prepared operand (base->U) or one built per call in u_ws
@@ -447,6 +448,7 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
       c.bwd2_lds = vbhem::bwd2_lds(cl->S, c.bwd2_nwb);
       c.bwd2_ppb = vbhem::bwd2_ppb(cl->S, c.bwd2_nwb);
       c.bwd4 = vbhem::bwd4_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD4");
+      c.list4 = vbhem::list4_supported(cl->S, b->SB, T, cl->K) && !std::getenv("VBHEM_NO_LIST4");
     }
   }
   return VBHEM_OK;
@@ -488,8 +490,16 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
   ca.list = list; ca.list_tot = list_tot; ca.list_cap = list_cap;
   hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
-  hipError_t e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_l), c.split.lds_l, st);
-  if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
+  hipError_t e;
+  if (c.list4) {  // S = 8, SB <= 8, T = 10: fb_list4_kernel (MFMA), one wave per quad item
+    ca.Atg = c.bwd.a.Atg;
+    const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list4_resident_blocks()));
+    e = vbhem::launch_list4(ca, grid, st);
+    if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
+  } else {
+    e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_l), c.split.lds_l, st);
+    if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
+  }
   if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
   if (fold) return VBHEM_OK;  // the statistics kernel takes the flagged pairs (StatsArgs::fold)
   vbhem::FbArgs a = c.plan.a;

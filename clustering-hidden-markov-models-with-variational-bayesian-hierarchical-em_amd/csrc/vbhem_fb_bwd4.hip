@@ -38,7 +38,7 @@
 #include <cmath>
 
 #include "vbhem_internal.h"
-#include "vbhem_log_table.h"
+#include "vbhem_mfma4.h"
 
 #ifndef VBHEM_BWD4_WAVES
 #define VBHEM_BWD4_WAVES 4   // waves per SIMD
@@ -55,128 +55,7 @@ constexpr int kQPW = VBHEM_BWD4_QPW;
 constexpr int kWaves = VBHEM_BWD4_WAVES;
 constexpr int kNWB = 4;             // waves per block; kWaves blocks per CU
 constexpr int kPPW = 4 * kQPW;      // pairs per wavefront (one tile)
-// underflow guard of the column sums Z (as fb_bwd2_kernel): Z < 2^-665
-constexpr int kZMinHi = 0x16600000;
-constexpr double kInvLn2N = 2954.639443740597;        // 2048 / ln 2
-constexpr double kLn2N = 0x1.62e42fefa39efp-12;       // ln 2 / 2048 (2048 kLn2N = ln 2 exactly)
-constexpr double kShiftU = 0x1.8p52 + 2147483648.0;   // low word of s = n + 2^31
-constexpr unsigned kBias = 1010u * 2048u;             // exp: 2^(-1010) folded into the table
-constexpr unsigned kWq0 = 0u - 2147483648u - 1023u * 2048u;  // log: m + 2^31 -> m - 1023*2048
-constexpr double kVMax = 7.0e5;                       // |V| limit of the integer maxima
-alignas(16) __device__ const double kExpTab4[2048] = VBHEM_EXP2048_TABLE_INIT;
-alignas(16) __device__ const double kLogTab4[2 * 1024] = VBHEM_LOG12_TABLE_INIT;
-
-__device__ __forceinline__ double mfma4(double a, double b, double c) {
-  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
-}
-
-// s = V 2048/ln2 + 1.5 2^52 + 2^31: n + 2^31 in the low word (exact for |V| < 7.3e5)
-__device__ __forceinline__ double red_s(double v) { return fma(v, kInvLn2N, kShiftU); }
-__device__ __forceinline__ unsigned lo_u(double x) { return (unsigned)__double2loint(x); }
-
-// exp(V - m ln2/2048) for wp = m + 2^31 - kBias, N elements stage by stage (the
-// chains interleave: the kernel's latency is hidden by ILP, not by more waves):
-// d = max(0, n - m + kBias) (the clamp sends anything below exp(-700) to
-// ~exp(-700)); 2^(d/2048 - 1010) from the table (scaled by 2^-1010) and the
-// exponent add, exp(r) as a cubic, |r| <= ln2/4096
-template <int N>
-__device__ __forceinline__ void exp_m_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
-                                        const unsigned (&wp)[N], const double *etab) {
-  double r[N], t[N];
-  unsigned d[N];
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    d[x] = __builtin_elementwise_sub_sat(lo_u(s[x]), wp[x]);
-    t[x] = *reinterpret_cast<const double *>(
-        __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((d[x] << 3) & 0x3ff8u), 8));
-  }
-#pragma unroll
-  for (int x = 0; x < N; ++x) r[x] = fma(-(s[x] - kShiftU), kLn2N, v[x]);
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const double q = fma(r[x], 1.0 / 6.0, 0.5);
-    const double pp = fma(q, r[x] * r[x], r[x]);
-    const double m = fma(t[x], pp, t[x]);
-    // hi(m) + (d >> 11) << 20 as shift + shift-add: the shifted value is laundered
-    // through an empty asm so the combiner cannot merge the two shifts into a
-    // shift-and-mask (three ops).  No instruction is written in asm here: the
-    // compiler's hazard recognizer does not see operands of inline asm, and a VALU
-    // read of an MFMA result needs wait states it would not insert.
-    unsigned e = d[x] >> 11;
-    asm("" : "+v"(e));
-    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
-  }
-}
-
-// log(Z) + m ln2/2048 for wq = m - 1023*2048 (int32), N elements stage by stage:
-// Z = 2^e zz, zz in [1, 2), 1024 intervals {1/(2c), -log(1/c)}, log1p(r) to r^4 in
-// s = r/2; (e 2048 + m) ln2/2048 is one fma against the table constant (the
-// integer sum is exact)
-template <int N>
-__device__ __forceinline__ void log_m_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
-                                        const double *ltab) {
-  double zz[N], ic[N], w[N];
-  // exponent word of 1.0 in a register the combiner cannot see through: the
-  // mantissa insert below becomes one v_bfi_b32
-  unsigned one_hi = 0x3ff00000u;
-  asm("" : "+v"(one_hi));
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const unsigned hi = (unsigned)__double2hiint(z[x]);
-    // zz = mantissa with exponent 0, kk = (hi >> 20) 2048 + wq (shift + shift-add)
-    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
-    unsigned ex = hi >> 20;
-    asm("" : "+v"(ex));
-    const int kk = (int)(ex << 11) + wq[x];
-    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
-    const double2 e = *reinterpret_cast<const double2 *>(
-        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 6) & 0x3ff0u), 16));
-    ic[x] = e.x;
-    w[x] = fma((double)kk, kLn2N, e.y);
-  }
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const double sh = fma(zz[x], ic[x], -0.5);
-    const double s2 = sh * sh;
-    double q = fma(sh, -2.0, 4.0 / 3.0);
-    q = fma(q, sh, -1.0);
-    y[x] = fma(fma(q, s2, sh), 2.0, w[x]);
-  }
-}
-
-// column maxima of a quad's two column blocks: x0 / x1 = this lane row's maximum of
-// block J = 0 / 1; the result's lane row r holds block J = r & 1 (over all 4 rows)
-__device__ __forceinline__ unsigned colmax_rows(unsigned x0, unsigned x1) {
-  const auto a = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
-  const unsigned u = max((unsigned)a[0], (unsigned)a[1]);
-  const auto b = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return max((unsigned)b[0], (unsigned)b[1]);
-}
-// row r holds block r & 1 -> block 0 / block 1 in every row
-__device__ __forceinline__ void split_rows(unsigned w, unsigned &w0, unsigned &w1) {
-  const auto a = __builtin_amdgcn_permlane16_swap(w, w, false, false);
-  w0 = a[0];
-  w1 = a[1];
-}
-// the same row reduction as sums of doubles (the termination's column sums)
-__device__ __forceinline__ double colsum_rows(double x0, double x1) {
-  const auto al = __builtin_amdgcn_permlane16_swap(lo_u(x0), lo_u(x1), false, false);
-  const auto ah = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x0),
-                                                   (unsigned)__double2hiint(x1), false, false);
-  const double u = __hiloint2double((int)ah[0], (int)al[0]) + __hiloint2double((int)ah[1], (int)al[1]);
-  const auto bl = __builtin_amdgcn_permlane32_swap(lo_u(u), lo_u(u), false, false);
-  const auto bh = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(u),
-                                                   (unsigned)__double2hiint(u), false, false);
-  return __hiloint2double((int)bh[0], (int)bl[0]) + __hiloint2double((int)bh[1], (int)bl[1]);
-}
-
-__device__ __forceinline__ double shfl_xor_d(double x, int m) {
-  const int l = (int)__lane_id() ^ m;
-  const int lo = __builtin_amdgcn_ds_bpermute(l << 2, __double2loint(x));
-  const int hi = __builtin_amdgcn_ds_bpermute(l << 2, __double2hiint(x));
-  return __hiloint2double(hi, lo);
-}
-
+using namespace m4;
 }  // namespace
 
 __global__ __launch_bounds__(64 * kNWB) __attribute__((amdgpu_waves_per_eu(kWaves)))
@@ -186,10 +65,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];  // {1/(2c), -log(1/c)}
   __shared__ double amax[S], lpi[S];
   const int tid = threadIdx.x;
-  for (int x = tid; x < 2048; x += 64 * kNWB) {
-    etab[x] = kExpTab4[x] * 0x1p-1010;
-    ltab[x] = kLogTab4[x];
-  }
+  stage_tables(etab, ltab, tid, 64 * kNWB);
   const int SB = p.SB, K = p.K, T = p.T;
   // persistent: NB blocks per cluster; XCD-aware when NB % 8 == 0 (as fb_bwd2_kernel)
   const int bk = blockIdx.x, NB = (int)gridDim.x / K;

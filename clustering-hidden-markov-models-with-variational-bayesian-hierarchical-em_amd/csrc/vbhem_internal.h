@@ -284,6 +284,14 @@ int bwd4_ppb();              // pairs per block (one tile per wavefront)
 int bwd4_resident_blocks();  // per CU
 hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st);
 
+// fb_list4_kernel (vbhem_fb_list4.hip): the gate-list pass for S = 8, SB <= 8, T = 10
+// with every contraction on v_mfma_f64_4x4x4f64; SplitArgs fields as fb_split_kernel's
+// list mode (E, A, prior, Atg, logA, logPi, lists, nu1 / xi / tnu, flags)
+constexpr int kList4MaxK = 1024;
+bool list4_supported(int S, int SB, int T, int K);
+int list4_resident_blocks();  // per CU
+hipError_t launch_list4(const SplitArgs &a, unsigned grid, hipStream_t st);
+
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
 // Fallback bookkeeping in the workspace's int array `flags`:
 //   [0] pairs flagged by the current pass (consumed and reset by fb_exact_kernel)

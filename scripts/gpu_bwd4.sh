@@ -15,7 +15,8 @@ one() {  # label, then env assignments
 }
 for rep in 1 2; do
   one tree_$rep VBHEM_X=1 || exit 1
-  one bwd2_$rep VBHEM_NO_BWD4=1 || exit 1
+  one nolist4_$rep VBHEM_NO_LIST4=1 || exit 1
+  one bwd2_$rep VBHEM_NO_BWD4=1 VBHEM_NO_LIST4=1 || exit 1
   for lib in "$@"; do one $(basename $lib .so)_$rep VBHEM_LIB_PATH=$(realpath $lib) || exit 1; done
 done
 # PMC passes (the tree's library) when PMC=1: instruction mix and waits of the C4 step
