@@ -68,6 +68,10 @@ SHAPES = [
     ("C5like", 1, 32, 12, 12, 16, 1, 10, False),
     ("S16", 2, 3, 16, 16, 4, 1, 6, False),
     ("d16diag", 2, 3, 6, 6, 16, 0, 6, False),
+    # S = 8, T = 10: the MFMA kernels (fb_bwd4_kernel, fb_list4_kernel); padded base
+    # states (SB < 8, ragged) and gate lists that end inside a 4-pair quad
+    ("S8_ragged", 9, 5, 8, 6, 3, 1, 10, True),
+    ("S8_quads", 37, 4, 8, 8, 2, 0, 10, False),
     # outside the column-split kernel's limits (S <= 16, SB <= S, d <= 16): generic kernel
     ("d20", 3, 2, 3, 3, 20, 1, 5, False),
     ("S20", 2, 2, 20, 20, 2, 1, 4, False),

@@ -198,6 +198,33 @@ def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
     assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
+@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}])
+def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch):
+    """The adversarial cluster at S = Sb = 8, T = 10: its pairs underflow in the MFMA
+    backward pass (fb_bwd4_kernel) and, being gated, again in the MFMA gate-list pass
+    (fb_list4_kernel); both passes' flags reach the exact fallback (folded into the
+    consumers, or two fb_exact_kernel launches)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    N, K = 41, 2
+    cs, consts = adversarial_case(1, S=8, Sb=8, d=3, N=N, K=K, T=10)
+    consts["c"][1:] = 1.0e4
+    base, T = cs["base"], cs["T"]
+    S, d = 8, 3
+    pairs = vo.c_estep_pairs(base, consts, T)
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    assert (Z[:, 0] > 1e-8).all()
+    st = vo.c_statistics(Z, pairs, 1)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
+    assert eng.fallback_count() >= 2 * N
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, k
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
 def test_host_pointer_entry_point(vb, vo, capi_lib):
     """vbhem_estep_pairs_host (what the MEX gateway calls): host arrays in/out."""
     from vbhem_amd import _capi
