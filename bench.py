@@ -223,17 +223,29 @@ def main():
     # the statistics land in pinned host memory (what the host M-step reads): one
     # rank writes them there straight from the statistics kernel; several ranks
     # all-reduce the device vector, then copy it
-    host_stats = eng.host_stats_buffer()
+    # two of them: with one E-step of run-ahead the next step writes the other one
+    hbufs = [eng.host_stats_buffer(), eng.host_stats_buffer()]
+    host_stats = hbufs[0]
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def launch(k):
+        """Enqueue E-step k: statistics into pinned host buffer k % 2, then an event."""
+        hs = hbufs[k % 2]
         if world == 1 and not os.environ.get("VBHEM_BENCH_COPY"):
-            eng.fused(tN, out=host_stats)
+            eng.fused(tN, out=hs)
         else:
             st = eng.fused(tN)
             allreduce(st)
-            host_stats.copy_(st, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        return host_stats
+            hs.copy_(st, non_blocking=True)
+        done[k % 2].record(stream)
+        return hs
+
+    def step():
+        """One E-step, the host waiting for its statistics before anything else."""
+        hs = launch(0)
+        stream.synchronize()
+        return hs
 
     for _ in range(args.warmup):
         step()
@@ -248,13 +260,19 @@ def main():
     # each side of the kernel (10 us of a 160 us C3 step).  The per-kernel
     # breakdown comes from a separate instrumented pass below.
     time_every = 1 if args.steps < 8 else 4
+    # E-steps as the C++ EM loop issues them (vbhem_em_run): step k + 1 is enqueued
+    # before the host waits for step k's statistics (one step of run-ahead), so the
+    # GPU does not idle while the host takes a step's statistics and launches the
+    # next; every step's statistics still reach pinned host memory and are waited for
     t0 = time.perf_counter()
     for s in range(args.steps):
         if s % time_every == 0:
             _capi.timing_enable(True, fb_only=True)
-        stats = step()
+        stats = launch(s)
         if s % time_every == 0:
             _capi.timing_enable(False)
+        if s > 0:
+            done[(s - 1) % 2].synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     stats = stats.clone()
@@ -266,6 +284,18 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
     tk = _capi.timing_read()
+    # the same steps with the host waiting on each before launching the next (the
+    # rate of an E-step whose statistics must be on the host before anything else)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ts0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dts = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dts, op=dist.ReduceOp.MAX)
+    dts = float(dts.item())
     # per-kernel breakdown (emission, gated forward, statistics): a few more E-steps
     # with every launch timed (not part of `value`)
     bd_steps = max(1, min(args.steps, 5))
@@ -382,19 +412,30 @@ def main():
         eng_s.set_clusters(consts)
         eng_s.set_log_omega(logOm)
         tN_s = (float(opt["Nv"]) * N) * eng_s.base.omega
-        hs = eng_s.host_stats_buffer()
+        hs = [eng_s.host_stats_buffer(), eng_s.host_stats_buffer()]
+        ev_s = [torch.cuda.Event(), torch.cuda.Event()]
         for _ in range(3):
-            eng_s.fused(tN_s, out=hs)
-            torch.cuda.current_stream(dev).synchronize()
+            eng_s.fused(tN_s, out=hs[0])
+            stream.synchronize()
         nss = max(20, args.steps)
         ts0 = time.perf_counter()
-        for _ in range(nss):
-            eng_s.fused(tN_s, out=hs)
-            torch.cuda.current_stream(dev).synchronize()
+        for k in range(nss):  # one step of run-ahead, as the timed region above
+            eng_s.fused(tN_s, out=hs[k % 2])
+            ev_s[k % 2].record(stream)
+            if k > 0:
+                ev_s[(k - 1) % 2].synchronize()
+        stream.synchronize()
         es_ms = (time.perf_counter() - ts0) / nss * 1e3
+        ts0 = time.perf_counter()
+        for _ in range(nss):
+            eng_s.fused(tN_s, out=hs[0])
+            stream.synchronize()
+        es_sync_ms = (time.perf_counter() - ts0) / nss * 1e3
         em_s = em_iteration(eng_s, N)
         shard_sim = {"bases": ns, "estep_ms": es_ms,
                      "estep_ceiling_8gpu": (dt / args.steps * 1e3) / es_ms,
+                     "estep_sync_ms": es_sync_ms,
+                     "estep_sync_ceiling_8gpu": (dts / args.steps * 1e3) / es_sync_ms,
                      "em_iteration": em_s,
                      "em_ceiling_8gpu_excl_allreduce": (em_it["ms"] / em_s["ms"]
                                                         if em_it and em_s else None),
@@ -452,6 +493,11 @@ def main():
                                 f"Nv={opt['Nv']}"),
                    "N": N, "K": K, "S": S, "Sb": Sb, "d": d, "tau": T,
                    "parallelism": f"bases sharded over {world} GPU(s), 1 RCCL all-reduce/E-step"},
+        "pacing": ("one E-step of run-ahead (the C++ EM loop's): step k+1 is enqueued before "
+                   "the host waits for step k's statistics in pinned memory"),
+        "synchronous": {"value": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
+                        "note": "the host waits for each step's statistics before launching "
+                                "the next (no overlap of the host hand-over)"},
         "pairs_per_s": N * K * args.steps / dt,
         "roofline": {
             "bound": "valu",

@@ -70,8 +70,8 @@ class EStepEngine:
         self.LL = torch.zeros((N, K), dtype=F64, device=dv)
         self._ws_fused = None
         self._ws_pairs = None
-        self._mapped = None  # (host_stats_buffer tensor, its device address)
-        self._fused_args = None  # (pointers + stream key, entry point, name, ctypes arguments)
+        self._mapped = {}  # host_stats_buffer data pointer -> (tensor, its device address)
+        self._fused_args = {}  # pointers + stream key -> (entry point, name, ctypes arguments)
 
     # -- inputs -------------------------------------------------------------
     @property
@@ -136,7 +136,7 @@ class EStepEngine:
         """A pinned host vector of stats_len doubles for ``fused(out=...)`` (its
         device address is resolved once, here)."""
         buf = torch.zeros((self.stats_len,), dtype=F64, pin_memory=True)
-        self._mapped = (buf, self._device_address(buf))
+        self._mapped[buf.data_ptr()] = (buf, self._device_address(buf))
         return buf
 
     def _device_address(self, host: torch.Tensor) -> int:
@@ -152,8 +152,9 @@ class EStepEngine:
             if out.device != self.device:
                 raise ValueError("out is on another device")
             return _capi.ptr(out)
-        if self._mapped is not None and self._mapped[0] is out:
-            return self._mapped[1]
+        m = self._mapped.get(out.data_ptr())
+        if m is not None and m[0] is out:
+            return m[1]
         # pinned host memory: the kernel writes it through its device address
         return self._device_address(out)
 
@@ -174,7 +175,7 @@ class EStepEngine:
         sp = _capi.ptr(self.stats) if out is None else self._out_ptr(out)
         st = torch.cuda.current_stream(self.device).cuda_stream
         key = (tildeN.data_ptr(), sp, st)
-        if self._fused_args is None or self._fused_args[0] != key:
+        if key not in self._fused_args:
             # the call's ctypes arguments, rebuilt only when a pointer or the stream changes
             # (an EM loop repeats the same call: ~4 us of Python per E-step otherwise)
             head = (ctypes.byref(self._bt), ctypes.byref(self._ct))
@@ -184,8 +185,10 @@ class EStepEngine:
                            ctypes.c_void_p(st))
             fn, name = ((self.lib.vbhem_estep_fused, "vbhem_estep_fused") if self.trials == 1 else
                         (self.lib.vbhem_estep_fused_trials, "vbhem_estep_fused_trials"))
-            self._fused_args = (key, fn, name, args)
-        _, fn, name, args = self._fused_args
+            if len(self._fused_args) >= 8:  # (a few buffers / streams alternate at most)
+                self._fused_args.clear()
+            self._fused_args[key] = (fn, name, args)
+        fn, name, args = self._fused_args[key]
         _capi.check(fn(*args), name)
         return res
 

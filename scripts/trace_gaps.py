@@ -9,7 +9,7 @@ idx = [i for i, r in enumerate(rows) if "emission_prep" in r["Kernel_Name"]]
 shown = 0
 for k in range(len(idx) - 1):
     s, e = idx[k], idx[k + 1]
-    if not any("bwd2" in r["Kernel_Name"] for r in rows[s:e]) or k < 6:
+    if not any("fb_bwd" in r["Kernel_Name"] for r in rows[s:e]) or k < 6:
         continue
     t0 = int(rows[s]["Start_Timestamp"])
     prev = t0
