@@ -97,8 +97,8 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2) AT[k2][i2] = p.Atg[(size_t)j * S * S + (4 * i2 + c) * S + 4 * k2 + r];
   // A operand of the amax fold (rows amax[sigma], Q layout: sigma = 4I + c)
-  const double amQ[2] = {amax[c], amax[4 + c]};
-  const double lpP[2] = {lpi[r], lpi[4 + r]};  // P layout: sigma = 4I + r
+  // amax (Q layout: sigma = 4I + c) and lpi (P layout: sigma = 4I + r) are read from
+  // LDS where they are used (once per tile), not held in registers across the loop
   bool cl_nf = false;
 #pragma unroll
   for (int x = 0; x < S; ++x) cl_nf |= isnan(amax[x]) || isnan(lpi[x]);
@@ -137,7 +137,8 @@ void fb_bwd4_kernel(const SplitArgs p) {
                                (be < SB ? be : SB - 1)];
           V[q][i2][jj] = e;
           // Ef = E + amax[sigma] sum_b' Ab[beta][b'] on the matrix cores
-          Ef[q][i2][jj] = mfma4(amQ[i2], AbT[q][1][jj], mfma4(amQ[i2], AbT[q][0][jj], e));
+          const double am = amax[4 * i2 + c];
+          Ef[q][i2][jj] = mfma4(am, AbT[q][1][jj], mfma4(am, AbT[q][0][jj], e));
           mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[q][i2][jj])));
           nf |= !isfinite(Ef[q][i2][jj]);
         }
@@ -242,7 +243,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           // (a state of zero initial probability: lpi = -inf, kept in the integer range)
-          W[i2][jj] = fmax(lpP[i2] + V[q][i2][jj], -7.2e5);
+          W[i2][jj] = fmax(lpi[4 * i2 + r] + V[q][i2][jj], -7.2e5);
           s[i2][jj] = red_s(W[i2][jj]);
         }
       const unsigned w = colmax_rows(max(lo_u(s[0][0]), lo_u(s[1][0])), max(lo_u(s[0][1]), lo_u(s[1][1])));
