@@ -60,23 +60,29 @@ void fb_list4_kernel(const SplitArgs p) {
   }
   __syncthreads();
   const int nitem = __builtin_amdgcn_readfirstlane(pre[K]);
-  const int lane = tid & 63, wave = tid >> 6;
-  const int r = lane >> 4, b = (lane >> 2) & 3, c = lane & 3;
-  const int qsrc0 = (4 * b + r) << 2, qsrc1 = (16 + 4 * b + r) << 2;
-  const int taddr = (16 * c + 4 * b + r) << 2;
-  const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
   const double vlim = kVMax / (double)T - 3.0;
-  const int gw = (int)blockIdx.x * kL4NWB + wave, nw = (int)gridDim.x * kL4NWB;
+  const int gw = (int)blockIdx.x * kL4NWB + (tid >> 6), nw = (int)gridDim.x * kL4NWB;
 
-  int jc = -1, js = 0;
-  double AT[2][2], Ap[2][2], amQ[2], lpP[2];
-  bool cl_nf = false;
+  int js = 0;
   for (int it = gw; it < nitem; it += nw) {
+    // lane geometry recomputed per item from an opaque copy of the thread id, so that
+    // no lane-invariant address is hoisted out of the item loop (such live ranges
+    // spilled to scratch at 256 VGPRs)
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int lane = tq & 63;
+    const int r = lane >> 4, b = (lane >> 2) & 3, c = lane & 3;
+    const int qsrc0 = (4 * b + r) << 2, qsrc1 = (16 + 4 * b + r) << 2;
+    const int taddr = (16 * c + 4 * b + r) << 2;
+    const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
     while (pre[js + 1] <= it) ++js;  // items ascend within a wave: continue the search
     const int j = __builtin_amdgcn_readfirstlane(js);
-    if (j != jc) {
-      // the cluster's constants: A'^T as the B operand of Z^T (block (K, I'):
-      // A'[4I' + c][4K + r]), A' in P (A'[4I + r][4I' + c]), amax (rows 4I + c), lpi
+    // the cluster's constants, loaded per item (cache hits; holding them across items
+    // spilled 17 values to scratch): A'^T as the B operand of Z^T (block (K, I'):
+    // A'[4I' + c][4K + r]), A' in P (A'[4I + r][4I' + c]), amax (rows 4I + c), lpi
+    double AT[2][2], Ap[2][2], amQ[2], lpP[2];
+    bool cl_nf;
+    {
       const double *At = p.Atg + (size_t)j * S * S;
       bool nf = false;
 #pragma unroll
@@ -97,7 +103,6 @@ void fb_list4_kernel(const SplitArgs p) {
         nf |= isnan(mx) || isnan(lpP[i2]);
       }
       cl_nf = __ballot(nf) != 0;
-      jc = j;
     }
     const int n0 = (it - pre[j]) * 4;
     const int tot = p.list_tot[j];
