@@ -53,7 +53,14 @@ namespace {
 
 constexpr int kQPW = VBHEM_BWD4_QPW;
 constexpr int kWaves = VBHEM_BWD4_WAVES;
-constexpr int kNWB = 4;             // waves per block; kWaves blocks per CU
+#ifndef VBHEM_BWD4_NWB
+#define VBHEM_BWD4_NWB 4
+#endif
+// waves per block (the 32 KB of tables once per block; LDS then allows 4 blocks per CU):
+// 5 waves per SIMD (VBHEM_BWD4_WAVES=5, NWB=10, with the lane geometry recomputed per
+// tile to fit) measured 1.87 vs 1.69 ms, 8-wave blocks 1.69-1.72: more waves per SIMD
+// only add contention between the MFMA and VALU work
+constexpr int kNWB = VBHEM_BWD4_NWB;
 constexpr int kPPW = 4 * kQPW;      // pairs per wavefront (one tile)
 using namespace m4;
 }  // namespace
