@@ -42,7 +42,7 @@ __device__ __forceinline__ unsigned lo_u(double x) { return (unsigned)__double2l
 // chains interleave: the kernel's latency is hidden by ILP, not by more waves):
 // d = max(0, n - m + kBias) (the clamp sends anything below exp(-700) to
 // ~exp(-700)); 2^(d/2048 - 1010) from the table (scaled by 2^-1010) and the
-// exponent add, exp(r) as a cubic, |r| <= ln2/4096
+// exponent add, exp(r) as a quadratic, |r| <= ln2/4096
 template <int N>
 __device__ __forceinline__ void exp_m_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
                                         const unsigned (&wp)[N], const double *etab) {
@@ -58,8 +58,10 @@ __device__ __forceinline__ void exp_m_n(double (&g)[N], const double (&v)[N], co
   for (int x = 0; x < N; ++x) r[x] = fma(-(s[x] - kShiftU), kLn2N, v[x]);
 #pragma unroll
   for (int x = 0; x < N; ++x) {
-    const double q = fma(r[x], 1.0 / 6.0, 0.5);
-    const double pp = fma(q, r[x] * r[x], r[x]);
+    // exp(r) - 1 to second order: |r| <= ln2/4096, the dropped r^3/6 <= 8.1e-13
+    // relative -- an absolute 8e-13 in log Z per step, far below the recursion's
+    // 1e-10 (pairs) and 1e-5 (ELBO) tolerances; one fp64 operation less than cubic
+    const double pp = fma(0.5 * r[x], r[x], r[x]);
     const double m = fma(t[x], pp, t[x]);
     // hi(m) + (d >> 11) << 20 as shift + shift-add: the shifted value is laundered
     // through an empty asm so the combiner cannot merge the two shifts into a
@@ -73,7 +75,7 @@ __device__ __forceinline__ void exp_m_n(double (&g)[N], const double (&v)[N], co
 }
 
 // log(Z) + m ln2/2048 for wq = m - 1023*2048 (int32), N elements stage by stage:
-// Z = 2^e zz, zz in [1, 2), 1024 intervals {1/(2c), -log(1/c)}, log1p(r) to r^4 in
+// Z = 2^e zz, zz in [1, 2), 1024 intervals {1/(2c), -log(1/c)}, log1p(r) to r^3 in
 // s = r/2; (e 2048 + m) ln2/2048 is one fma against the table constant (the
 // integer sum is exact)
 template <int N>
@@ -100,10 +102,11 @@ __device__ __forceinline__ void log_m_n(double (&y)[N], const double (&z)[N], co
   }
 #pragma unroll
   for (int x = 0; x < N; ++x) {
+    // log1p(r) = 2 (s - s^2 + 4/3 s^3) with s = r/2, |s| <= 2^-12: the dropped -4 s^4
+    // is <= 1.4e-14 absolute
     const double sh = fma(zz[x], ic[x], -0.5);
     const double s2 = sh * sh;
-    double q = fma(sh, -2.0, 4.0 / 3.0);
-    q = fma(q, sh, -1.0);
+    const double q = fma(sh, 4.0 / 3.0, -1.0);
     y[x] = fma(fma(q, s2, sh), 2.0, w[x]);
   }
 }
