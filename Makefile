@@ -35,7 +35,7 @@ $(LIBDIR)/%_mex.so: integration/%_mex.c integration/h3m_mex_common.h include/vbh
 # test-only: the restricted-domain exp/log/rcp of vbhem_math.h, host and device
 mathcheck: tests/mathcheck/libmathcheck.so
 
-tests/mathcheck/libmathcheck.so: tests/mathcheck/mathcheck.hip $(PKG)/csrc/vbhem_math.h $(PKG)/csrc/vbhem_log_table.h
+tests/mathcheck/libmathcheck.so: tests/mathcheck/mathcheck.hip $(PKG)/csrc/vbhem_math.h $(PKG)/csrc/vbhem_log_table.h $(PKG)/csrc/vbhem_mfma4.h
 	$(HIPCC) $(HIPFLAGS) -I$(PKG)/csrc -shared -o $@ $<
 
 clean:

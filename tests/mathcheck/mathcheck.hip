@@ -7,6 +7,7 @@
 
 #include "vbhem_log_table.h"
 #include "vbhem_math.h"
+#include "vbhem_mfma4.h"
 
 static const double kLogTabHost[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
 __device__ const double kLogTabDev[vbhem::kLogTabDoubles] = VBHEM_LOG_TABLE_INIT;
@@ -67,6 +68,27 @@ __global__ void logtabe_kernel(int n, const double* __restrict__ x, double* __re
     vbhem::log_tabe_n<1>(y, z, lt);
     l[i] = y[0];
     vbhem::exp_tabe_n<1>(y, m, et);
+    e[i] = y[0];
+  }
+}
+
+// exp_m_n / log_m_n of the MFMA kernels (vbhem_mfma4.h) with the column maximum m = 0:
+// log at x, exp at -x (device only: integer builtins of gfx950)
+__global__ void logtabm_kernel(int n, const double* __restrict__ x, double* __restrict__ l,
+                               double* __restrict__ e) {
+  __shared__ __attribute__((aligned(16))) double et[2048];
+  __shared__ __attribute__((aligned(16))) double lt[2 * 1024];
+  vbhem::m4::stage_tables(et, lt, threadIdx.x, blockDim.x);
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    double y[1];
+    const double z[1] = {x[i]}, v[1] = {-x[i]}, s[1] = {vbhem::m4::red_s(-x[i])};
+    const int wq[1] = {(int)(2147483648u + vbhem::m4::kWq0)};
+    const unsigned wp[1] = {2147483648u - vbhem::m4::kBias};
+    vbhem::m4::log_m_n<1>(y, z, wq, lt);
+    l[i] = y[0];
+    vbhem::m4::exp_m_n<1>(y, v, s, wp, et);
     e[i] = y[0];
   }
 }
@@ -162,6 +184,7 @@ static int logtab_device_impl(int n, const double* x, double* l, double* e, int 
   if (st == hipSuccess && n > 0) {
     if (fast == 2) logtabc_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
     else if (fast == 3) logtabe_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
+    else if (fast == 4) logtabm_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de);
     else logtab_kernel<<<(n + 255) / 256, 256>>>(n, dx, dl, de, fast);
     st = hipGetLastError();
   }
@@ -187,6 +210,10 @@ int logtabc_device(int n, const double* x, double* l, double* e) {
 
 int logtabe_device(int n, const double* x, double* l, double* e) {
   return logtab_device_impl(n, x, l, e, 3);
+}
+
+int logtabm_device(int n, const double* x, double* l, double* e) {
+  return logtab_device_impl(n, x, l, e, 4);
 }
 
 // Same on device 0 (host arrays in/out).  Returns 0 or a hipError_t.

@@ -167,3 +167,27 @@ def test_logtabe_host_build(mathcheck):
 @pytest.mark.gpu
 def test_logtabe_device_build(mathcheck):
     assert _check_logtabe(mathcheck.logtabe_device) == 0
+
+
+@pytest.mark.gpu
+def test_mfma_kernels_exp_log_device_build(mathcheck):
+    """exp_m_n / log_m_n of fb_bwd4_kernel and fb_list4_kernel (vbhem_mfma4.h) at the
+    column maximum m = 0: exp to second order (|r| <= ln2/4096: <= 8.1e-13 relative,
+    plus the one-constant reduction's 3.3e-17 |x|) on [0, 700] and clamped at ~exp(-700)
+    below; log1p to third order (<= 1.4e-14 absolute) over the positive normals."""
+    dp = ctypes.POINTER(ctypes.c_double)
+    fn = mathcheck.logtabm_device
+    fn.argtypes = [ctypes.c_int, dp, dp, dp]
+    x = _samples()
+    x = np.concatenate([x, np.random.default_rng(11).uniform(0.99, 1.01, N // 4),
+                        np.random.default_rng(12).uniform(0.0, 1.0, N // 4),
+                        np.random.default_rng(13).uniform(0.0, 700.0, N // 4), [700.0, 745.0, 800.0, 1e4]])
+    l, e = np.zeros_like(x), np.zeros_like(x)
+    assert fn(len(x), x.ctypes.data_as(dp), l.ctypes.data_as(dp), e.ctypes.data_as(dp)) == 0
+    pos = x >= 1e-200
+    ref = np.log(x[pos])
+    assert (np.abs(l[pos] - ref) <= 2.0 * np.spacing(np.abs(ref)) + 2e-14).all()
+    m = x <= 700
+    rel = np.abs(e[m] - np.exp(-x[m])) / np.exp(-x[m])
+    assert (rel <= 1e-12 + 1e-16 * x[m]).all(), float(rel.max())
+    assert (e[x > 710] > 0).all() and (e[x > 710] < 1e-300).all()
