@@ -1479,12 +1479,10 @@ static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st
   return hipGetLastError();
 }
 
-template <int NTW, int G, int KSM, int NXR>
-static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+template <int NTW, int G, int KSM, int NXR, int PD>
+static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
   const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double);
-  // ring depth 2 (C4: 0.177 ms of statistics per step against 0.191 with depth 4 and
-  // its 768 resident blocks)
-  auto *fn = &stats_list_m_kernel<NTW, G, KSM, NXR, 2>;
+  auto *fn = &stats_list_m_kernel<NTW, G, KSM, NXR, PD>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   // one generation of resident blocks (the kernel is latency-bound: a second round of
@@ -1498,6 +1496,17 @@ static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st
   if (a.fold) nb = std::min<long long>(nb, a.xslots);  // one fallback scratch slot per block
   hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(64 * kSmWaves), lds, st, a);
   return hipGetLastError();
+}
+
+// ring depth 2 (C4: 0.177 ms of statistics per step against 0.191 with depth 4 and
+// its 768 resident blocks); VBHEM_SM_PD=3 (A/B) for the one-pair-group variant
+template <int NTW, int G, int KSM, int NXR>
+static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
+  if (G == 1) {
+    if (const char *ev = std::getenv("VBHEM_SM_PD"))
+      if (std::atoi(ev) == 3) return launch_sm_pd<NTW, G, KSM, NXR, 3>(a, grid, st);
+  }
+  return launch_sm_pd<NTW, G, KSM, NXR, 2>(a, grid, st);
 }
 
 // the sum_nu_1 | sum_xi chunks per wave: ceil(ceil((S + S^2) / 64) / tile groups)
