@@ -83,13 +83,16 @@ def fb_bytes_per_pair(S, Sb, d, covmode, K, split=True, backward_only=False):
 
 
 def committed_traffic(config, N, world, want):
-    """HBM bytes per launch of the E-step kernel from the newest committed PMC
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC
     summary for this config (profiles/rNN_<config>.json, made by
     scripts/profile.sh + scripts/prof_summary.py; FETCH_SIZE x2 + WRITE_SIZE per
     MI355X_MICROARCH.md).  The counters cannot be collected inside the timed
-    run, so the value is read back here; None when no summary matches."""
+    run, so the value is read back here; None when no summary matches.  The
+    full-size launches are taken alone when the summary separates them (a bench
+    run under the profiler also launches the kernel at the shard size)."""
     import glob
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config.lower()}.json")))
+    short = want.split("::")[-1].split("<")[0]
     for path in reversed(cands):
         try:
             with open(path) as f:
@@ -98,6 +101,11 @@ def committed_traffic(config, N, world, want):
             continue
         if summ.get("N") not in (None, N) or summ.get("n_gpus", 1) != world:
             continue
+        full = summ.get("full_size_launches", {}).get(short, {})
+        if "hbm_bytes" in full:
+            return full["hbm_bytes"]["traffic"], os.path.relpath(path, ROOT) + " (full-size launches)"
+        if not summ.get("pmc_full_size_only"):
+            continue    # PMC passes that mixed launch sizes: not this kernel's traffic
         for name, k in summ.get("kernels", {}).items():
             if name == want and "hbm_bytes_per_launch" in k:
                 return k["hbm_bytes_per_launch"]["traffic"], os.path.relpath(path, ROOT)
@@ -220,6 +228,21 @@ def main():
     eng.set_log_omega(logOm)
     tN = (float(opt["Nv"]) * N) * eng.base.omega
     allreduce = make_allreduce()
+    # the native collective: an RCCL communicator of our own (include/vbhem_dist.h),
+    # all-reduced in-stream by the C++ EM loop and by the E-steps below; torch's
+    # process group then only carries the barriers and the timing maxima
+    rccl, rccl_err = None, None
+    if world > 1 and backend == "nccl" and not os.environ.get("VBHEM_BENCH_NO_RCCL"):
+        from vbhem_amd.dist import RcclComm
+        try:
+            rccl = RcclComm(dev)
+        except Exception as ex:  # noqa: BLE001 -- reported, then torch's RCCL path
+            rccl_err = repr(ex)
+        ok = torch.tensor([0.0 if rccl is None else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() < 1.0 and rccl is not None:
+            rccl.close()
+            rccl = None
     # the statistics land in pinned host memory (what the host M-step reads): one
     # rank writes them there straight from the statistics kernel; several ranks
     # all-reduce the device vector, then copy it
@@ -236,7 +259,10 @@ def main():
             eng.fused(tN, out=hs)
         else:
             st = eng.fused(tN)
-            allreduce(st)
+            if rccl is not None:
+                rccl.allreduce(st)
+            else:
+                allreduce(st)
             hs.copy_(st, non_blocking=True)
         done[k % 2].record(stream)
         return hs
@@ -344,30 +370,44 @@ def main():
     # E-step, the all-reduce, the statistics' copy to the host, the bound, the M-step
     # and the next iteration's psi prelude + constant upload
     def em_iteration(engine, n_total):
-        """Per-iteration cost of the C++ EM loop: two runs of different length, the
-        difference of their times over the difference of their iteration counts
-        (the per-run setup -- posterior upload, workspace, result copies -- cancels)."""
+        """Per-iteration cost of the C++ EM loop (vbhem_em_run_ext).  Primary: the
+        loop's own host clock -- the time at which each iteration's bound reaches
+        the host -- over one long run, the median of the per-iteration differences
+        after the first two.  Beside it the median of 5 paired differences
+        (t(run of 1 + n iterations) - t(run of 1)) / n, where the per-run set-up
+        (posterior upload, result copies) cancels."""
         if args.em_iters <= 0:
             return None
         from vbhem_amd import native_em
         o = dict(opt, minDiff=0.0)          # no early stop: exactly max_iter + 1 iterations
+        kw = dict(total_N=n_total, allreduce=None if rccl else allreduce, comm=rccl)
 
-        def timed(n):
+        def timed(n, stamps=False):
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
             t0 = time.perf_counter()
-            r = native_em.run(post, engine, o, total_N=n_total, allreduce=allreduce, max_iter=n)
+            r = native_em.run(post, engine, o, max_iter=n, timestamps=stamps, **kw)
             torch.cuda.synchronize()
             dt_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
             if world > 1:
                 dist.all_reduce(dt_, op=dist.ReduceOp.MAX)
-            return float(dt_.item()), r.iters
+            return float(dt_.item()), r
 
         timed(1)
-        t_a, n_a = timed(1)
-        t_b, n_b = timed(1 + args.em_iters)
-        ms = (t_b - t_a) / max(1, n_b - n_a) * 1e3
+        n_long = max(20, 4 * args.em_iters)
+        _, rl = timed(n_long, stamps=True)
+        steps = np.diff(rl.iter_seconds)[2:] * 1e3
+        ms_loc = float(np.median(steps))
+        if world > 1:   # the slowest rank's clock
+            t_ = torch.tensor([ms_loc], dtype=torch.float64, device=dev)
+            dist.all_reduce(t_, op=dist.ReduceOp.MAX)
+            ms_loc = float(t_.item())
+        pairs = []
+        for _ in range(5):
+            t_a, ra = timed(1)
+            t_b, rb = timed(1 + args.em_iters)
+            pairs.append((t_b - t_a) / max(1, rb.iters - ra.iters) * 1e3)
         # the loop's per-iteration math kernel (bound + M-step + next prelude on the
         # device), timed with events in one more run
         _capi.timing_read()
@@ -376,9 +416,17 @@ def main():
         _capi.timing_enable(False)
         tm = _capi.timing_read()
         math_ms = tm["em_math_ms"] / tm["em_math_launches"] if tm["em_math_launches"] else None
-        return dict(ms=ms, per_s=1e3 / ms, iterations=n_b - n_a, math_kernel_ms=math_ms,
-                    method=("(t(run of %d iterations) - t(run of %d)) / %d: the per-run setup "
-                            "cancels" % (n_b, n_a, n_b - n_a)))
+        return dict(ms=ms_loc, per_s=1e3 / ms_loc, iterations=int(steps.size),
+                    iteration_ms_p10_p90=[float(np.percentile(steps, 10)),
+                                          float(np.percentile(steps, 90))],
+                    paired_diff_ms=float(np.median(pairs)), paired_diff_all_ms=pairs,
+                    math_kernel_ms=math_ms,
+                    collective=("RCCL in the loop (vbhem_rccl_allreduce_sum, %d ranks)" % world
+                                if rccl else ("torch.distributed callback" if world > 1 else "none")),
+                    method=("median of the per-iteration differences of the loop's own host clock "
+                            "(vbhem_em_run_ext iter_seconds) over a %d-iteration run, iterations 3.. ; "
+                            "paired_diff_ms: median of 5 x (t(run of %d) - t(run of 1)) / %d"
+                            % (n_long + 1, 1 + args.em_iters + 1, args.em_iters)))
 
     em_it = em_iteration(eng, N)
     step()   # hat_Z / L_elbo of the bench's own constants again (the EM run moved them)
@@ -445,6 +493,8 @@ def main():
         del eng_s
 
     if rank != 0:
+        if rccl is not None:
+            rccl.close()
         if world > 1:
             dist.destroy_process_group()
         return
@@ -493,6 +543,10 @@ def main():
                                 f"Nv={opt['Nv']}"),
                    "N": N, "K": K, "S": S, "Sb": Sb, "d": d, "tau": T,
                    "parallelism": f"bases sharded over {world} GPU(s), 1 RCCL all-reduce/E-step"},
+        "collective": ({"kind": "native RCCL communicator (vbhem_rccl_allreduce_sum)", "ranks": world}
+                       if rccl is not None else
+                       {"kind": "torch.distributed all_reduce" if world > 1 else "none (one rank)",
+                        "ranks": world, "rccl_error": rccl_err}),
         "pacing": ("one E-step of run-ahead (the C++ EM loop's): step k+1 is enqueued before "
                    "the host waits for step k's statistics in pinned memory"),
         "synchronous": {"value": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
@@ -552,13 +606,13 @@ def main():
         "emission_kernel_ms": tkb["em_ms"] / max(1, tkb["em_launches"]),
         "stats_kernels_ms_per_step": tkb["stats_ms"] / bd_steps,
         "breakdown_steps": bd_steps,
-        "host_mstep_ms": em_it["math_kernel_ms"] if em_it else None,
-        "host_mstep_note": ("the per-iteration math of the EM loop (vbhem_em_run: bound, M-step, "
-                            "next psi prelude) as the loop runs it: one device kernel on the "
-                            "E-step stream, replicated on every rank, HIP-event timed; "
-                            "host_math_cpp_ms: the same math in C++ on the host "
-                            "(vbhem_em_host_iteration, the loop's path for d > 16 or S > 64), "
-                            "host_math_python_ms: the Python path"),
+        "em_math_kernel_ms": em_it["math_kernel_ms"] if em_it else None,
+        "em_math_note": ("the per-iteration math of the EM loop (vbhem_em_run: bound, M-step, "
+                         "next psi prelude) as the loop runs it: one device kernel on the "
+                         "E-step stream, replicated on every rank, HIP-event timed; "
+                         "host_math_cpp_ms: the same math in C++ on the host "
+                         "(vbhem_em_host_iteration, the loop's path for d > 16 or S > 32), "
+                         "host_math_python_ms: the Python host path"),
         "host_math_cpp_ms": host_ms,
         "host_math_python_ms": host_py_ms,
         "em_iteration": em_it,
@@ -602,6 +656,8 @@ def main():
                                            "oracle/vbhem_oracle.c on %d host threads" % thr),
                                 "tolerance": {"LL_elbo": 1e-10, "hat_Z": 1e-5}}
     print(json.dumps(res))
+    if rccl is not None:
+        rccl.close()
     if world > 1:
         dist.destroy_process_group()
 

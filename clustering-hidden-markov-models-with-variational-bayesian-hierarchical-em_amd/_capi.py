@@ -56,7 +56,12 @@ class HmmParamsT(ctypes.Structure):  # include/vbhmm_fb.h vbhmm_params_t
                 ("const_denominator", ctypes.c_double)]
 
 
+class EmExtT(ctypes.Structure):  # include/vbhem_em.h vbhem_em_ext_t
+    _fields_ = [("rccl_comm", _vp), ("iter_seconds", _vp), ("calc_deriv", _c_int), ("dLL", _vp)]
+
+
 ALLREDUCE_FN = ctypes.CFUNCTYPE(_c_int, _vp, _c_size, _vp, _vp)
+RCCL_ID_BYTES = 128  # include/vbhem_dist.h VBHEM_RCCL_ID_BYTES
 
 EXPORTS = {
     "vbhem_prepare_base_bytes": (_c_size, [ctypes.POINTER(BaseT)]),
@@ -111,6 +116,17 @@ EXPORTS = {
                               ctypes.POINTER(PostT), _vp, ctypes.POINTER(_c_int),
                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int), _vp, _vp,
                               _vp, _vp, _c_size, _vp, ALLREDUCE_FN, _vp]),
+    "vbhem_em_run_ext": (_c_int, [ctypes.POINTER(BaseT), _vp, _c_int, ctypes.POINTER(EmOptT),
+                                  ctypes.POINTER(PostT), _vp, ctypes.POINTER(_c_int),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int), _vp, _vp,
+                                  _vp, _vp, _c_size, _vp, ALLREDUCE_FN, _vp,
+                                  ctypes.POINTER(EmExtT)]),
+    "vbhem_em_lower_bound_derivs": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp,
+                                             _vp, _vp, _vp, _vp]),
+    "vbhem_rccl_unique_id": (_c_int, [_vp]),
+    "vbhem_rccl_comm_init": (_c_int, [_c_int, _c_int, _vp, _c_int, ctypes.POINTER(_vp)]),
+    "vbhem_rccl_comm_destroy": (_c_int, [_vp]),
+    "vbhem_rccl_allreduce_sum": (_c_int, [_vp, _vp, _c_size, _vp]),
     "vbhmm_fb_workspace_bytes": (_c_size, [ctypes.POINTER(SeqsT), _c_int]),
     "vbhmm_fb": (_c_int, [ctypes.POINTER(SeqsT), ctypes.POINTER(HmmParamsT), _vp, _vp, _vp, _vp, _vp,
                           _c_size, _vp]),

@@ -843,8 +843,9 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   // group, one trial: two fb_exact_kernel launches less per E-step)
   // (the statistics kernel needs a block, and so a scratch slot, per cluster: K below
   // the slot count)
+  // (and resp_kernel needs one per chunk block: at most kExactThreads chunks)
   const bool fold = gated && R == 1 && base->N <= w.group && ctx.split.ok && K < kExactThreads &&
-                    !std::getenv("VBHEM_NO_FOLD_EXACT");
+                    w.nslab <= kExactThreads && !std::getenv("VBHEM_NO_FOLD_EXACT");
   sa.fold = 0;
   for (int g0 = 0; g0 < base->N; g0 += w.group) {
     const int g1 = std::min(base->N, g0 + w.group);

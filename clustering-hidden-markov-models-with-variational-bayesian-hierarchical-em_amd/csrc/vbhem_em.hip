@@ -14,8 +14,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -380,6 +383,74 @@ int vbhem_em_mstep(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t 
   return VBHEM_OK;
 }
 
+int vbhem_em_lower_bound_derivs(const vbhem_post_t *post, const vbhem_em_opt_t *opt,
+                                const double *logLambdaTilde, const double *logA,
+                                const double *logPi, const double *logOmega, double *dLL) {
+  if (!post_ok(post) || !opt_ok(opt, post->d) || !logLambdaTilde || !logA || !logPi || !logOmega ||
+      !dLL)
+    return VBHEM_ERR_ARG;
+  // vbhemh3m_lb.m:202-345 (the same arithmetic as vbhem_amd/host.py::lower_bound_derivs)
+  const int K = post->K, S = post->S, d = post->d;
+  const bool full = post->covmode == VBHEM_COV_FULL;
+  const size_t dd = full ? (size_t)d * d : (size_t)d;
+  const double a0 = opt->alpha0, e0 = opt->eta0, ep0 = opt->epsilon0, l0 = opt->lambda0,
+               v0 = opt->v0;
+  std::vector<double> W0inv;
+  w0_inv(opt, d, W0inv);
+  const bool iid = opt->W0_len == 1;
+  double logdetW0inv = 0.0;
+  if (iid) logdetW0inv = d * std::log(W0inv[0]);
+  else for (int a = 0; a < d; ++a) logdetW0inv += std::log(W0inv[(size_t)a * d + a]);
+  double sO = 0.0, sPi = 0.0, sA = 0.0, sL = 0.0;
+  for (int k = 0; k < K; ++k) sO += logOmega[k];
+  for (size_t x = 0; x < (size_t)K * S; ++x) { sPi += logPi[x]; sL += logLambdaTilde[x]; }
+  for (size_t x = 0; x < (size_t)K * S * S; ++x) sA += logA[x];
+  double *g = dLL;
+  g[0] = K * psi(K * a0) - K * psi(a0) + sO;                              // alpha0
+  g[1] = K * (S * psi(S * e0) - S * psi(e0)) + sPi;                       // eta0
+  g[2] = (double)K * S * (S * psi(S * ep0) - S * psi(ep0)) + sA;          // epsilon0
+  double sp = 0.0;
+  for (int q = 1; q <= d; ++q) sp += psi(0.5 * (v0 + 1 - q));
+  g[3] = (double)K * S * (0.5 * logdetW0inv - (d / 2.0) * std::log(2.0) - 0.5 * sp) + 0.5 * sL;  // v0
+  const int nW = opt->W0_len;
+  double *gW = g + 5, *gm = g + 5 + nW;
+  double lam0 = 0.0;
+  for (int x = 0; x < nW; ++x) gW[x] = 0.0;
+  for (int a = 0; a < d; ++a) gm[a] = 0.0;
+  std::vector<double> Wf((size_t)d * d), Wd((size_t)d);
+  for (size_t ks = 0; ks < (size_t)K * S; ++ks) {
+    const double *W = post->W + ks * dd, *mk = post->m + ks * d;
+    const double v = post->v[ks], lam = post->lam[ks];
+    if (full) {
+      for (size_t x = 0; x < dd; ++x) Wf[x] = W[x];
+    } else {
+      std::fill(Wf.begin(), Wf.end(), 0.0);
+      for (int a = 0; a < d; ++a) Wf[(size_t)a * d + a] = W[a];
+    }
+    double mWm = 0.0, trW = 0.0;
+    for (int a = 0; a < d; ++a) {
+      double wd = 0.0;  // (W (m - m0))[a]
+      for (int b = 0; b < d; ++b) wd += Wf[(size_t)a * d + b] * (mk[b] - opt->m0[b]);
+      mWm += (mk[a] - opt->m0[a]) * wd;
+      trW += Wf[(size_t)a * d + a];
+      gm[a] += l0 * v * wd;
+    }
+    lam0 += 0.5 * (d / l0 - d / lam - v * mWm);
+    if (iid) {
+      gW[0] += -0.5 * (-v * W0inv[0] * W0inv[0] * trW);
+    } else {
+      for (int a = 0; a < d; ++a) {
+        const double wi = W0inv[(size_t)a * d + a];
+        gW[a] += -0.5 * (-v * wi * wi * Wf[(size_t)a * d + a]);
+      }
+    }
+  }
+  g[4] = lam0;                                                            // lambda0
+  if (iid) gW[0] += (double)K * S * (-0.5 * v0 * d * W0inv[0]);
+  else for (int a = 0; a < d; ++a) gW[a] += (double)K * S * (-0.5 * v0 * W0inv[(size_t)a * d + a]);
+  return VBHEM_OK;
+}
+
 int vbhem_em_host_iteration(const vbhem_em_opt_t *opt, const double *stats, vbhem_post_t *post,
                              double *logA, double *logPi, double *m, double *P, double *c,
                              double *logLambdaTilde, double *logOmega, double *L) {
@@ -473,12 +544,97 @@ hipError_t copy_post(const vbhem_post_t *h, const PostDev &q, size_t dd, hipMemc
   return hipSuccess;
 }
 
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The loop's bound slots + sequence words live in pinned, mapped host memory.  One
+// 64-byte block per concurrent run, taken from a per-device pool and given back at
+// the end of the run: allocated once per process, not per run (hipHostMalloc /
+// hipHostFree of mapped memory cost a kernel-driver round trip each).
+struct Mapped {
+  double *h = nullptr, *d = nullptr;
+};
+std::mutex g_mapped_mu;
+std::map<int, std::vector<Mapped>> g_mapped_free;
+
+hipError_t acquire_mapped(Mapped &m) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    std::lock_guard<std::mutex> g(g_mapped_mu);
+    auto &v = g_mapped_free[dev];
+    if (!v.empty()) {
+      m = v.back();
+      v.pop_back();
+      return hipSuccess;
+    }
+  }
+  e = hipHostMalloc(reinterpret_cast<void **>(&m.h), 64, hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&m.d), m.h, 0);
+  return e;
+}
+
+void release_mapped(const Mapped &m) {
+  if (!m.h) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;  // keep it (never reused) rather than free mid-run
+  std::lock_guard<std::mutex> g(g_mapped_mu);
+  g_mapped_free[dev].push_back(m);
+}
+
+// the statistics' one collective per E-step run: in-stream RCCL, or the caller's hook
+int reduce_stats(const vbhem_em_ext_t *ext, vbhem_allreduce_fn allreduce, void *ctx,
+                 double *stats_dev, size_t slen, hipStream_t st) {
+  if (ext && ext->rccl_comm) return vbhem_rccl_allreduce_sum(ext->rccl_comm, stats_dev, slen, st);
+  if (allreduce && allreduce(stats_dev, slen, st, ctx) != 0) return VBHEM_ERR_HIP;
+  return VBHEM_OK;
+}
+
+// a host copy of a posterior (the one before the last M-step, for the derivatives)
+struct HostPost {
+  std::vector<double> a[7];
+  vbhem_post_t t{};
+  void size_like(const vbhem_post_t *p) {
+    const int K = p->K, S = p->S, d = p->d;
+    const size_t dd = p->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
+    const size_t n[7] = {(size_t)K, (size_t)K * S, (size_t)K * S * S, (size_t)K * S, (size_t)K * S,
+                         (size_t)K * S * d, (size_t)K * S * dd};
+    for (int x = 0; x < 7; ++x) a[x].resize(n[x]);
+    t = {K, S, d, p->covmode, a[0].data(), a[1].data(), a[2].data(), a[3].data(), a[4].data(),
+         a[5].data(), a[6].data()};
+  }
+  void copy_from(const vbhem_post_t *p) {
+    size_like(p);
+    const double *src[7] = {p->alpha, p->eta, p->epsilon, p->lam, p->v, p->m, p->W};
+    for (int x = 0; x < 7; ++x) std::copy(src[x], src[x] + a[x].size(), a[x].begin());
+  }
+};
+
+// vbhemh3m_lb.m:202-345 at a posterior: its prelude, then the raw derivatives
+int derivs_at(const vbhem_post_t *p, const vbhem_em_opt_t *opt, double *dLL) {
+  const int K = p->K, S = p->S, d = p->d;
+  const size_t dd = p->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
+  std::vector<double> lA((size_t)K * S * S), lPi((size_t)K * S), m((size_t)K * S * d),
+      P((size_t)K * S * dd), c((size_t)K * S), lLT((size_t)K * S), lO((size_t)K);
+  int rc = vbhem_em_prelude(p, lA.data(), lPi.data(), m.data(), P.data(), c.data(), lLT.data(),
+                            lO.data());
+  if (rc != VBHEM_OK) return rc;
+  return vbhem_em_lower_bound_derivs(p, opt, lLT.data(), lA.data(), lPi.data(), lO.data(), dLL);
+}
+
+void nan_derivs(const vbhem_em_opt_t *opt, int d, double *dLL) {
+  for (int x = 0; x < VBHEM_DLL_LEN(d, opt->W0_len); ++x) dLL[x] = std::nan("");
+}
+
 // The EM loop with the per-iteration host math in C++ on the host (shapes outside
-// the device kernels: d > 16 or S > 64).
+// the device kernels: d > 16 or S > 32).
 int em_run_host(const vbhem_base_t *base, const double *tildeN_dev, int T, const vbhem_em_opt_t *opt,
                 vbhem_post_t *post, double *LogLs, int *iters, double *L_final, int *stable,
                 double *stats_dev, double *hatZ_dev, double *LL_dev, void *workspace_dev,
-                hipStream_t st, vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
+                hipStream_t st, vbhem_allreduce_fn allreduce, void *allreduce_ctx,
+                const vbhem_em_ext_t *ext) {
   const int K = post->K, S = post->S, d = post->d;
   const size_t dd = post->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
   vbhem_cluster_t c0 = {K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -493,6 +649,8 @@ int em_run_host(const vbhem_base_t *base, const double *tildeN_dev, int T, const
   const double *dlogOmega = dc + nA + nPi + nm + nP + nc;
   const size_t slen = vbhem_stats_len(K, S, d, post->covmode);
   std::vector<double> stats(slen);
+  const bool deriv = ext && ext->calc_deriv && ext->dLL;
+  HostPost pre;
   double lastL = -DBL_MAX, L = -INFINITY;
   int it = 0;
   *stable = 1;
@@ -506,14 +664,17 @@ int em_run_host(const vbhem_base_t *base, const double *tildeN_dev, int T, const
     rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hatZ_dev, LL_dev,
                            workspace_dev, fused, st);
     if (rc != VBHEM_OK) return rc;
-    if (allreduce && allreduce(stats_dev, slen, st, allreduce_ctx) != 0) return VBHEM_ERR_HIP;
+    rc = reduce_stats(ext, allreduce, allreduce_ctx, stats_dev, slen, st);
+    if (rc != VBHEM_OK) return rc;
     e = hipMemcpyAsync(stats.data(), stats_dev, slen * sizeof(double), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return VBHEM_ERR_HIP;
+    if (deriv) pre.copy_from(post);
     // the bound of this iteration's E-step, then (stable) the M-step and the next
     // iteration's prelude: the whole per-iteration host math, one call
     rc = vbhem_em_host_iteration(opt, stats.data(), post, hA, hPi, hm, hP, hc, lLT.data(), hO, &L);
     if (rc != VBHEM_OK) return rc;
+    if (ext && ext->iter_seconds) ext->iter_seconds[it] = now_s();
     if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, stop before the M-step
       L = -INFINITY;
       *stable = 0;
@@ -529,19 +690,25 @@ int em_run_host(const vbhem_base_t *base, const double *tildeN_dev, int T, const
   }
   *iters = it;
   *L_final = L;
+  if (deriv) {
+    if (*stable) return derivs_at(&pre.t, opt, ext->dLL);  // step_fc.m:356-360
+    nan_derivs(opt, d, ext->dLL);                           // :362-368
+  }
   return VBHEM_OK;
 }
 
 }  // namespace
 
-int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
-                 const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
-                 double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
-                 double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
-                 vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
+int vbhem_em_run_ext(const vbhem_base_t *base, const double *tildeN_dev, int T,
+                     const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
+                     double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
+                     double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
+                     vbhem_allreduce_fn allreduce, void *allreduce_ctx, const vbhem_em_ext_t *ext) {
   if (!base || !post_ok(post) || !opt_ok(opt, post->d) || !LogLs || !iters || !L_final ||
       !stable || !stats_dev || post->d != base->d || post->covmode != base->covmode)
     return VBHEM_ERR_ARG;
+  if (ext && ext->rccl_comm && allreduce)
+    return vbhem::set_error(VBHEM_ERR_ARG, "vbhem_em_run_ext: an RCCL communicator and an all-reduce callback");
   const int K = post->K, S = post->S, d = post->d;
   const size_t dd = post->covmode == VBHEM_COV_FULL ? (size_t)d * d : (size_t)d;
   const size_t need = vbhem_em_workspace_bytes(base, K, S, T);
@@ -549,7 +716,7 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!vbhem::em_dev_supported(d, S) || std::getenv("VBHEM_EM_HOST_MATH"))
     return em_run_host(base, tildeN_dev, T, opt, post, LogLs, iters, L_final, stable, stats_dev,
-                       hatZ_dev, LL_dev, workspace_dev, st, allreduce, allreduce_ctx);
+                       hatZ_dev, LL_dev, workspace_dev, st, allreduce, allreduce_ctx, ext);
   vbhem_cluster_t c0 = {K, S, nullptr, nullptr, nullptr, nullptr, nullptr};
   const size_t fused = (vbhem_fused_workspace_bytes(base, &c0, T) + 255) / 256 * 256;
   const size_t nA = (size_t)K * S * S, nPi = (size_t)K * S, nm = (size_t)K * S * d,
@@ -591,10 +758,9 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
   // the bound of iteration j goes straight to pinned, mapped host memory (slot j % 2),
   // followed by a sequence word the host polls: no stream synchronisation per
   // iteration, and the next E-step is already queued behind the bound
-  double *Lh = nullptr, *Ld = nullptr;
-  if (e == hipSuccess)
-    e = hipHostMalloc(reinterpret_cast<void **>(&Lh), 4 * sizeof(double), hipHostMallocMapped);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&Ld), Lh, 0);
+  Mapped mb;
+  if (e == hipSuccess) e = acquire_mapped(mb);
+  double *Lh = mb.h, *Ld = mb.d;
   int *flag_h = Lh ? reinterpret_cast<int *>(Lh + 2) : nullptr;  // two ints after L[2]
   if (flag_h) flag_h[0] = flag_h[1] = 0;
   auto set_post = [&a](const PostDev &in, const PostDev &out) {
@@ -613,10 +779,8 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     rc = vbhem_estep_fused(base, &cl, T, tildeN_dev, dlogOmega, stats_dev, hz[j % 2], ll[j % 2],
                            workspace_dev, fused, st);
     if (rc != VBHEM_OK) return false;
-    if (allreduce && allreduce(stats_dev, slen, st, allreduce_ctx) != 0) {
-      rc = VBHEM_ERR_HIP;
-      return false;
-    }
+    rc = reduce_stats(ext, allreduce, allreduce_ctx, stats_dev, slen, st);
+    if (rc != VBHEM_OK) return false;
     set_post(pd[j % 3], pd[(j + 1) % 3]);
     a.seq = j + 1;
     a.flag = reinterpret_cast<int *>(Ld + 2) + (j % 2);
@@ -635,6 +799,7 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
     if (it + 1 <= opt->max_iter && !enqueue(it + 1)) break;
     e = wait_flag(flag_h + (it % 2), it + 1, st);
     if (e != hipSuccess) break;
+    if (ext && ext->iter_seconds) ext->iter_seconds[it] = now_s();
     L = Lh[it % 2];
     fin_e = it % 2;
     if (std::isnan(L)) {  // step_fc.m:338-374: unstable model, the posterior before the M-step
@@ -661,14 +826,36 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
       e = hipMemcpyAsync(LL_dev, ll[1], (size_t)base->N * K * sizeof(double),
                          hipMemcpyDeviceToDevice, st);
   }
+  // the derivatives (step_fc.m:356-368) are taken at the posterior before the last
+  // M-step: pd[(it - 1) % 3], which neither the last M-step nor the discarded
+  // speculative one ((it + 1) % 3) wrote
+  const bool deriv = ext && ext->calc_deriv && ext->dLL;
+  HostPost pre;
+  if (deriv && *stable && it >= 1) pre.size_like(post);
   if (e == hipSuccess && rc == VBHEM_OK) e = copy_post(post, pd[fin_post], dd, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && rc == VBHEM_OK && deriv && *stable && it >= 1)
+    e = copy_post(&pre.t, pd[(it - 1) % 3], dd, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && rc == VBHEM_OK) e = hipStreamSynchronize(st);
-  if (Lh) (void)hipHostFree(Lh);
+  if (e == hipSuccess) release_mapped(mb);  // a failed stream may still write it: not reused
   if (rc != VBHEM_OK) return rc;
   if (e != hipSuccess) return VBHEM_ERR_HIP;
   *iters = it;
   *L_final = L;
+  if (deriv) {
+    if (*stable && it >= 1) return derivs_at(&pre.t, opt, ext->dLL);
+    nan_derivs(opt, d, ext->dLL);
+  }
   return VBHEM_OK;
+}
+
+int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
+                 const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
+                 double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
+                 double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
+                 vbhem_allreduce_fn allreduce, void *allreduce_ctx) {
+  return vbhem_em_run_ext(base, tildeN_dev, T, opt, post, LogLs, iters, L_final, stable, stats_dev,
+                          hatZ_dev, LL_dev, workspace_dev, workspace_bytes, stream, allreduce,
+                          allreduce_ctx, nullptr);
 }
 
 }  // extern "C"

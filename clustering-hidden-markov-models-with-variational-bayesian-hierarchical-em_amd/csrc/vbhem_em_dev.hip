@@ -16,8 +16,9 @@
 //      sums; the last wave to finish (a ticket counter) reduces all of them in a
 //      fixed order and writes L (deterministic);
 //   2. the M-step of (k, s) into the other posterior buffer: the d x d inverse of
-//      W0^-1 + Nr SC + mult1 dd' by Gauss-Jordan elimination with partial pivoting
-//      in wave-private LDS, lanes = entries of [A | I];
+//      W0^-1 + Nr SC + mult1 dd' by Gauss-Jordan elimination without row exchanges
+//      (the operand is symmetric positive definite; see gauss_jordan) in
+//      wave-private LDS, lanes = entries of [A | I];
 //   3. the prelude of the new (k, s): logLambdaTilde (psi over the lanes, det W by
 //      the same elimination), c, P = v W, m, its logATilde row, logPiTilde and (one
 //      wave per cluster) logOmega -- the sums over a cluster's states or over all

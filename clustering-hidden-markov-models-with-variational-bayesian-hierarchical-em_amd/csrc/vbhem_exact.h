@@ -1,7 +1,7 @@
 // vbhem_exact.h -- the reference-order recursion of one flagged pair (mex.c:715-1298
 // step by step: K1, the backward LSE with stored Theta, termination, the forward sweep),
 // shared by fb_exact_kernel and the kernels that fold the fallback into their prologue
-// (resp_kernel, stats_list_m_kernel).  w: the thread's scratch slot (exact_stride doubles:
+// (resp_kernel, stats_list_m_kernel, through fold_exact).  w: the thread's scratch slot (exact_stride doubles:
 // E, L, Ln, lt, nu, tn [S][SB] each, ls [SB], Theta [T][S][S][SB]).  Internal.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -120,6 +120,35 @@ static __device__ __forceinline__ void exact_pair(const FbArgs &p, int pair, dou
   }
   for (int k = 0; k < S * SB; ++k) p.tnu[lp * S * SB + k] = tn[k];
   for (int k = 0; k < S * S; ++k) p.xi[lp * S * S + k] = xi[k];
+}
+
+// The exact fallback folded into a consumer kernel's prologue (resp_kernel,
+// stats_list_m_kernel): the flagged pairs flag_list[x0, x1) that `mine` accepts are
+// found by the whole block, blockDim entries per round (coalesced), queued in LDS
+// (q [blockDim], *qn), and recomputed by the block's first `nw` threads, thread t on
+// scratch slot slot0 + t -- the block's own slots, so no two threads of the grid
+// share one.  A block whose bases were all flagged (a diverged trial) runs its
+// pairs nw at a time instead of one after another.  Block-uniform: every thread
+// calls it; it ends with a barrier.
+template <class Mine>
+static __device__ __forceinline__ void fold_exact(const FbArgs &fx, int x0, int x1, Mine mine,
+                                                  double *scratch, long long stride, int slot0,
+                                                  int nw, int *q, int *qn) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int b = x0; b < x1; b += nt) {
+    if (tid == 0) *qn = 0;
+    __syncthreads();
+    const int x = b + tid;
+    if (x < x1) {
+      const int pair = fx.flag_list[x];
+      if (mine(pair)) q[atomicAdd(qn, 1)] = pair;
+    }
+    __syncthreads();
+    const int n = *qn;
+    if (tid < nw)
+      for (int y = tid; y < n; y += nw) exact_pair(fx, q[y], scratch + (size_t)(slot0 + tid) * stride);
+    __syncthreads();
+  }
 }
 
 }  // namespace vbhem

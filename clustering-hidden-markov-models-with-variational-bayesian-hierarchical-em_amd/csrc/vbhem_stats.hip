@@ -96,25 +96,26 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   double *accNj = lds;               // [NW*BPW][K]
   double *accLt = accNj + NW * BPW * K;  // [NW][2]
   int *gcnt = reinterpret_cast<int *>(accLt + 2 * NW);  // [K] gated pairs of this chunk
-  for (int x = tid; x < NW * BPW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
-  for (int x = tid; x < K; x += kRespThreads) gcnt[x] = 0;
   int b0, b1;
   chunk_range(p.i_end - p.i_begin, p.i_begin, blockIdx.x, gridDim.x, b0, b1);
-  if (p.fold && tid == 0) {
+  if (p.fold) {
     // the folded fallback (vbhem_internal.h, kFlagHead): the backward pass's flagged
     // pairs of this block's bases get their exact L_elbo (and other outputs) before any
-    // of them is read; block 0 records where the gate-list pass's entries will start
+    // of them is read; block 0 records where the gate-list pass's entries will start.
+    // The block's scratch slots: xslots / gridDim of them (the host folds only when
+    // gridDim <= xslots); the queue borrows the accumulators' LDS before they are set
     int *fc = p.fx.flag_count;
     const int cnt = __atomic_load_n(fc, __ATOMIC_RELAXED);
-    if (blockIdx.x == 0) fc[3] = cnt;
-    if (cnt > 0) {
-      double *w = p.xscratch + (size_t)(blockIdx.x % p.xslots) * p.xstride;
-      for (int x = 0; x < cnt; ++x) {
-        const int pair = p.fx.flag_list[x], i = pair / K;
-        if (i >= b0 && i < b1) exact_pair(p.fx, pair, w);
-      }
+    if (blockIdx.x == 0 && tid == 0) fc[3] = cnt;
+    if (cnt > 0) {  // block-uniform
+      const int nw = min(kRespThreads, max(1, p.xslots / (int)gridDim.x));
+      int *q = reinterpret_cast<int *>(lds), *qn = q + kRespThreads;
+      fold_exact(p.fx, 0, cnt, [&](int pair) { const int i = pair / K; return i >= b0 && i < b1; },
+                 p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn);
     }
   }
+  for (int x = tid; x < NW * BPW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
+  for (int x = tid; x < K; x += kRespThreads) gcnt[x] = 0;
   __syncthreads();
   double l1 = 0.0, l7 = 0.0;
   if (K <= G) {
@@ -865,8 +866,10 @@ size_t resp_lds(int K, int KT) {
   int G = 1;
   while (G < K && G < 64) G <<= 1;
   const size_t R = KT >= 1 && K % KT == 0 ? (size_t)(K / KT) : 1;
-  return ((size_t)(kRespThreads / 64) * ((64 / G) * (size_t)K + 2 * R)) * sizeof(double) +
-         (size_t)K * sizeof(int);
+  // (at least the folded fallback's queue, which borrows this space first)
+  return std::max(((size_t)(kRespThreads / 64) * ((64 / G) * (size_t)K + 2 * R)) * sizeof(double) +
+                      (size_t)K * sizeof(int),
+                  (size_t)(kRespThreads + 1) * sizeof(int));
 }
 
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
@@ -1192,16 +1195,15 @@ __global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const Stats
     // bases lst[n0] .. lst[n1 - 1]) get their exact outputs before they are read
     const int *fc = p.fx.flag_count;
     const int c1 = fc[3], cnt = __atomic_load_n(fc, __ATOMIC_RELAXED);
-    if (cnt > c1) {  // block-uniform
-      if (tid == 0 && n0 < n1) {
-        const int ilo = lst[n0], ihi = lst[n1 - 1];
-        double *w = p.xscratch + (size_t)(blockIdx.x % p.xslots) * p.xstride;
-        for (int x = c1; x < cnt; ++x) {
-          const int pair = p.fx.flag_list[x], i = pair / K;
-          if (pair - i * K == j && i >= ilo && i <= ihi) exact_pair(p.fx, pair, w);
-        }
-      }
-      __syncthreads();
+    if (cnt > c1 && n0 < n1) {  // block-uniform
+      // xslots / gridDim scratch slots per block (the launch caps gridDim at xslots);
+      // the queue sits past the kernel's own LDS
+      const int ilo = lst[n0], ihi = lst[n1 - 1];
+      const int nw = min(64 * kSmWaves, max(1, p.xslots / (int)gridDim.x));
+      int *q = reinterpret_cast<int *>(zs + d), *qn = q + 64 * kSmWaves;
+      fold_exact(p.fx, c1, cnt,
+                 [&](int pair) { const int i = pair / K; return pair - i * K == j && i >= ilo && i <= ihi; },
+                 p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn);
     }
   }
   // one pair's operands: A values per k-slice, B values per (tile, k-slice), its Z and
@@ -1481,7 +1483,9 @@ static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st
 
 template <int NTW, int G, int KSM, int NXR, int PD>
 static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
-  const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double);
+  // (+ the folded fallback's queue: one int per thread and its count)
+  const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double) +
+                     (a.fold ? (64 * kSmWaves + 1) * sizeof(int) : 0);
   auto *fn = &stats_list_m_kernel<NTW, G, KSM, NXR, PD>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;

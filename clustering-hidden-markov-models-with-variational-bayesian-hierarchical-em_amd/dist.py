@@ -33,3 +33,63 @@ def make_allreduce(group=None) -> Callable[[torch.Tensor], None]:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
     return _ar
+
+
+class RcclComm:
+    """A native RCCL communicator for the statistics' all-reduce
+    (include/vbhem_dist.h): the C++ EM loop (``native_em.run(..., comm=...)``)
+    issues ``ncclAllReduce(sum, fp64)`` on its own stream once per E-step, with
+    no Python callback in the loop.  Rank 0 makes the id; it travels to the
+    other ranks over the already-initialised torch.distributed group (one
+    broadcast at set-up).  A world of one rank is allowed (the all-reduce is
+    then a local copy) so the path runs on a one-GPU box too."""
+
+    def __init__(self, device: torch.device, rank: int = None, world: int = None, group=None):
+        import ctypes
+
+        from . import _capi
+        self._lib = _capi.lib()
+        inited = dist.is_available() and dist.is_initialized()
+        self.rank = (dist.get_rank(group) if inited else 0) if rank is None else int(rank)
+        self.world = (dist.get_world_size(group) if inited else 1) if world is None else int(world)
+        self.device = torch.device(device)
+        idb = (ctypes.c_char * _capi.RCCL_ID_BYTES)()
+        err = None
+        if self.rank == 0 and self._lib.vbhem_rccl_unique_id(idb) != 0:
+            err = self._lib.vbhem_last_error().decode(errors="replace")
+        if self.world > 1:
+            # the id (or rank 0's error) reaches every rank, so no rank waits in
+            # ncclCommInitRank for a rank 0 that could not make one
+            obj = [err if err is not None else bytes(idb)]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            if isinstance(obj[0], str):
+                err = obj[0]
+            else:
+                ctypes.memmove(idb, obj[0], _capi.RCCL_ID_BYTES)
+        if err is not None:
+            raise _capi.VbhemError(f"vbhem_rccl_unique_id failed: {err}")
+        h = ctypes.c_void_p()
+        _capi.check(self._lib.vbhem_rccl_comm_init(self.world, self.rank, idb,
+                                                   int(self.device.index or 0), ctypes.byref(h)),
+                    "vbhem_rccl_comm_init")
+        self.handle = h
+
+    def allreduce(self, t: torch.Tensor) -> None:
+        """In-place SUM of a device fp64 vector on the current stream."""
+        from . import _capi
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("RcclComm.allreduce: a contiguous fp64 device tensor")
+        st = torch.cuda.current_stream(t.device).cuda_stream
+        _capi.check(self._lib.vbhem_rccl_allreduce_sum(self.handle, _capi.ptr(t), t.numel(), st),
+                    "vbhem_rccl_allreduce_sum")
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.vbhem_rccl_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass

@@ -36,6 +36,7 @@ class EMResult:
     point: Optional[dict] = None    # convert_h3mrtoh3mb point estimates
     label: Optional[torch.Tensor] = None  # argmax_j hat_Z (0-based), form_outputH3M.m:274-275
     dLL: Optional[dict] = None      # opt['calc_LLderiv']: bound derivatives at the last E-step
+    iter_seconds: Optional[np.ndarray] = None  # native_em.run(timestamps=True): per-iteration clock
 
 
 def tilde_n(engine: EStepEngine, Nv: float, total_N: int) -> torch.Tensor:

@@ -236,6 +236,20 @@ def lower_bound_derivs(logOmega: np.ndarray, post: Posterior, consts: dict, opt:
         d_tr = -v[..., None] * myW0inv ** 2 * dgW
         dLt["W0"] = K * S * (-0.5 * v0 * myW0inv) - 0.5 * d_tr.sum(axis=(0, 1))
     dLt["m0"] = (l0 * v[..., None] * np.einsum("ksab,ksb->ksa", Wf, post.m - m0)).sum(axis=(0, 1))
+    return transform_derivs(dLt, opt, clipped)
+
+
+def transform_derivs(dLt: dict, opt: dict, clipped: dict = None) -> dict:
+    """vbhemh3m_lb.m:326-356 on raw derivatives (alpha0, eta0, epsilon0, v0,
+    lambda0, W0, m0 -- host.lower_bound_derivs or the C++ loop's
+    vbhem_em_lower_bound_derivs): zeroed where a clipped hyperparameter would
+    move further out of range, then taken with respect to the transformed
+    hyperparameters the optimiser works in."""
+    d = len(opt["m0"])
+    a0, e0, ep0, l0, v0 = opt["alpha0"], opt["eta0"], opt["epsilon0"], opt["lambda0"], opt["v0"]
+    W0inv = np.linalg.inv(_W0(opt, d))
+    myW0 = 1.0 / W0inv[0, 0] if np.asarray(opt["W0"]).size == 1 else 1.0 / np.diag(W0inv)
+    dLt = {k: np.array(v, dtype=float) for k, v in dLt.items()}
     if clipped is not None:
         for name, fl in clipped.items():
             g = dLt[name]

@@ -301,19 +301,32 @@ def _minimize(X0, F, length, method, MFEPLS, MSR, mem):
 # vbhem_h3m_c_hyp.m
 # ----------------------------------------------------------------------------
 def vbhem_h3m_c_hyp(base: BaseSet, opt: dict, init_post: Posterior, engine: EStepEngine,
-                    length: Optional[int] = None, learn_hyps=None) -> dict:
+                    length: Optional[int] = None, learn_hyps=None, loop: str = "python") -> dict:
     """Learn the hyperparameters for one trial (vbhem_h3m_c_hyp.m:1-63): L-BFGS
     on -LL over the transformed hyperparameters, each evaluation an EM run from
-    ``init_post`` with its bound derivatives, then a final EM run."""
+    ``init_post`` with its bound derivatives, then a final EM run.
+
+    loop: "python" -- the EM runs on :func:`vbhem_amd.em.vbhem_h3m_c_step_fc`;
+    "native" -- on the C++ loop (``native_em.run``, vbhem_em_run_ext), which
+    computes the derivatives itself (vbhem_em_lower_bound_derivs)."""
     info = hypinfo(opt.get("learn_hyps", 1) if learn_hyps is None else learn_hyps, opt)
     n_eval = [0]
+    if loop == "native":
+        from . import native_em
+
+        def em_run(post, eng, o):
+            return native_em.run(post, eng, o, calc_deriv=bool(o.get("calc_LLderiv", 0)))
+    elif loop == "python":
+        em_run = em.vbhem_h3m_c_step_fc
+    else:
+        raise ValueError("loop must be 'python' or 'native'")
 
     def grad(X):
         o = set_opt(X, opt, info)
         o, flags = clip_hyps(o, with_flags=True)          # vbh3m_grad: vbhem_clip_hyps
         o["hyp_clipped"] = flags
         o["calc_LLderiv"] = 1
-        res = em.vbhem_h3m_c_step_fc(init_post, engine, o)
+        res = em_run(init_post, engine, o)
         n_eval[0] += 1
         L = -res.LL
         dL = np.concatenate([-np.atleast_1d(res.dLL[h.derivname]).reshape(-1) for h in info])
@@ -329,6 +342,6 @@ def vbhem_h3m_c_hyp(base: BaseSet, opt: dict, init_post: Posterior, engine: ESte
                              method=method)
     o2 = set_opt(Xopt, opt, info)
     o2 = clip_hyps(o2)
-    final = em.vbhem_h3m_c_step_fc(init_post, engine, o2)
+    final = em_run(init_post, engine, o2)
     return dict(result=final, opt_transhyp=Xopt, opt_L=-fX[-1], fX=fX, line_searches=nls,
                 evaluations=n_eval[0], vbopt=o2, hypinfo=info)

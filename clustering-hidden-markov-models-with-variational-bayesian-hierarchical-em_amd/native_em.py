@@ -107,26 +107,52 @@ class HostIteration:
         return float(self.L.value)
 
 
+def _workspace(engine: EStepEngine, nb: int) -> torch.Tensor:
+    """The loop's device workspace, kept on the engine and reused by later runs
+    (grown when a run needs more): no allocation on the per-run path."""
+    ws = getattr(engine, "_em_ws", None)
+    if ws is None or ws.numel() < nb:
+        ws = engine._em_ws = torch.empty((nb,), dtype=torch.uint8, device=engine.device)
+    return ws
+
+
 def run(post: Posterior, engine: EStepEngine, opt: dict, *, total_N: Optional[int] = None,
         allreduce: Optional[Callable[[torch.Tensor], None]] = None,
-        max_iter: Optional[int] = None) -> EMResult:
+        max_iter: Optional[int] = None, comm=None, timestamps: bool = False,
+        calc_deriv: bool = False) -> EMResult:
     """The EM loop in C++ on the engine's base set; same result type as
-    :func:`vbhem_amd.em.vbhem_h3m_c_step_fc`."""
+    :func:`vbhem_amd.em.vbhem_h3m_c_step_fc`.
+
+    comm:       a :class:`vbhem_amd.dist.RcclComm`: the loop all-reduces the packed
+                statistics with RCCL on its own stream (no callback); exclusive
+                with ``allreduce`` (a Python hook the loop calls once per E-step).
+    timestamps: ``res.iter_seconds`` = the host clock at which each iteration's
+                bound reached the host (the loop's own per-iteration timing).
+    calc_deriv: ``res.dLL`` = the bound derivatives of the last accepted iteration
+                (vbhemh3m_lb.m:202-356, before its M-step; computed by the C++
+                loop), in the form of :func:`vbhem_amd.em.vbhem_h3m_c_step_fc`'s
+                (``opt["hyp_clipped"]`` applied); NaN when the run is unstable."""
     from .em import tilde_n
     covmode = engine.base.covmode
     total_N = engine.N if total_N is None else int(total_N)
     opt = dict(opt)
     if max_iter is not None:
         opt["max_iter"] = int(max_iter)
+    if comm is not None and allreduce is not None:
+        raise ValueError("native_em.run: give comm or allreduce, not both")
     pb, ob = _PostBuf(post, covmode), _OptBuf(opt)
     K, S = pb.t.K, pb.t.S
+    d = pb.a["m"].shape[2]
     tN = tilde_n(engine, opt["Nv"], total_N).contiguous()
     lib = _capi.lib()
     nb = int(lib.vbhem_em_workspace_bytes(ctypes.byref(engine._bt), K, S, engine.T))
     if nb == 0:
         raise _capi.VbhemError("vbhem_em_workspace_bytes: unsupported shape")
-    ws = torch.empty((nb,), dtype=torch.uint8, device=engine.device)
+    ws = _workspace(engine, nb)
     LogLs = np.zeros(int(opt["max_iter"]) + 1)
+    tsec = np.zeros(int(opt["max_iter"]) + 1) if timestamps else None
+    nW = int(ob.W0.size)
+    dLL = np.zeros(5 + nW + d) if calc_deriv else None
     iters, L, stable = ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
     stats = engine.stats
 
@@ -138,18 +164,51 @@ def run(post: Posterior, engine: EStepEngine, opt: dict, *, total_N: Optional[in
             return 1
 
     cb = _capi.ALLREDUCE_FN(_ar) if allreduce is not None else _capi.ALLREDUCE_FN()
-    rc = lib.vbhem_em_run(ctypes.byref(engine._bt), _capi.ptr(tN), engine.T, ctypes.byref(ob.t),
-                          ctypes.byref(pb.t), _p(LogLs), ctypes.byref(iters), ctypes.byref(L),
-                          ctypes.byref(stable), _capi.ptr(stats), _capi.ptr(engine.hatZ),
-                          _capi.ptr(engine.LL), _capi.ptr(ws), ws.numel(), engine._stream(), cb,
-                          None)
-    _capi.check(rc, "vbhem_em_run")
+    ext = _capi.EmExtT(comm.handle if comm is not None else None,
+                       _p(tsec) if tsec is not None else None, 1 if calc_deriv else 0,
+                       _p(dLL) if dLL is not None else None)
+    rc = lib.vbhem_em_run_ext(ctypes.byref(engine._bt), _capi.ptr(tN), engine.T, ctypes.byref(ob.t),
+                              ctypes.byref(pb.t), _p(LogLs), ctypes.byref(iters), ctypes.byref(L),
+                              ctypes.byref(stable), _capi.ptr(stats), _capi.ptr(engine.hatZ),
+                              _capi.ptr(engine.LL), _capi.ptr(ws), ws.numel(), engine._stream(), cb,
+                              None, ctypes.byref(ext))
+    _capi.check(rc, "vbhem_em_run_ext")
     it = int(iters.value)
     res = EMResult(post=pb.posterior(), LogLs=[float(x) for x in LogLs[:it]], LL=float(L.value),
                    iters=it, stable=bool(stable.value), hatZ=engine.hatZ.clone(),
                    L_elbo=engine.LL.clone(), Nj=None, syn=None)
+    if tsec is not None:
+        res.iter_seconds = tsec[:max(it, 1) if not res.stable else it].copy()
+    if dLL is not None:
+        from . import host
+        raw = _raw_dict(dLL, nW)
+        # as em.vbhem_h3m_c_step_fc: clipped and transformed (step_fc.m:356-360), or
+        # NaN when the run ended unstable (:362-368)
+        tr = host.transform_derivs(raw, opt, opt.get("hyp_clipped"))
+        res.dLL = tr if res.stable else {k: np.full_like(np.atleast_1d(v), np.nan)
+                                         for k, v in tr.items() if k != "raw"}
     if res.stable:
         from . import host
         res.point = host.convert_to_point(res.post, covmode)
         res.label = torch.argmax(res.hatZ, dim=1)
     return res
+
+
+def _raw_dict(g: np.ndarray, nW: int) -> dict:
+    return {"alpha0": g[0:1].copy(), "eta0": g[1:2].copy(), "epsilon0": g[2:3].copy(),
+            "v0": g[3:4].copy(), "lambda0": g[4:5].copy(), "W0": g[5:5 + nW].copy(),
+            "m0": g[5 + nW:].copy()}
+
+
+def lower_bound_derivs(post: Posterior, opt: dict, covmode: int) -> dict:
+    """vbhem_em_lower_bound_derivs at a posterior (its prelude computed in C++):
+    the raw derivatives, keyed as host.lower_bound_derivs(...)["raw"]."""
+    pb, ob = _PostBuf(post, covmode), _OptBuf(opt)
+    pre = prelude(post, covmode)
+    d = pb.a["m"].shape[2]
+    nW = int(ob.W0.size)
+    g = np.zeros(5 + nW + d)
+    _capi.check(_capi.lib().vbhem_em_lower_bound_derivs(
+        ctypes.byref(pb.t), ctypes.byref(ob.t), _p(pre["logLambdaTilde"]), _p(pre["logA"]),
+        _p(pre["logPi"]), _p(pre["logOmega"]), _p(g)), "vbhem_em_lower_bound_derivs")
+    return _raw_dict(g, nW)

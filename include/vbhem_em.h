@@ -13,6 +13,7 @@
 
 #include <stddef.h>
 
+#include "vbhem_dist.h"
 #include "vbhem_estep.h"
 
 #ifdef __cplusplus
@@ -93,6 +94,39 @@ int vbhem_em_run(const vbhem_base_t *base, const double *tildeN_dev, int T,
                  double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
                  double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
                  vbhem_allreduce_fn allreduce, void *allreduce_ctx);
+
+/* Number of raw bound derivatives (vbhem_em_lower_bound_derivs): alpha0, eta0,
+ * epsilon0, v0, lambda0, W0[W0_len], m0[d]. */
+#define VBHEM_DLL_LEN(d, W0_len) (5 + (W0_len) + (d))
+
+/* Optional extensions of vbhem_em_run (zero-initialise, set what is used). */
+typedef struct {
+  /* RCCL communicator (include/vbhem_dist.h): the packed statistics are SUM
+   * all-reduced in-stream after every E-step run, in the loop itself (no host
+   * callback; the callback must then be NULL). */
+  void *rccl_comm;
+  /* [max_iter + 1] or NULL: host steady-clock seconds at which each accepted
+   * iteration's bound reached the host (the loop's own per-iteration clock). */
+  double *iter_seconds;
+  /* vbhemh3m_lb.m:202-345 (calc_LLderiv, vbhem_h3m_c_step_fc.m:356-368): raw
+   * derivatives of the last accepted iteration's bound, taken before its M-step,
+   * into dLL [VBHEM_DLL_LEN(d, W0_len)]; all NaN when the run ends unstable. */
+  int calc_deriv;
+  double *dLL;
+} vbhem_em_ext_t;
+
+int vbhem_em_run_ext(const vbhem_base_t *base, const double *tildeN_dev, int T,
+                     const vbhem_em_opt_t *opt, vbhem_post_t *post, double *LogLs, int *iters,
+                     double *L_final, int *stable, double *stats_dev, double *hatZ_dev,
+                     double *LL_dev, void *workspace_dev, size_t workspace_bytes, void *stream,
+                     vbhem_allreduce_fn allreduce, void *allreduce_ctx, const vbhem_em_ext_t *ext);
+
+/* vbhemh3m_lb.m:202-345: the raw derivatives of the bound with respect to the
+ * hyperparameters (posterior held fixed; no clipping, no change of variables --
+ * vbhem_amd/hyp.py applies :326-356), from the posterior and its prelude outputs. */
+int vbhem_em_lower_bound_derivs(const vbhem_post_t *post, const vbhem_em_opt_t *opt,
+                                const double *logLambdaTilde, const double *logA,
+                                const double *logPi, const double *logOmega, double *dLL);
 
 #ifdef __cplusplus
 }

@@ -33,6 +33,10 @@ def main(src, out):
                 b = json.loads(line)
                 res.update(N=b["config"]["N"], n_gpus=b["n_gpus"], workload=b["config"]["workload"],
                            bench_under_trace=b)
+    pa = os.path.join(src, "pmc_args.txt")
+    if os.path.exists(pa):  # scripts/profile.sh: PMC passes without shard-size launches
+        res["pmc_args"] = open(pa).read().strip()
+        res["pmc_full_size_only"] = "--no-shard-sim" in res["pmc_args"]
     stats = glob.glob(os.path.join(src, "trace", "*_kernel_stats.csv"))
     if stats:
         with open(stats[0]) as f:

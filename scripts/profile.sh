@@ -8,11 +8,18 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 ARGS="$@"
+# the PMC passes run the full-size E-steps only (no shard simulation, no EM-loop
+# timing): every launch of a kernel then has the same size and the per-dispatch
+# averages are the full-size launch's counters (prof_summary.py records this)
+PMC_ARGS="--no-shard-sim --em-iters 0 --no-parity-sample --steps 6 --warmup 2"
 run() {  # name, extra rocprof args
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline $ARGS > $OUT/$name.log 2>&1
+  local extra=$ARGS
+  case $name in pmc*) extra="$ARGS $PMC_ARGS";; esac
+  timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline $extra > $OUT/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc"; return $rc
 }
+echo "$PMC_ARGS" > $OUT/pmc_args.txt
 run trace --kernel-trace --stats || exit $?
 [ "$PASSES" = trace ] && exit 0
 run pmc1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE &&

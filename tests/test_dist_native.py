@@ -64,7 +64,7 @@ def _worker(rank, name, N, world, outdir, port, iters):
     _run(name, N, world, rank, outdir, port, iters)
 
 
-@pytest.mark.parametrize("name,N", [("C3", 2000), ("C4", 1000)])
+@pytest.mark.parametrize("name,N", [("C3", 2000), ("C4", 1000), ("C4", 1003)])
 def test_native_em_two_ranks_gloo(tmp_path, name, N):
     import torch.multiprocessing as mp
     iters = 4

@@ -204,3 +204,14 @@ def test_c5_multigroup_vs_oracle(vb, vo, monkeypatch):
     statistics accumulated into the same slabs."""
     monkeypatch.setenv("VBHEM_GROUP_BASES", "6000")
     assert _full_size_vs_oracle(vb, vo, "C5", N=20_000, chunk=1000) == 20_000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 6, 7, 9, 15, 16, 17, 31, 33, 125, 250, 333, 500, 501])
+def test_c4_shard_sizes_vs_oracle(vb, vo, N):
+    """C4 shapes (S = Sb = 8, T = 10: fb_bwd4_kernel and fb_list4_kernel, the MFMA
+    kernels) at base counts of every residue class that matters to them -- a quad
+    is 4 bases, a block's tile 16 -- up to the 500 / 501-base shards of a two-rank
+    run: every pair, hat_Z entry and statistic against the oracle.  (Regression
+    for the mid-round-3 two-rank C4 failure)"""
+    assert _full_size_vs_oracle(vb, vo, "C4", N=N, chunk=512, nthreads=8) == N

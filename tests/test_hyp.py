@@ -183,3 +183,63 @@ def test_hyp_learning_run(vb):
     assert out["result"].LL >= L0 - 1e-6 * abs(L0)
     assert out["evaluations"] >= 2
     del torch
+
+
+@pytest.mark.parametrize("cov,W0", [(1, 0.7), (1, [0.4, 0.9, 1.3]), (0, 0.25), (0, [0.3, 0.5, 2.0])],
+                         ids=["full-iid", "full-diagW0", "diag-iid", "diag-diagW0"])
+def test_native_derivatives_match_host(vb, cov, W0):
+    """vbhem_em_lower_bound_derivs (C++, the loop's calc_LLderiv) against
+    host.lower_bound_derivs (itself checked against finite differences and the
+    oracle above): raw derivatives at 1e-12."""
+    from vbhem_amd import native_em
+    cs = make_case(6, 4, 3, 3, 3, cov, seed=29, tau=5, W0=W0, m0=[0.2, -0.4, 0.8])
+    opt = dict(cs["opt"])
+    P, consts = cs["P"], cs["consts"]
+    logOm = vb.host.log_omega_tilde(P.alpha)
+    ref = vb.host.lower_bound_derivs(logOm, P, consts, opt, cov)["raw"]
+    got = native_em.lower_bound_derivs(P, opt, cov)
+    for k, v in ref.items():
+        np.testing.assert_allclose(got[k], np.atleast_1d(v), rtol=1e-12, atol=1e-12, err_msg=k)
+    # the clipping / change of variables is shared with the Python path
+    tr = vb.host.transform_derivs(got, opt)
+    full = vb.host.lower_bound_derivs(logOm, P, consts, opt, cov)
+    for k in ("d_logalpha0", "d_logv0D1", "d_logW0", "d_m0"):
+        np.testing.assert_allclose(tr[k], full[k], rtol=1e-12, atol=1e-12, err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cov", [1, 0])
+def test_native_loop_derivatives_match_python_loop(vb, cov):
+    """calc_LLderiv on the C++ loop (vbhem_em_run_ext: the posterior before the last
+    M-step kept on the device, derivatives in C++) equals the Python loop's."""
+    from vbhem_amd import em, native_em
+    from vbhem_amd.estep import EStepEngine
+    cs = make_case(60, 3, 3, 2, 2, cov, seed=41 + cov, tau=10, W0=1.0, m0=[1.5, 1.5])
+    opt = dict(cs["opt"], max_iter=30, minDiff=1e-7, calc_LLderiv=1)
+    eng = EStepEngine(cs["bs"], 3, 3, 10, device="cuda:0")
+    ref = em.vbhem_h3m_c_step_fc(cs["P"], eng, opt)
+    got = native_em.run(cs["P"], eng, opt, calc_deriv=True)
+    assert got.iters == ref.iters and got.stable and ref.stable
+    for k, v in ref.dLL.items():
+        if k == "raw":
+            continue
+        np.testing.assert_allclose(np.atleast_1d(got.dLL[k]), np.atleast_1d(v), rtol=1e-10,
+                                   atol=1e-9, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_hyp_learning_native_loop_matches_python_loop(vb):
+    """vbhem_h3m_c_hyp with every evaluation on the C++ loop (loop='native') follows
+    the Python-loop run: same line searches, bounds and hyperparameters."""
+    from vbhem_amd import em, hyp
+    from vbhem_amd.estep import EStepEngine
+    cs = make_case(40, 3, 3, 2, 2, 1, seed=5, tau=10, W0=1.0, m0=[1.5, 1.5])
+    opt = dict(cs["opt"], max_iter=200, minDiff=1e-10, learn_hyps=1)
+    eng = EStepEngine(cs["bs"], 3, 3, 10, device="cuda:0")
+    start = em.vbhem_h3m_c_step_fc(cs["P"], eng, opt)
+    a = hyp.vbhem_h3m_c_hyp(cs["bs"], opt, start.post, eng, length=6, loop="python")
+    b = hyp.vbhem_h3m_c_hyp(cs["bs"], opt, start.post, eng, length=6, loop="native")
+    assert a["evaluations"] == b["evaluations"] and a["line_searches"] == b["line_searches"]
+    np.testing.assert_allclose(b["fX"], a["fX"], rtol=1e-10)
+    np.testing.assert_allclose(b["opt_transhyp"], a["opt_transhyp"], rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(b["result"].LL, a["result"].LL, rtol=1e-10)

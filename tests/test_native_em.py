@@ -135,3 +135,81 @@ def test_host_iteration_matches_steps(vb, vo, name, cov, S):
     assert np.isnan(hi(bad))
     for k, v in before.items():
         assert np.array_equal(hi.pb.a[k], v, equal_nan=True), k
+
+
+@pytest.mark.gpu
+def test_native_em_timestamps_and_reused_buffers(vb):
+    """vbhem_em_run_ext's per-iteration host clock: one stamp per accepted
+    iteration, increasing; repeated runs on one engine reuse its workspace (no
+    per-run allocation) and give identical results."""
+    from vbhem_amd import native_em
+    from vbhem_amd.estep import EStepEngine
+    cs = make_case(300, 4, 3, 3, 2, 1, seed=33, tau=8)
+    opt = dict(cs["opt"], max_iter=6, minDiff=0.0)
+    eng = EStepEngine(cs["bs"], 4, 3, 8, device="cuda:0")
+    r1 = native_em.run(cs["P"], eng, opt, timestamps=True)
+    ws = eng._em_ws
+    r2 = native_em.run(cs["P"], eng, opt, timestamps=True)
+    assert eng._em_ws is ws
+    assert r1.iters == r2.iters == 7 and r1.LogLs == r2.LogLs
+    for r in (r1, r2):
+        t = r.iter_seconds
+        assert t.shape == (r.iters,) and np.all(np.diff(t) > 0) and t[0] > 0
+
+
+@pytest.mark.gpu
+def test_native_em_rccl_one_rank(vb):
+    """The in-loop RCCL all-reduce (RcclComm, vbhem_rccl_*) on a one-rank
+    communicator: the statistics pass through ncclAllReduce every E-step and the
+    run equals the run without a collective bit for bit."""
+    import torch
+    from vbhem_amd import native_em
+    from vbhem_amd.dist import RcclComm
+    from vbhem_amd.estep import EStepEngine
+    cs = make_case(300, 4, 3, 3, 2, 1, seed=34, tau=8)
+    opt = dict(cs["opt"], max_iter=5)
+    eng = EStepEngine(cs["bs"], 4, 3, 8, device="cuda:0")
+    ref = native_em.run(cs["P"], eng, opt)
+    comm = RcclComm(torch.device("cuda", 0), rank=0, world=1)
+    try:
+        got = native_em.run(cs["P"], eng, opt, comm=comm)
+        x = torch.arange(10, dtype=torch.float64, device="cuda:0")
+        comm.allreduce(x)
+        torch.cuda.synchronize()
+        assert torch.equal(x, torch.arange(10, dtype=torch.float64, device="cuda:0"))
+    finally:
+        comm.close()
+    assert got.iters == ref.iters and got.LogLs == ref.LogLs
+    for k in ("alpha", "eta", "epsilon", "lam", "v", "m", "W"):
+        assert np.array_equal(getattr(got.post, k), getattr(ref.post, k)), k
+    with pytest.raises(ValueError):
+        native_em.run(cs["P"], eng, opt, comm=comm, allreduce=lambda t: None)
+
+
+@pytest.mark.gpu
+def test_native_em_unstable_device_path(vb, monkeypatch):
+    """A NaN bound on the device EM path (the next iteration already queued): the
+    run stops unstable with L = -inf, the posterior is the one before the failing
+    iteration's M-step, and hat_Z is that iteration's -- as the host-math path
+    (VBHEM_EM_HOST_MATH) gives."""
+    import torch
+    from vbhem_amd import native_em
+    from vbhem_amd.estep import EStepEngine
+    cs = make_case(200, 3, 3, 3, 2, 1, seed=35, tau=6)
+    P = cs["P"].copy()
+    P.alpha[0] = np.nan          # logOmega NaN -> every bound NaN from iteration 0
+    opt = dict(cs["opt"], max_iter=5)
+    eng = EStepEngine(cs["bs"], 3, 3, 6, device="cuda:0")
+    dev = native_em.run(P, eng, opt, calc_deriv=True)
+    hz_dev = dev.hatZ.clone()
+    monkeypatch.setenv("VBHEM_EM_HOST_MATH", "1")
+    host = native_em.run(P, eng, opt, calc_deriv=True)
+    for r in (dev, host):
+        assert not r.stable and r.LL == -np.inf and r.iters == 0 and r.LogLs == []
+        assert all(np.isnan(np.atleast_1d(v)).all() for v in r.dLL.values())
+    for k in ("eta", "epsilon", "lam", "v", "m", "W"):
+        assert np.array_equal(getattr(dev.post, k), getattr(P, k)), k
+        assert np.array_equal(getattr(host.post, k), getattr(P, k)), k
+    assert torch.equal(torch.isnan(hz_dev), torch.isnan(host.hatZ))
+    torch.testing.assert_close(torch.nan_to_num(hz_dev), torch.nan_to_num(host.hatZ), rtol=1e-12,
+                               atol=0)
