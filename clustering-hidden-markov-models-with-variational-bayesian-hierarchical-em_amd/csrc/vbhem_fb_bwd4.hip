@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "vbhem_internal.h"
 #include "vbhem_mfma4.h"
@@ -47,6 +48,28 @@
 #define VBHEM_BWD4_QPW 1     // quads (of 4 pairs) per wavefront
 #endif
 
+// Step-loop variants (A/B switches; the defaults are the measured best):
+//   VBHEM_BWD4_BIGLOG   the log from an 8192-interval table ({1/c, -log(1/c)}, 128 KB
+//                       of LDS: one 16-wave block per CU) with log1p to second order
+//                       (|r| <= 2^-14: the dropped r^3/3 <= 7.6e-14), two fp64
+//                       operations less per element and step than the 1024-interval
+//                       table's third-order series
+//   VBHEM_BWD4_DECOUPLE column maxima rounded down to a multiple of ln 2 (M = k ln2):
+//                       the exp table index n mod 2048 no longer depends on the maximum,
+//                       so its LDS read issues right after the range reduction, beside
+//                       the cross-lane maximum chain instead of after it
+//   VBHEM_BWD4_ZSAFE    no per-step underflow test of Z for a cluster whose A' entries
+//                       are all >= 2^-600 (Z >= min A' G_max >= 2^-601 > 2^-665 always)
+#ifndef VBHEM_BWD4_BIGLOG
+#define VBHEM_BWD4_BIGLOG 0
+#endif
+#ifndef VBHEM_BWD4_DECOUPLE
+#define VBHEM_BWD4_DECOUPLE 0
+#endif
+#ifndef VBHEM_BWD4_ZSAFE
+#define VBHEM_BWD4_ZSAFE 0
+#endif
+
 namespace vbhem {
 
 namespace {
@@ -54,7 +77,11 @@ namespace {
 constexpr int kQPW = VBHEM_BWD4_QPW;
 constexpr int kWaves = VBHEM_BWD4_WAVES;
 #ifndef VBHEM_BWD4_NWB
+#if VBHEM_BWD4_BIGLOG
+#define VBHEM_BWD4_NWB 16   // one block per CU: the 144 KB of tables once per CU
+#else
 #define VBHEM_BWD4_NWB 4
+#endif
 #endif
 // waves per block (the 32 KB of tables once per block; LDS then allows 4 blocks per CU):
 // 5 waves per SIMD (VBHEM_BWD4_WAVES=5, NWB=10, with the lane geometry recomputed per
@@ -63,16 +90,120 @@ constexpr int kWaves = VBHEM_BWD4_WAVES;
 constexpr int kNWB = VBHEM_BWD4_NWB;
 constexpr int kPPW = 4 * kQPW;      // pairs per wavefront (one tile)
 using namespace m4;
+
+// the 8192-interval log table, {1/c, -log(1/c)} with c the centre of [1 + k/8192,
+// 1 + (k+1)/8192) and 1/c rounded to a double (the table need not hold 1/c exactly:
+// log zz = -log(ic) + log1p(zz ic - 1) for any ic), staged per block with the
+// device's correctly rounded division and libm-accurate log
+__device__ __forceinline__ void stage_log8k(double *ltab, int tid, int nt) {
+  for (int k = tid; k < 8192; k += nt) {
+    const double c = 1.0 + ((double)k + 0.5) * (1.0 / 8192.0);
+    const double ic = 1.0 / c;
+    ltab[2 * k] = ic;
+    ltab[2 * k + 1] = -log(ic);
+  }
+}
+
+// log(Z) + M, 8192-interval table, log1p(r) = r - r^2/2 (|r| <= 2^-14): kk = the
+// binary exponent of Z plus the maximum's term (integer, exact), then one fma
+template <int N, bool DEC>
+__device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
+                                        const double *ltab) {
+  double zz[N], ic[N], w[N];
+  unsigned one_hi = 0x3ff00000u;
+  asm("" : "+v"(one_hi));
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const unsigned hi = (unsigned)__double2hiint(z[x]);
+    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
+    unsigned ex = hi >> 20;
+    asm("" : "+v"(ex));
+    const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
+    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    const double2 e = *reinterpret_cast<const double2 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 3) & 0x1fff0u), 16));
+    ic[x] = e.x;
+    w[x] = fma((double)kk, DEC ? 0x1.62e42fefa39efp-1 : kLn2N, e.y);
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double r = fma(zz[x], ic[x], -1.0);
+    const double h = fma(r, -0.5, 1.0);
+    y[x] = fma(r, h, w[x]);
+  }
+}
+
+// log(Z) + M with the 1024-interval table (m4::log_m_n's series) for the decoupled
+// maxima: kk = exponent + the maximum's multiple of ln 2
+template <int N>
+__device__ __forceinline__ void log_d_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
+                                        const double *ltab) {
+  double zz[N], ic[N], w[N];
+  unsigned one_hi = 0x3ff00000u;
+  asm("" : "+v"(one_hi));
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const unsigned hi = (unsigned)__double2hiint(z[x]);
+    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
+    const int kk = (int)(hi >> 20) + wq[x];
+    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    const double2 e = *reinterpret_cast<const double2 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 6) & 0x3ff0u), 16));
+    ic[x] = e.x;
+    w[x] = fma((double)kk, 0x1.62e42fefa39efp-1, e.y);
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double sh = fma(zz[x], ic[x], -0.5);
+    const double s2 = sh * sh;
+    const double q = fma(sh, 4.0 / 3.0, -1.0);
+    y[x] = fma(fma(q, s2, sh), 2.0, w[x]);
+  }
+}
+
+// exp(V - M) for M = (h - 2^20) ln 2, h = the column maximum of lo(s) >> 11: the table
+// index is lo(s) mod 2048 (independent of M), the scale 2^(lo(s) >> 11 - h) clamped
+// below at 2^-1010 (wph = h - 1010): table scaled by 2^-1010, exponent added
+template <int N>
+__device__ __forceinline__ void exp_d_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
+                                        const double (&t)[N], const unsigned (&wph)[N]) {
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
+    const double pp = fma(0.5 * r, r, r);
+    const double m = fma(t[x], pp, t[x]);
+    unsigned e = __builtin_elementwise_sub_sat(lo_u(s[x]) >> 11, wph[x]);
+    asm("" : "+v"(e));
+    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
+  }
+}
+__device__ __forceinline__ double etab_at(const double *etab, double s) {
+  return *reinterpret_cast<const double *>(
+      __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & 0x3ff8u), 8));
+}
 }  // namespace
 
 __global__ __launch_bounds__(64 * kNWB) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void fb_bwd4_kernel(const SplitArgs p) {
   constexpr int S = 8;
+#if VBHEM_BWD4_BIGLOG
+  // one array, the exp table first: both tables' LDS offsets then fit the 16-bit
+  // offset field of ds_read (no address add per lookup)
+  __shared__ __attribute__((aligned(16))) double tabs[2048 + 2 * 8192];
+  double *const etab = tabs;                 // 2^(i/2048 - 1010)
+  double *const ltab8 = tabs + 2048;         // {1/c, -log(1/c)}
+#else
   __shared__ __attribute__((aligned(16))) double etab[2048];      // 2^(i/2048 - 1010)
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];  // {1/(2c), -log(1/c)}
+#endif
   __shared__ double amax[S], lpi[S];
   const int tid = threadIdx.x;
+#if VBHEM_BWD4_BIGLOG
+  for (int x = tid; x < 2048; x += 64 * kNWB) etab[x] = kExpTab4[x] * 0x1p-1010;
+  stage_log8k(ltab8, tid, 64 * kNWB);
+#else
   stage_tables(etab, ltab, tid, 64 * kNWB);
+#endif
   const int SB = p.SB, K = p.K, T = p.T;
   // persistent: NB blocks per cluster; XCD-aware when NB % 8 == 0 (as fb_bwd2_kernel)
   const int bk = blockIdx.x, NB = (int)gridDim.x / K;
@@ -109,11 +240,27 @@ void fb_bwd4_kernel(const SplitArgs p) {
   bool cl_nf = false;
 #pragma unroll
   for (int x = 0; x < S; ++x) cl_nf |= isnan(amax[x]) || isnan(lpi[x]);
+#if VBHEM_BWD4_ZSAFE
+  // the lanes hold the 64 entries of A' between them: a wave minimum (once per block)
+  bool zsafe;
+  {
+    double am = fmin(fmin(AT[0][0], AT[0][1]), fmin(AT[1][0], AT[1][1]));
+    for (int o = 32; o >= 1; o >>= 1) am = fmin(am, __shfl_xor(am, o, 64));
+    zsafe = am >= 0x1p-600;  // NaN: not safe
+  }
+  zsafe = __builtin_amdgcn_readfirstlane((int)zsafe) != 0;
+#else
+  constexpr bool zsafe = false;
+#endif
   // ds_bpermute sources of the log's column maxima (Q layout: column 4J + r)
   const int qsrc0 = (0 * 16 + 4 * b + r) << 2, qsrc1 = (1 * 16 + 4 * b + r) << 2;
   const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
   const double vlim = kVMax / (double)T - 3.0;
 
+  // the tile loop, versioned on the underflow test (ZS: the cluster's A' makes it
+  // unnecessary, VBHEM_BWD4_ZSAFE)
+  auto tiles = [&](auto zs_tag) {
+  constexpr bool ZS = decltype(zs_tag)::value;
   const int ntile = (p.i_end - p.i_begin + kPPW - 1) / kPPW;
   for (int tile = wave * NB + t0; tile < ntile; tile += NB * kNWB) {
     const int i0 = p.i_begin + tile * kPPW;
@@ -163,8 +310,45 @@ void fb_bwd4_kernel(const SplitArgs p) {
     // (column maxima -> exp -> MFMA -> log -> MFMA)
     for (int t = T - 1; t >= 1; --t) {
       double s[kQPW][2][2];
-      unsigned wp[kQPW][2];
       int mq[kQPW][2];
+      constexpr int NE = 4 * kQPW;  // elements per lane: (q, I, J) flattened
+      double G[kQPW][2][2];
+#if VBHEM_BWD4_DECOUPLE
+      // table values first (they do not need the maxima), then the maxima chain
+      double tv[NE];
+      unsigned wph[kQPW][2];
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q)
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) s[q][i2][jj] = red_s(V[q][i2][jj]);
+#pragma unroll
+      for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, s[x / 4][(x / 2) % 2][x % 2]);
+#pragma unroll
+      for (int q = 0; q < kQPW; ++q) {
+        const unsigned w = colmax_rows(max(lo_u(s[q][0][0]), lo_u(s[q][1][0])),
+                                       max(lo_u(s[q][0][1]), lo_u(s[q][1][1]))) >> 11;
+        const int wq = (int)w - (1 << 20) - 1023;
+        mq[q][0] = __builtin_amdgcn_ds_bpermute(qsrc0, wq);
+        mq[q][1] = __builtin_amdgcn_ds_bpermute(qsrc1, wq);
+        split_rows(w - 1010u, wph[q][0], wph[q][1]);
+      }
+      {
+        double vv[NE], sf[NE], gg[NE];
+        unsigned wpf[NE];
+#pragma unroll
+        for (int x = 0; x < NE; ++x) {
+          vv[x] = V[x / 4][(x / 2) % 2][x % 2];
+          sf[x] = s[x / 4][(x / 2) % 2][x % 2];
+          wpf[x] = wph[x / 4][x % 2];
+        }
+        exp_d_n<NE>(gg, vv, sf, tv, wpf);
+#pragma unroll
+        for (int x = 0; x < NE; ++x) G[x / 4][(x / 2) % 2][x % 2] = gg[x];
+      }
+#else
+      unsigned wp[kQPW][2];
 #pragma unroll
       for (int q = 0; q < kQPW; ++q) {
 #pragma unroll
@@ -178,8 +362,6 @@ void fb_bwd4_kernel(const SplitArgs p) {
         mq[q][1] = __builtin_amdgcn_ds_bpermute(qsrc1, wq);
         split_rows(w - kBias, wp[q][0], wp[q][1]);
       }
-      constexpr int NE = 4 * kQPW;  // elements per lane: (q, I, J) flattened
-      double G[kQPW][2][2];
       {
         double vv[NE], sf[NE], gg[NE];
         unsigned wpf[NE];
@@ -193,6 +375,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
         for (int x = 0; x < NE; ++x) G[x / 4][(x / 2) % 2][x % 2] = gg[x];
       }
+#endif
       // Z^T block (J, I') = sum_K G^T(J, K) A'^T(K, I'); G^T(J, K) is V's block (K, J)
       double Z[kQPW][2][2];
 #pragma unroll
@@ -216,11 +399,19 @@ void fb_bwd4_kernel(const SplitArgs p) {
           zf[x] = Z[x / 4][(x / 2) % 2][x % 2];
           wqf[x] = mq[x / 4][(x / 2) % 2];
         }
+        if constexpr (!ZS) {
 #pragma unroll
-        for (int q = 0; q < kQPW; ++q)
-          zmin[q] = min(zmin[q], min(min(__double2hiint(zf[4 * q]), __double2hiint(zf[4 * q + 1])),
-                                     min(__double2hiint(zf[4 * q + 2]), __double2hiint(zf[4 * q + 3]))));
+          for (int q = 0; q < kQPW; ++q)
+            zmin[q] = min(zmin[q], min(min(__double2hiint(zf[4 * q]), __double2hiint(zf[4 * q + 1])),
+                                       min(__double2hiint(zf[4 * q + 2]), __double2hiint(zf[4 * q + 3]))));
+        }
+#if VBHEM_BWD4_BIGLOG
+        log_q_n<NE, VBHEM_BWD4_DECOUPLE != 0>(yf, zf, wqf, ltab8);
+#elif VBHEM_BWD4_DECOUPLE
+        log_d_n<NE>(yf, zf, wqf, ltab);
+#else
         log_m_n<NE>(yf, zf, wqf, ltab);
+#endif
 #pragma unroll
         for (int x = 0; x < NE; ++x) sv[x / 4][(x / 2) % 2][x % 2] = yf[x];
       }
@@ -271,7 +462,11 @@ void fb_bwd4_kernel(const SplitArgs p) {
       {
         const double zsf[1] = {zs};
         const int wqf[1] = {(int)(w + kWq0)};
+#if VBHEM_BWD4_BIGLOG
+        log_q_n<1, false>(lse1, zsf, wqf, ltab8);
+#else
         log_m_n<1>(lse1, zsf, wqf, ltab);
+#endif
       }
       const double lse = lse1[0];
       const int be = 4 * (r & 1) + c;
@@ -297,6 +492,9 @@ void fb_bwd4_kernel(const SplitArgs p) {
       }
     }
   }
+  };
+  if (zsafe) tiles(std::true_type{});
+  else tiles(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------
