@@ -590,7 +590,10 @@ def main():
                               "ELBO partials, the all-reduce and the copy to the host; outputs "
                               "equal the dense schedule's (dense_schedule.max_rel_diff_vs_gated)"),
         "gated_pairs_frac": n_gated / float(N * K),
-        "gated_forward": ({"kernel": f"vbhem::fb_split_kernel<{S}, {lpc}, 2>", "kernel_ms": gf_ms,
+        "gated_forward": ({"kernel": ("vbhem::fb_list4_kernel<10>" if S == 8 and Sb <= 8 and T == 10
+                                      and not os.environ.get("VBHEM_NO_LIST4")
+                                      else f"vbhem::fb_split_kernel<{S}, {lpc}, 2>"),
+                           "kernel_ms": gf_ms,
                            "pairs_per_launch": n_gated / world,
                            "flops_per_pair": fb_flops_per_pair(S, Sb, T),
                            "achieved_TFLOPs": fb_flops_per_pair(S, Sb, T) * n_gated / world

@@ -48,7 +48,8 @@
 #define VBHEM_BWD4_QPW 1     // quads (of 4 pairs) per wavefront
 #endif
 
-// Step-loop variants (A/B switches; the defaults are the measured best):
+// Step-loop variants (A/B switches; the defaults are the measured best -- all three on:
+// 1.553 -> 1.496 ms per C4 launch on one box, gpurun_out r04a A/B):
 //   VBHEM_BWD4_BIGLOG   the log from an 8192-interval table ({1/c, -log(1/c)}, 128 KB
 //                       of LDS: one 16-wave block per CU) with log1p to second order
 //                       (|r| <= 2^-14: the dropped r^3/3 <= 7.6e-14), two fp64
@@ -61,13 +62,13 @@
 //   VBHEM_BWD4_ZSAFE    no per-step underflow test of Z for a cluster whose A' entries
 //                       are all >= 2^-600 (Z >= min A' G_max >= 2^-601 > 2^-665 always)
 #ifndef VBHEM_BWD4_BIGLOG
-#define VBHEM_BWD4_BIGLOG 0
+#define VBHEM_BWD4_BIGLOG 1
 #endif
 #ifndef VBHEM_BWD4_DECOUPLE
-#define VBHEM_BWD4_DECOUPLE 0
+#define VBHEM_BWD4_DECOUPLE 1
 #endif
 #ifndef VBHEM_BWD4_ZSAFE
-#define VBHEM_BWD4_ZSAFE 0
+#define VBHEM_BWD4_ZSAFE 1
 #endif
 
 namespace vbhem {

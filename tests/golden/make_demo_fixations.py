@@ -1,8 +1,11 @@
 """Generates tests/golden/demo_fixations.npz: the fixation sequences of the
-reference's demo/demodata.xls as read by vbhem_amd.xls.read_xls_fixations
-(read_xls_fixations.m semantics), flattened: x [sum T][2], offsets [n_trials+1],
-subject index per trial, and the subject / trial names.  Run in a container
-that has /root/reference mounted:
+reference's demo/demodata.xls, flattened: x [sum T][2], offsets [n_trials+1],
+subject index per trial, and the subject / trial names.
+
+The cells come from tests/golden/biff_cells.py, a minimal compound-file + BIFF8
+walker written separately from vbhem_amd/xls.py (the reader the fixture checks),
+with the row loop of read_xls_fixations.m:84-138.  Run in a container that has
+/root/reference mounted:
 
     python tests/golden/make_demo_fixations.py
 """
@@ -11,17 +14,14 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, ROOT)
-import pkgload  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import biff_cells  # noqa: E402
 
 SRC = "/root/reference/demo/demodata.xls"
 
 
 def main():
-    vb = pkgload.load()
-    from vbhem_amd.xls import read_xls_fixations
-    data, names, trials = read_xls_fixations(SRC)
+    data, names, trials = biff_cells.read_fixations(SRC)
     seqs = [t for subj in data for t in subj]
     subj = np.array([s for s, subjd in enumerate(data) for _ in subjd], dtype=np.int32)
     off = np.zeros(len(seqs) + 1, dtype=np.int32)
@@ -29,7 +29,6 @@ def main():
     np.savez_compressed(os.path.join(os.path.dirname(__file__), "demo_fixations.npz"),
                         x=np.concatenate(seqs), offsets=off, subject=subj,
                         names=np.array(names), trials=np.array([t for tr in trials for t in tr]))
-    del vb
 
 
 if __name__ == "__main__":

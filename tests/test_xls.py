@@ -3,17 +3,25 @@ place of xlsread) and the demo's data path into the VB-HMM forward-backward.
 
 CPU: RK-number and shared-string decoding on hand-built records; the reference's
 demo/demodata.xls (when /root/reference is mounted) against the committed
-fixture tests/golden/demo_fixations.npz (made by make_demo_fixations.py).
+fixture tests/golden/demo_fixations.npz.  The fixture is made by
+make_demo_fixations.py from tests/golden/biff_cells.py, a second reader written
+separately from vbhem_amd/xls.py (compound file + SST/LABELSST/NUMBER/RK/MULRK
+only), so the check is not circular; both readers also decode the same
+hand-built records.
 GPU: the demo's 399 fixation sequences through vbhmm_fb (C1's first stage)
 against the oracle restatement of vbhmm_fb_mex.c."""
 import os
 import struct
+import sys
 
 import numpy as np
 import pytest
 
 import vbhem_oracle as vo
 from conftest import GOLDEN_DIR, rel_err
+
+sys.path.insert(0, GOLDEN_DIR)
+import biff_cells  # noqa: E402  (the independent reader; test infrastructure)
 
 DEMO = "/root/reference/demo/demodata.xls"
 
@@ -33,6 +41,31 @@ def test_sst_with_continue(vb):
     rec = struct.pack("<II", 2, 2) + struct.pack("<HB", len(s1), 0) + s1[:4].encode()
     cont = bytes([1]) + s1[4:].encode("utf-16-le") + struct.pack("<HB", len(s2), 0) + s2.encode()
     assert _read_sst([rec, cont]) == [s1, s2]
+
+
+def test_independent_reader_decodes_the_same(vb):
+    """biff_cells (the fixture's reader) on the hand-built inputs above."""
+    assert biff_cells._rk_value((123 << 2) | 2) == 123.0
+    assert biff_cells._rk_value((123 << 2) | 3) == 1.23
+    assert biff_cells._rk_value((((1 << 30) - 5) << 2) | 2) == -5.0
+    hi = struct.unpack("<Q", struct.pack("<d", 2.5))[0] >> 32
+    assert biff_cells._rk_value(hi) == 2.5
+    s1, s2 = "SubjectID", "FixX"
+    rec = struct.pack("<II", 2, 2) + struct.pack("<HB", len(s1), 0) + s1[:4].encode()
+    cont = bytes([1]) + s1[4:].encode("utf-16-le") + struct.pack("<HB", len(s2), 0) + s2.encode()
+    assert biff_cells._shared_strings([rec, cont]) == [s1, s2]
+
+
+def test_fixture_from_independent_reader(vb):
+    """The committed fixture is what biff_cells reads from the demo file."""
+    if not os.path.exists(DEMO):
+        pytest.skip("reference demo data not mounted")
+    fx = np.load(os.path.join(GOLDEN_DIR, "demo_fixations.npz"))
+    data, names, trials = biff_cells.read_fixations(DEMO)
+    seqs = [t for subj in data for t in subj]
+    np.testing.assert_array_equal(np.concatenate(seqs), fx["x"])
+    assert list(names) == list(fx["names"])
+    assert [t for tr in trials for t in tr] == list(fx["trials"])
 
 
 def test_demo_file_matches_fixture(vb):
