@@ -515,6 +515,9 @@ def main():
     if gated and S == 8 and Sb <= 8 and not os.environ.get("VBHEM_NO_BWD4") \
             and not os.environ.get("VBHEM_NO_BWD2"):
         kname = "vbhem::fb_bwd4_kernel"   # MFMA contractions (S = 8)
+    elif gated and S == 12 and Sb <= 12 and not os.environ.get("VBHEM_NO_BWD12") \
+            and not os.environ.get("VBHEM_NO_BWD2"):
+        kname = "vbhem::fb_bwd12_kernel"  # MFMA contractions (S = 12)
     elif gated and S <= 16 and not os.environ.get("VBHEM_NO_BWD2"):
         kname = f"vbhem::fb_bwd2_kernel<{S}>"
     else:

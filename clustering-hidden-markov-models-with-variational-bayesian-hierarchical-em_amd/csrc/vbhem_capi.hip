@@ -396,6 +396,7 @@ struct FbCtx {
   // the backward-only pass on fb_bwd2_kernel (S <= 8): LDS bytes, pairs per block
   size_t bwd2_lds = 0;
   int bwd2_ppb = 0, bwd2_nwb = 0;
+  bool bwd12 = false;  // S = 12, SB <= 12: fb_bwd12_kernel (MFMA contractions) instead
   bool bwd4 = false;  // S = 8, SB <= 8: fb_bwd4_kernel (MFMA contractions) instead
   bool list4 = false;  // S = 8, SB <= 8, T = 10: fb_list4_kernel for the gate-list pass
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
@@ -448,6 +449,7 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
       c.bwd2_lds = vbhem::bwd2_lds(cl->S, c.bwd2_nwb);
       c.bwd2_ppb = vbhem::bwd2_ppb(cl->S, c.bwd2_nwb);
       c.bwd4 = vbhem::bwd4_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD4");
+      c.bwd12 = vbhem::bwd12_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD12");
       c.list4 = vbhem::list4_supported(cl->S, b->SB, T, cl->K) && !std::getenv("VBHEM_NO_LIST4");
     }
   }
@@ -579,6 +581,15 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       if (nb >= 8) nb = nb / 8 * 8;
       e = vbhem::launch_bwd4(ca, (unsigned)ca.K * nb, st);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd4_kernel");
+    } else if (mode == vbhem::kFbBackward && c.bwd12) {
+      // fb_bwd12_kernel, persistent: NB blocks per cluster (x8 when possible)
+      const int ppb = vbhem::bwd12_ppb();
+      const unsigned nt12 = (unsigned)((i_end - i_begin + ppb - 1) / ppb);
+      const unsigned all = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::bwd12_resident_blocks()));
+      unsigned nb = std::max(1u, std::min(nt12, all / (unsigned)ca.K));
+      if (nb >= 8) nb = nb / 8 * 8;
+      e = vbhem::launch_bwd12(ca, (unsigned)ca.K * nb, st);
+      if (e != hipSuccess) return hip_fail(e, "fb_bwd12_kernel");
     } else if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
       ca.nwb = c.bwd2_nwb;

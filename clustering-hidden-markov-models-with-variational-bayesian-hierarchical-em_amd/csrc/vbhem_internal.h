@@ -283,6 +283,11 @@ int bwd4_waves();            // waves per block
 int bwd4_ppb();              // pairs per block (one tile per wavefront)
 int bwd4_resident_blocks();  // per CU
 hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st);
+// fb_bwd12_kernel (vbhem_fb_bwd12.hip): the same pass for S = 12, SB <= 12 (3 x 3 blocks)
+bool bwd12_supported(int S, int SB);
+int bwd12_ppb();              // pairs per block (one quad per wavefront)
+int bwd12_resident_blocks();  // per CU
+hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st);
 
 // fb_list4_kernel (vbhem_fb_list4.hip): the gate-list pass for S = 8, SB <= 8, T = 10
 // with every contraction on v_mfma_f64_4x4x4f64; SplitArgs fields as fb_split_kernel's

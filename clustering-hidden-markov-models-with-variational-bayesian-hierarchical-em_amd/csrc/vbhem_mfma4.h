@@ -167,5 +167,97 @@ __device__ __forceinline__ void stage_tables(double *etab, double *ltab, int tid
   }
 }
 
+// ---- the round-4 step helpers (fb_bwd4_kernel, fb_bwd12_kernel) ----
+// the 8192-interval log table, {1/c, -log(1/c)} with c the centre of [1 + k/8192,
+// 1 + (k+1)/8192) and 1/c rounded to a double (the table need not hold 1/c exactly:
+// log zz = -log(ic) + log1p(zz ic - 1) for any ic), staged per block with the
+// device's correctly rounded division and libm-accurate log
+__device__ __forceinline__ void stage_log8k(double *ltab, int tid, int nt) {
+  for (int k = tid; k < 8192; k += nt) {
+    const double c = 1.0 + ((double)k + 0.5) * (1.0 / 8192.0);
+    const double ic = 1.0 / c;
+    ltab[2 * k] = ic;
+    ltab[2 * k + 1] = -log(ic);
+  }
+}
+
+// log(Z) + M, 8192-interval table, log1p(r) = r - r^2/2 (|r| <= 2^-14): kk = the
+// binary exponent of Z plus the maximum's term (integer, exact), then one fma
+template <int N, bool DEC>
+__device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
+                                        const double *ltab) {
+  double zz[N], ic[N], w[N];
+  unsigned one_hi = 0x3ff00000u;
+  asm("" : "+v"(one_hi));
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const unsigned hi = (unsigned)__double2hiint(z[x]);
+    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
+    unsigned ex = hi >> 20;
+    asm("" : "+v"(ex));
+    const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
+    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    const double2 e = *reinterpret_cast<const double2 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 3) & 0x1fff0u), 16));
+    ic[x] = e.x;
+    w[x] = fma((double)kk, DEC ? 0x1.62e42fefa39efp-1 : kLn2N, e.y);
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double r = fma(zz[x], ic[x], -1.0);
+    const double h = fma(r, -0.5, 1.0);
+    y[x] = fma(r, h, w[x]);
+  }
+}
+
+// log(Z) + M with the 1024-interval table (m4::log_m_n's series) for the decoupled
+// maxima: kk = exponent + the maximum's multiple of ln 2
+template <int N>
+__device__ __forceinline__ void log_d_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
+                                        const double *ltab) {
+  double zz[N], ic[N], w[N];
+  unsigned one_hi = 0x3ff00000u;
+  asm("" : "+v"(one_hi));
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const unsigned hi = (unsigned)__double2hiint(z[x]);
+    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
+    const int kk = (int)(hi >> 20) + wq[x];
+    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    const double2 e = *reinterpret_cast<const double2 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 6) & 0x3ff0u), 16));
+    ic[x] = e.x;
+    w[x] = fma((double)kk, 0x1.62e42fefa39efp-1, e.y);
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double sh = fma(zz[x], ic[x], -0.5);
+    const double s2 = sh * sh;
+    const double q = fma(sh, 4.0 / 3.0, -1.0);
+    y[x] = fma(fma(q, s2, sh), 2.0, w[x]);
+  }
+}
+
+// exp(V - M) for M = (h - 2^20) ln 2, h = the column maximum of lo(s) >> 11: the table
+// index is lo(s) mod 2048 (independent of M), the scale 2^(lo(s) >> 11 - h) clamped
+// below at 2^-1010 (wph = h - 1010): table scaled by 2^-1010, exponent added
+template <int N>
+__device__ __forceinline__ void exp_d_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
+                                        const double (&t)[N], const unsigned (&wph)[N]) {
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
+    const double pp = fma(0.5 * r, r, r);
+    const double m = fma(t[x], pp, t[x]);
+    unsigned e = __builtin_elementwise_sub_sat(lo_u(s[x]) >> 11, wph[x]);
+    asm("" : "+v"(e));
+    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
+  }
+}
+__device__ __forceinline__ double etab_at(const double *etab, double s) {
+  return *reinterpret_cast<const double *>(
+      __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & 0x3ff8u), 8));
+}
+
 }  // namespace m4
 }  // namespace vbhem

@@ -1502,6 +1502,9 @@ static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t
   return hipGetLastError();
 }
 
+#ifndef VBHEM_SM_PDD
+#define VBHEM_SM_PDD 2   // the ring depth (build switch for A/B)
+#endif
 // ring depth 2 (C4: 0.177 ms of statistics per step against 0.191 with depth 4 and
 // its 768 resident blocks); VBHEM_SM_PD=3 (A/B) for the one-pair-group variant
 template <int NTW, int G, int KSM, int NXR>
@@ -1510,7 +1513,7 @@ static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st
     if (const char *ev = std::getenv("VBHEM_SM_PD"))
       if (std::atoi(ev) == 3) return launch_sm_pd<NTW, G, KSM, NXR, 3>(a, grid, st);
   }
-  return launch_sm_pd<NTW, G, KSM, NXR, 2>(a, grid, st);
+  return launch_sm_pd<NTW, G, KSM, NXR, VBHEM_SM_PDD>(a, grid, st);
 }
 
 // the sum_nu_1 | sum_xi chunks per wave: ceil(ceil((S + S^2) / 64) / tile groups)

@@ -11,7 +11,7 @@ for rep in 1 2; do
   for lib in tree "$@"; do
     if [ "$lib" = tree ]; then unset VBHEM_LIB_PATH; else export VBHEM_LIB_PATH=$(realpath $lib); fi
     timeout -k 10 200 python bench.py $ARGS $EXTRA > gpurun_out/ab.json 2>&1 || { tail -5 gpurun_out/ab.json; exit 1; }
-    tail -1 gpurun_out/ab.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); ps=d.get('parity_sample') or {}; print('$lib', 'ms',round(d['ms_per_step'],4),'bwd',round(d['roofline']['kernel_ms'],4),'fwd',round(d['gated_forward']['kernel_ms'],4),'stats',round(d['stats_kernels_ms_per_step'],4),'em',round(d['emission_kernel_ms'],4), 'LLerr', ps.get('LL_elbo_max_rel_err'), 'hzerr', ps.get('hat_Z_max_err'))"
+    tail -1 gpurun_out/ab.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); ps=d.get('parity_sample') or {}; print('$lib', 'ms',round(d['ms_per_step'],4),'bwd',round(d['roofline']['kernel_ms'],4),'fwd',round(d['gated_forward']['kernel_ms'],4),'stats',round(d['stats_kernels_ms_per_step'],4),'em',round(d['emission_kernel_ms'],4), 'LLerr', ps.get('LL_elbo_max_rel_err'), 'hzerr', ps.get('hat_Z_max_err'), 'gated_vs_dense', d['dense_schedule']['max_rel_diff_vs_gated'])"
   done
 done
 unset VBHEM_LIB_PATH

@@ -72,6 +72,11 @@ SHAPES = [
     # states (SB < 8, ragged) and gate lists that end inside a 4-pair quad
     ("S8_ragged", 9, 5, 8, 6, 3, 1, 10, True),
     ("S8_quads", 37, 4, 8, 8, 2, 0, 10, False),
+    # S = 12: the MFMA backward pass on 3 x 3 blocks (fb_bwd12_kernel); SB < 12 pads
+    # whole and partial column blocks, a quad ending past the last base
+    ("S12_ragged", 9, 5, 12, 9, 3, 1, 10, True),
+    ("S12_quads", 37, 4, 12, 12, 2, 0, 10, False),
+    ("S12_sb5", 7, 3, 12, 5, 2, 1, 6, False),
     # outside the column-split kernel's limits (S <= 16, SB <= S, d <= 16): generic kernel
     ("d20", 3, 2, 3, 3, 20, 1, 5, False),
     ("S20", 2, 2, 20, 20, 2, 1, 4, False),

@@ -199,18 +199,19 @@ def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}])
-def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch):
-    """The adversarial cluster at S = Sb = 8, T = 10: its pairs underflow in the MFMA
-    backward pass (fb_bwd4_kernel) and, being gated, again in the MFMA gate-list pass
-    (fb_list4_kernel); both passes' flags reach the exact fallback (folded into the
-    consumers, or two fb_exact_kernel launches)."""
+@pytest.mark.parametrize("S", [8, 12])
+def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch, S):
+    """The adversarial cluster at S = Sb = 8 (12), T = 10: its pairs underflow in the
+    MFMA backward pass (fb_bwd4_kernel / fb_bwd12_kernel) and, being gated, again in
+    the gate-list pass (fb_list4_kernel / fb_split_kernel); both passes' flags reach
+    the exact fallback (folded into the consumers, or two fb_exact_kernel launches)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     N, K = 41, 2
-    cs, consts = adversarial_case(1, S=8, Sb=8, d=3, N=N, K=K, T=10)
+    cs, consts = adversarial_case(1, S=S, Sb=S, d=3, N=N, K=K, T=10)
     consts["c"][1:] = 1.0e4
     base, T = cs["base"], cs["T"]
-    S, d = 8, 3
+    d = 3
     pairs = vo.c_estep_pairs(base, consts, T)
     tN = 100.0 * N * base["omega"]
     logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
