@@ -123,6 +123,7 @@ EXPORTS = {
                                   ctypes.POINTER(EmExtT)]),
     "vbhem_em_lower_bound_derivs": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp,
                                              _vp, _vp, _vp, _vp]),
+    "vbhem_hmms_to_h3m": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_vp] * 15),
     "vbhem_rccl_unique_id": (_c_int, [_vp]),
     "vbhem_rccl_comm_init": (_c_int, [_c_int, _c_int, _vp, _c_int, ctypes.POINTER(_vp)]),
     "vbhem_rccl_comm_destroy": (_c_int, [_vp]),

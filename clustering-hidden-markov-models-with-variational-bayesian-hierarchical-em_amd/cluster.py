@@ -29,7 +29,8 @@ from scipy.special import gammaln
 
 from . import em
 from .estep import EStepEngine
-from .h3m import COV_FULL, BaseSet, baseem_draws, baseem_init, default_options, hmms_to_h3m_hem
+from .h3m import (COV_FULL, BaseSet, baseem_draws, baseem_init, default_options, hmms_to_h3m_hem,
+                  hmms_to_h3m_hem_device)
 
 
 def unique_ll(LLall: Sequence[float], diffthresh: float) -> List[int]:
@@ -133,7 +134,10 @@ def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda
         from .vbhmm_em import vbhmm_remove_empty
         if opt.get("remove_empty", 1):
             hmms = [vbhmm_remove_empty(h, 1e-3) if h is not None else None for h in hmms]
-        base = hmms_to_h3m_hem(hmms, COV_FULL, use_post=True)
+        if opt.get("convert_on_device", 0) and torch.device(device).type == "cuda":
+            base = hmms_to_h3m_hem_device(hmms, COV_FULL, True, device)  # csrc/vbhem_h3m.hip
+        else:
+            base = hmms_to_h3m_hem(hmms, COV_FULL, use_post=True)
     if len(Ks) > 1:
         outs = [vbhem_h3m_cluster(None, k, Ss, dict(opt), device, base, engine_factory) for k in Ks]
         LLk = np.array([o["LL"] for o in outs]) + gammaln(np.array(Ks) + 1.0)

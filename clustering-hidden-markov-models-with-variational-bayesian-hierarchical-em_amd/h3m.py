@@ -4,7 +4,8 @@
   layout the device E-step consumes (include/vbhem_estep.h).
 * :class:`Posterior` -- the K cluster HMMs' variational parameters ``h3m_r``
   (eta, epsilon, lambda, v, m, W per cluster; alpha over clusters).
-* :func:`hmms_to_h3m_hem` -- src/vbhem/hmms_to_h3m_hem.m:1-144.
+* :func:`hmms_to_h3m_hem` -- src/vbhem/hmms_to_h3m_hem.m:1-144 (host), and
+  :func:`hmms_to_h3m_hem_device` -- the same conversion as a HIP kernel.
 * :func:`baseem_init` -- the 'baseem' initialisation of
   src/vbhem/vbhemhmm_init.m:58-100 with the random draws injected.
 * :func:`synth_workload` -- the synthetic (N, K, S, d) grids of BASELINE.md.
@@ -146,6 +147,62 @@ def hmms_to_h3m_hem(hmms: List[Optional[dict]], covmode: int = COV_FULL,
     omega = omega / omega.sum()
     return BaseSet.from_numpy(dict(nstates=ns, prior=prior, A=A, centres=cen, covars=cov,
                                    omega=omega, covmode=covmode))
+
+
+def hmms_to_h3m_hem_device(hmms: List[Optional[dict]], covmode: int = COV_FULL,
+                           use_post: bool = True, device="cuda") -> BaseSet:
+    """:func:`hmms_to_h3m_hem` with the conversion on the device
+    (vbhem_hmms_to_h3m, csrc/vbhem_h3m.hip): the HMM list is packed into padded
+    arrays of the raw variational counts, point estimates, means and covariances
+    here, uploaded once, and the digamma / exp / inflation / weights run as a
+    kernel; the BaseSet comes back on ``device``."""
+    import ctypes
+
+    from . import _capi
+    nin = next(len(h["pdf"][0]["mean"]) for h in hmms if h is not None)
+    N, d = len(hmms), nin
+    SB = max(len(h["prior"]) if h is not None else 1 for h in hmms)
+    ns = np.zeros(N, dtype=np.int32)
+    al, be = np.ones((N, SB)), np.ones((N, SB))
+    ep = np.ones((N, SB, SB))
+    pr, tr = np.zeros((N, SB)), np.zeros((N, SB, SB))
+    mu, cv = np.zeros((N, SB, d)), np.zeros((N, SB, d, d))
+    for j, h in enumerate(hmms):
+        if h is None:
+            continue
+        S = len(h["prior"])
+        ns[j] = S
+        if use_post:
+            al[j, :S] = h["varpar"]["alpha"]
+            ep[j, :S, :S] = h["varpar"]["epsilon"]
+            be[j, :S] = h["varpar"]["beta"]
+        else:
+            pr[j, :S] = h["prior"]
+            tr[j, :S, :S] = h["trans"]
+        for st in range(S):
+            mu[j, st] = h["pdf"][st]["mean"]
+            cv[j, st] = h["pdf"][st]["cov"]
+    dev = torch.device(device)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)
+    ins = dict(ns=torch.as_tensor(ns, device=dev), al=t(al), ep=t(ep), be=t(be), pr=t(pr), tr=t(tr),
+               mu=t(mu), cv=t(cv))
+    out = dict(prior=torch.empty((N, SB), dtype=torch.float64, device=dev),
+               A=torch.empty((N, SB, SB), dtype=torch.float64, device=dev),
+               centres=torch.empty((N, SB, d), dtype=torch.float64, device=dev),
+               covars=torch.empty((N, SB, d, d) if covmode == COV_FULL else (N, SB, d),
+                                  dtype=torch.float64, device=dev),
+               omega=torch.empty((N,), dtype=torch.float64, device=dev))
+    ws = torch.zeros((1,), dtype=torch.int32, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = _capi.ptr
+    _capi.check(_capi.lib().vbhem_hmms_to_h3m(
+        N, SB, d, int(covmode), 1 if use_post else 0, p(ins["ns"]), p(ins["al"]), p(ins["ep"]),
+        p(ins["be"]), p(ins["pr"]), p(ins["tr"]), p(ins["mu"]), p(ins["cv"]), p(out["prior"]),
+        p(out["A"]), p(out["centres"]), p(out["covars"]), p(out["omega"]), p(ws), st),
+        "vbhem_hmms_to_h3m")
+    nstates = torch.as_tensor(np.maximum(ns, 1), dtype=torch.int32, device=dev)
+    return BaseSet(nstates, out["prior"], out["A"], out["centres"], out["covars"], out["omega"],
+                   int(covmode))
 
 
 # ----------------------------------------------------------------------------

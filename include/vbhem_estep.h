@@ -91,6 +91,23 @@ typedef struct {
 size_t vbhem_prepare_base_bytes(const vbhem_base_t *base);
 int vbhem_prepare_base(const vbhem_base_t *base, double *U_dev, size_t bytes, void *stream);
 
+/* src/vbhem/hmms_to_h3m_hem.m:42-140 on the device: N learned VB-HMMs, zero-padded
+ * to SB states, into the base-set arrays above.  Inputs (device): nstates [N] (0 =
+ * an empty entry, which becomes a one-state dummy HMM with weight 0), the variational
+ * counts alpha [N][SB], epsilon [N][SB][SB], beta [N][SB] (use_post = 1: prior =
+ * exp(psi(alpha) - psi(sum alpha)), A rows likewise from epsilon, covariances times
+ * (beta + 1) / beta) or the point estimates prior_in [N][SB], trans_in [N][SB][SB]
+ * (use_post = 0), the means centres_in [N][SB][d] and FULL covariances
+ * covars_in [N][SB][d][d] (diag mode keeps their diagonals).  Outputs: prior, A,
+ * centres, covars (layout of covmode) and omega [N] = 1 / (number of non-empty
+ * entries) or 0.  workspace: 4 bytes of device memory.  Replaces the MATLAB host loop
+ * the reference runs once per vbhem_h3m_cluster call (vbhem_h3m_cluster.m:237). */
+int vbhem_hmms_to_h3m(int N, int SB, int d, int covmode, int use_post, const int *nstates,
+                      const double *alpha, const double *epsilon, const double *beta,
+                      const double *prior_in, const double *trans_in, const double *centres_in,
+                      const double *covars_in, double *prior, double *A, double *centres,
+                      double *covars, double *omega, void *workspace, void *stream);
+
 /* Per-pair outputs of the reference MEX (mex.c:396-409), laid out [N][K][...]:
  *   LL_elbo [N][K]; sum_nu_1 [N][K][S]; emit_pr [N][K][S]; emit_mu [N][K][S][d];
  *   emit_Mu [N][K][S][d][d] (full) | [N][K][S][d] (diag); sum_xi [N][K][S][S].

@@ -209,3 +209,18 @@ def test_synth_workload_shards_consistent(vb, N):
             np.testing.assert_array_equal(getattr(P0, k), getattr(Pu, k))
     np.testing.assert_allclose((b0.omega.sum() + b1.omega.sum()).item(), 1.0, rtol=1e-13)
     assert torch.equal(b0.omega, b1.omega)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cov", [0, 1])
+@pytest.mark.parametrize("use_post", [True, False])
+def test_hmms_to_h3m_hem_device(vb, vo, cov, use_post):
+    """hmms_to_h3m_hem.m on the device (vbhem_hmms_to_h3m, csrc/vbhem_h3m.hip) against
+    the oracle's restatement: ragged state counts, an empty entry (weight 0, the
+    one-state dummy), 1e-13 (the device psi / exp against SciPy's)."""
+    hmms = random_vbhmms(40, 5, 3, seed=6, with_none=True)
+    got = vb.h3m.hmms_to_h3m_hem_device(hmms, covmode=cov, use_post=use_post, device="cuda:0").numpy()
+    ref = vo.hmms_to_h3m_hem(hmms, cov, use_post=use_post)
+    for k in ("nstates", "prior", "A", "centres", "covars", "omega"):
+        np.testing.assert_allclose(got[k], ref[k], rtol=1e-13, atol=0, err_msg=k)
+    assert got["omega"][1] == 0.0 and abs(got["omega"].sum() - 1) < 1e-15
