@@ -232,14 +232,17 @@ def main():
     # all-reduced in-stream by the C++ EM loop and by the E-steps below; torch's
     # process group then only carries the barriers and the timing maxima
     rccl, rccl_err = None, None
-    if world > 1 and backend == "nccl" and not os.environ.get("VBHEM_BENCH_NO_RCCL"):
+    # (VBHEM_BENCH_RCCL_ONE: a one-rank communicator on a one-GPU run, to rehearse the path)
+    if ((world > 1 and backend == "nccl") or os.environ.get("VBHEM_BENCH_RCCL_ONE")) \
+            and not os.environ.get("VBHEM_BENCH_NO_RCCL"):
         from vbhem_amd.dist import RcclComm
         try:
             rccl = RcclComm(dev)
         except Exception as ex:  # noqa: BLE001 -- reported, then torch's RCCL path
             rccl_err = repr(ex)
         ok = torch.tensor([0.0 if rccl is None else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if ok.item() < 1.0 and rccl is not None:
             rccl.close()
             rccl = None
@@ -255,7 +258,7 @@ def main():
     def launch(k):
         """Enqueue E-step k: statistics into pinned host buffer k % 2, then an event."""
         hs = hbufs[k % 2]
-        if world == 1 and not os.environ.get("VBHEM_BENCH_COPY"):
+        if world == 1 and rccl is None and not os.environ.get("VBHEM_BENCH_COPY"):
             eng.fused(tN, out=hs)
         else:
             st = eng.fused(tN)

@@ -83,6 +83,10 @@ __device__ __forceinline__ double group_sum(double v, int G) {
   return v;
 }
 
+#ifndef VBHEM_RESP_UNROLL
+#define VBHEM_RESP_UNROLL 1   // base steps of a wave unrolled (build switch for A/B)
+#endif
+
 // G = lanes per base (power of two >= K, <= 64): 64/G bases per wavefront step.
 __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
   extern __shared__ double lds[];
@@ -127,13 +131,11 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
     int ii = i < b1 ? i : b0;
     double tn = p.tildeN[ii];
     double ll = gl < K ? p.LL[(size_t)ii * K + gl] : 0.0;
-    for (; i - sub < b1; i += stride) {
+    // one base step: hat_Z, Z and the sums of base ib (valid when ib < b1)
+    auto step = [&](int ib, double tnb, double llb) {
 #pragma clang fp contract(off)
-      const bool iv = i < b1;
-      const int in = i + stride < b1 ? i + stride : b0;
-      const double tn_n = p.tildeN[in];
-      const double ll_n = gl < K ? p.LL[(size_t)in * K + gl] : 0.0;
-      const double lz = tn * (lo + ll);  // rounded before the shift (see below)
+      const bool iv = ib < b1;
+      const double lz = tnb * (lo + llb);  // rounded before the shift (see below)
       double mx = gl < K ? lz : -INFINITY;
       mx = group_max(mx, G);
       double sm = gl < K ? exp(lz - mx) : 0.0;
@@ -141,17 +143,40 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
       const double lse = mx + log(sm);
       if (iv && gl < K) {
         const double hz = exp(lz - lse) + 1e-50;
-        const double Z = hz * tn;
-        p.hatZ[(size_t)i * K + gl] = hz;
-        p.Z[(size_t)(i - p.i_buf0) * K + gl] = Z;
+        const double Z = hz * tnb;
+        p.hatZ[(size_t)ib * K + gl] = hz;
+        p.Z[(size_t)(ib - p.i_buf0) * K + gl] = Z;
         accNj[(wave * BPW + sub) * K + gl] += Z;
         if (Z > kGateZ) atomicAdd(&gcnt[gl], 1);
-        l1 += Z * ll;
+        l1 += Z * llb;
         l7 += hz * log(hz);
       }
+    };
+#if VBHEM_RESP_UNROLL == 2
+    // two base steps per iteration: their chains (group max, exp, group sum, log)
+    // interleave; the sums still take base i before base i + stride
+    for (; i - sub < b1; i += 2 * stride) {
+      const int i2 = i + stride, i2c = i2 < b1 ? i2 : b0;
+      const int in = i + 2 * stride < b1 ? i + 2 * stride : b0;
+      const double tn2 = p.tildeN[i2c];
+      const double ll2 = gl < K ? p.LL[(size_t)i2c * K + gl] : 0.0;
+      const double tn_n = p.tildeN[in];
+      const double ll_n = gl < K ? p.LL[(size_t)in * K + gl] : 0.0;
+      step(i, tn, ll);
+      step(i2, tn2, ll2);
       tn = tn_n;
       ll = ll_n;
     }
+#else
+    for (; i - sub < b1; i += stride) {
+      const int in = i + stride < b1 ? i + stride : b0;
+      const double tn_n = p.tildeN[in];
+      const double ll_n = gl < K ? p.LL[(size_t)in * K + gl] : 0.0;
+      step(i, tn, ll);
+      tn = tn_n;
+      ll = ll_n;
+    }
+#endif
   } else
   for (int i = b0 + wave * BPW + sub; i - sub < b1; i += NW * BPW) {
     // log_Z = tilde_N .* (logOmega + L_elbo) is rounded before the shift, as in

@@ -8,8 +8,8 @@ rc=$?; tail -3 $OUT/tests.log
 # ordinary test failures (rc 1) do not stop the measurements; a crash, abort or time
 # limit does
 [ $rc -gt 1 ] && exit $rc
-timeout -k 10 600 bash scripts/ab_lib.sh build/ab/pd3.so build/ab/pd4.so > $OUT/ab_c4.txt 2>&1; cat $OUT/ab_c4.txt
-timeout -k 10 600 bash scripts/ab_lib.sh --args "--steps 20 --warmup 3 --N 12500" build/ab/pd3.so build/ab/pd4.so > $OUT/ab_12k.txt 2>&1; cat $OUT/ab_12k.txt
+timeout -k 10 900 bash scripts/ab_lib.sh build/ab/pd3.so build/ab/pd4.so build/ab/q2w2.so build/ab/q2w3.so build/ab/ru2.so > $OUT/ab_c4.txt 2>&1; cat $OUT/ab_c4.txt
+timeout -k 10 600 bash scripts/ab_lib.sh --args "--steps 20 --warmup 3 --N 12500" build/ab/pd3.so build/ab/pd4.so build/ab/ru2.so > $OUT/ab_12k.txt 2>&1; cat $OUT/ab_12k.txt
 C5ARGS="--config C5 --steps 4 --warmup 1 --no-cpu-baseline --no-shard-sim --em-iters 0 --parity-seconds 3"
 for v in tree b12w2 bwd2; do
   case $v in tree) E="";; b12w2) E="VBHEM_LIB_PATH=$(realpath build/ab/b12w2.so)";; bwd2) E="VBHEM_NO_BWD12=1";; esac
