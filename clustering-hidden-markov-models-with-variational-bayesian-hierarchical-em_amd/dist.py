@@ -53,26 +53,38 @@ class RcclComm:
         self.rank = (dist.get_rank(group) if inited else 0) if rank is None else int(rank)
         self.world = (dist.get_world_size(group) if inited else 1) if world is None else int(world)
         self.device = torch.device(device)
-        idb = (ctypes.c_char * _capi.RCCL_ID_BYTES)()
-        err = None
-        if self.rank == 0 and self._lib.vbhem_rccl_unique_id(idb) != 0:
-            err = self._lib.vbhem_last_error().decode(errors="replace")
-        if self.world > 1:
-            # the id (or rank 0's error) reaches every rank, so no rank waits in
-            # ncclCommInitRank for a rank 0 that could not make one
-            obj = [err if err is not None else bytes(idb)]
-            dist.broadcast_object_list(obj, src=0, group=group)
-            if isinstance(obj[0], str):
-                err = obj[0]
-            else:
-                ctypes.memmove(idb, obj[0], _capi.RCCL_ID_BYTES)
-        if err is not None:
-            raise _capi.VbhemError(f"vbhem_rccl_unique_id failed: {err}")
+        idb = (ctypes.c_char * _capi.RCCL_ID_BYTES).from_buffer_copy(
+            self.exchange_id(self.rank, self.world, group))
         h = ctypes.c_void_p()
         _capi.check(self._lib.vbhem_rccl_comm_init(self.world, self.rank, idb,
                                                    int(self.device.index or 0), ctypes.byref(h)),
                     "vbhem_rccl_comm_init")
         self.handle = h
+
+    @staticmethod
+    def exchange_id(rank: int, world: int, group=None) -> bytes:
+        """Rank 0's communicator id on every rank.  The id -- or rank 0's error --
+        reaches every rank, so no rank waits in ncclCommInitRank for a rank 0 that
+        could not make one."""
+        import ctypes
+
+        from . import _capi
+        lib = _capi.lib()
+        idb = (ctypes.c_char * _capi.RCCL_ID_BYTES)()
+        err = None
+        if rank == 0 and lib.vbhem_rccl_unique_id(idb) != 0:
+            err = lib.vbhem_last_error().decode(errors="replace")
+        out = bytes(idb)
+        if world > 1:
+            obj = [err if err is not None else out]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            if isinstance(obj[0], str):
+                err = obj[0]
+            else:
+                out = obj[0]
+        if err is not None:
+            raise _capi.VbhemError(f"vbhem_rccl_unique_id failed: {err}")
+        return out
 
     def allreduce(self, t: torch.Tensor) -> None:
         """In-place SUM of a device fp64 vector on the current stream."""

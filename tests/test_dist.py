@@ -123,3 +123,29 @@ def test_gloo_two_ranks_batched_trials(tmp_path):
         np.testing.assert_array_equal(r0[k], r1[k])
         np.testing.assert_allclose(r0[k], single[k], rtol=1e-10, err_msg=k)
     assert int(r0["best"]) == int(single["best"])
+
+
+def _rccl_id_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    import pkgload
+    pkgload.load()
+    from vbhem_amd.dist import RcclComm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    uid = RcclComm.exchange_id(rank, world)
+    with open(os.path.join(outdir, f"id{rank}.bin"), "wb") as f:
+        f.write(uid)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_id_exchange_two_ranks_gloo(tmp_path):
+    """The native communicator's set-up (dist.RcclComm.exchange_id): rank 0's RCCL
+    id (vbhem_rccl_unique_id, which needs no GPU) reaches every rank of a gloo
+    group unchanged -- the bytes every rank then hands to ncclCommInitRank."""
+    world = 2
+    mp.spawn(_rccl_id_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ids = [open(tmp_path / f"id{r}.bin", "rb").read() for r in range(world)]
+    assert len(ids[0]) == 128 and ids[0] == ids[1] and any(ids[0])
