@@ -31,12 +31,19 @@
 #include "vbhem_math.h"
 #include "vbhem_mfma4.h"
 
+// VBHEM_LIST4_R4: the backward half with fb_bwd4_kernel's round-4 step (the exp table
+// index decoupled from the column maxima, the 8192-interval log table: 144 KB of LDS,
+// one 8-wave block per CU) -- A/B switch
+#ifndef VBHEM_LIST4_R4
+#define VBHEM_LIST4_R4 0
+#endif
+
 namespace vbhem {
 
 namespace {
 using namespace m4;
 constexpr int kL4Waves = 2;   // waves per SIMD (the lattice is 72 VGPRs)
-constexpr int kL4NWB = 4;     // waves per block
+constexpr int kL4NWB = VBHEM_LIST4_R4 ? 8 : 4;   // waves per block
 constexpr int kL4T = 10;      // the tau this kernel is built for (C3 - C5)
 }  // namespace
 
@@ -44,11 +51,21 @@ template <int T>
 __global__ __launch_bounds__(64 * kL4NWB) __attribute__((amdgpu_waves_per_eu(kL4Waves)))
 void fb_list4_kernel(const SplitArgs p) {
   constexpr int S = 8;
+#if VBHEM_LIST4_R4
+  __shared__ __attribute__((aligned(16))) double tabs[2048 + 2 * 8192];
+  double *const etab = tabs, *const ltab8 = tabs + 2048;
+#else
   __shared__ __attribute__((aligned(16))) double etab[2048];
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];
+#endif
   __shared__ int pre[kList4MaxK + 1];  // first quad item of every cluster
   const int tid = threadIdx.x;
+#if VBHEM_LIST4_R4
+  for (int x = tid; x < 2048; x += 64 * kL4NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
+  stage_log8k(ltab8, tid, 64 * kL4NWB);
+#else
   stage_tables(etab, ltab, tid, 64 * kL4NWB);
+#endif
   const int K = p.K, SB = p.SB;
   if (tid == 0) {
     int s = 0;
@@ -148,6 +165,24 @@ void fb_list4_kernel(const SplitArgs p) {
       for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) s[i2][jj] = red_s(V[i2][jj]);
+#if VBHEM_LIST4_R4
+      const double sf[4] = {s[0][0], s[0][1], s[1][0], s[1][1]};
+      double tv[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) tv[x] = etab_at(etab, sf[x]);
+      const unsigned w = colmax_rows(max(lo_u(s[0][0]), lo_u(s[1][0])), max(lo_u(s[0][1]), lo_u(s[1][1]))) >> 11;
+      const int wq = (int)w - (1 << 20) - 1023;
+      const int mq[2] = {__builtin_amdgcn_ds_bpermute(qsrc0, wq), __builtin_amdgcn_ds_bpermute(qsrc1, wq)};
+      unsigned wp[2];
+      split_rows(w - 1010u, wp[0], wp[1]);
+      {
+        const double vf[4] = {V[0][0], V[0][1], V[1][0], V[1][1]};
+        const unsigned wpf[4] = {wp[0], wp[1], wp[0], wp[1]};
+        double gf[4];
+        exp_d_n<4>(gf, vf, sf, tv, wpf);
+        lat[t][0][0] = gf[0]; lat[t][0][1] = gf[1]; lat[t][1][0] = gf[2]; lat[t][1][1] = gf[3];
+      }
+#else
       const unsigned w = colmax_rows(max(lo_u(s[0][0]), lo_u(s[1][0])), max(lo_u(s[0][1]), lo_u(s[1][1])));
       const int wq = (int)(w + kWq0);
       const int mq[2] = {__builtin_amdgcn_ds_bpermute(qsrc0, wq), __builtin_amdgcn_ds_bpermute(qsrc1, wq)};
@@ -161,6 +196,7 @@ void fb_list4_kernel(const SplitArgs p) {
         exp_m_n<4>(gf, vf, sf, wpf, etab);
         lat[t][0][0] = gf[0]; lat[t][0][1] = gf[1]; lat[t][1][0] = gf[2]; lat[t][1][1] = gf[3];
       }
+#endif
       double z[4];
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
@@ -172,7 +208,11 @@ void fb_list4_kernel(const SplitArgs p) {
       double svf[4];
       {
         const int wqf[4] = {mq[0], mq[0], mq[1], mq[1]};
+#if VBHEM_LIST4_R4
+        log_q_n<4, true>(svf, z, wqf, ltab8);
+#else
         log_m_n<4>(svf, z, wqf, ltab);
+#endif
       }
       // sv(I, J') is Z^T's block (J', I) = svf[2 J' + I]
 #pragma unroll
@@ -210,7 +250,11 @@ void fb_list4_kernel(const SplitArgs p) {
       {
         const double zsf[1] = {zs};
         const int wqf[1] = {(int)(w + kWq0)};
+#if VBHEM_LIST4_R4
+        log_q_n<1, false>(lser, zsf, wqf, ltab8);
+#else
         log_m_n<1>(lser, zsf, wqf, ltab);
+#endif
       }
       bad = zmin < kZMinHi || rbad || !isfinite(lser[0]);
       const auto sl = __builtin_amdgcn_permlane16_swap(lo_u(lser[0]), lo_u(lser[0]), false, false);

@@ -756,7 +756,12 @@ bool split_supported(int S, int SB, int d) {
   return S >= 1 && S <= kSplitMaxS && SB >= 1 && SB <= S && d >= 1 && d <= 64;
 }
 
-int split_lpc(int S) { return S <= 4 ? 1 : S <= 8 ? 2 : 4; }
+int split_lpc(int S) {
+#ifdef VBHEM_SPLIT_LPC5
+  if (S == 5) return VBHEM_SPLIT_LPC5;
+#endif
+  return S <= 4 ? 1 : S <= 8 ? 2 : 4;
+}
 int split_lpc_bwd(int S) { return S <= 8 ? 1 : 2; }
 
 }  // namespace vbhem

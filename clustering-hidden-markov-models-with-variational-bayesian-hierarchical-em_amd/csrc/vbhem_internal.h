@@ -137,7 +137,11 @@ struct StatsArgs {
 constexpr int kSplitMaxS = 16;
 template <int S>
 struct SplitLPC {
+#ifdef VBHEM_SPLIT_LPC5   // A/B: lanes per column of the dense / list modes at S = 5
+  static constexpr int value = S <= 4 ? 1 : S == 5 ? VBHEM_SPLIT_LPC5 : S <= 8 ? 2 : 4;
+#else
   static constexpr int value = S <= 4 ? 1 : S <= 8 ? 2 : 4;
+#endif
 };
 // the backward-only mode's alternative (no H / sum_t_nu registers: wider columns fit)
 template <int S>
