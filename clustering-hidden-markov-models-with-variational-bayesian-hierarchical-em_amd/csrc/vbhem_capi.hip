@@ -17,6 +17,7 @@
 
 #include "vbhem_estep.h"
 #include "vbhem_internal.h"
+#include "vbhem_exact.h"
 #include "vbhem_math.h"
 
 namespace {
@@ -111,7 +112,7 @@ namespace {
 
 constexpr size_t kLdsLimit = 160 * 1024;          // gfx950 LDS per workgroup
 constexpr int kFbMaxThreads = 512;                // fb_pairs_kernel launch bound
-constexpr int kExactThreads = vbhem::kExactBlock * vbhem::kExactBlocks;  // fallback threads
+constexpr int kExactThreads = vbhem::kExactSlots;  // fallback scratch slots (one per wavefront)
 constexpr int kChunkMinBases = 64;                 // fused epilogue: bases per chunk, at least
 constexpr size_t kGroupBudget = (size_t)8 << 30;  // per-pair buffers per group (fused)
 constexpr int kMaxSlabs = 512;    // statistics chunks (= resp/stats blocks per group)
@@ -267,8 +268,8 @@ SplitPlan plan_split(int SB, int d, int covmode, int K, int S, int T, int LPC) {
   return sp;
 }
 
-size_t exact_stride(int S, int SB, int T) {
-  return (size_t)6 * S * SB + SB + (size_t)S * S * SB * T;
+size_t exact_stride(int S, int SB, int T) {  // Theta [T][S][S][SB], then the small arrays
+  return (size_t)S * S * SB * T + (size_t)vbhem::exact_wave_lds(S, SB);
 }
 
 int check_inputs(const vbhem_base_t *b, const vbhem_cluster_t *c, int T, bool need_ptrs = true) {
@@ -329,7 +330,6 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   Carver cv(ws);
   const size_t np = (size_t)b->N * c->K;
   w.flags = cv.take<int>(vbhem::kFlagHead + np);
-  w.scratch = cv.take<double>(exact_stride(c->S, b->SB, T) * kExactThreads);
   w.tnu = need_tnu ? cv.take<double>(np * c->S * b->SB) : nullptr;
   w.E = cv.take<double>(np * c->S * b->SB);
   w.W = cv.take<double>(emission_w_doubles(b->d, b->covmode, c->K, c->S));
@@ -338,6 +338,8 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.U = need_u_ws(b) ? cv.take<double>(vbhem::u_doubles((long long)b->N * b->SB + 16, b->d,
                                                          b->covmode))
                      : nullptr;
+  // the exact fallback's scratch last: its size does not move the hot buffers
+  w.scratch = cv.take<double>(exact_stride(c->S, b->SB, T) * kExactThreads);
   return cv.off + 256;
 }
 
@@ -370,7 +372,6 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   // flagged-pair list: with the fallback folded into the consumers the backward pass's
   // entries stay while the gate-list pass appends its own (at most g K + g K)
   w.flags = cv.take<int>(vbhem::kFlagHead + 2 * g * K);
-  w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   w.nu1 = cv.take<double>(g * K * S);
   w.xi = cv.take<double>(g * K * S * S);
   w.tnu = cv.take<double>(g * K * S * SB);
@@ -386,6 +387,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.list = cv.take<int>(g * K);
   w.list_tot = cv.take<int>((size_t)K);
   w.Atg = cv.take<double>((size_t)K * S * S);
+  // the exact fallback's scratch last: its size does not move the hot buffers
+  w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   return cv.off + 256;
 }
 

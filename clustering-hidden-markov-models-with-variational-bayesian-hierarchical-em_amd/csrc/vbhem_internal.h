@@ -316,9 +316,10 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 //       the rest)
 constexpr int kFlagHead = 4;
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
-constexpr int kExactBlock = 256;   // fb_exact_kernel: threads per block
-constexpr int kExactBlocks = 8;    // fb_exact_kernel: blocks (grid-stride over the list)
-hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
+constexpr int kExactBlock = 256;   // fb_exact_kernel: threads per block (4 wavefronts)
+constexpr int kExactBlocks = 512;  // fb_exact_kernel: blocks (wavefronts grid-stride over the list)
+constexpr int kExactSlots = kExactBlocks * kExactBlock / 64;  // scratch slots: one per wavefront
+hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nslots,
                            hipStream_t st);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t st);
 bool plan_stats(StatsArgs &a, size_t &lds, int &ngroups);

@@ -365,24 +365,33 @@ __global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// fb_exact_kernel: reference-order recursion for flagged pairs (one thread per
-// pair, grid-stride over the list; Theta in global scratch).  Mirrors
-// mex.c:715-1298 step by step.  kExactBlocks blocks consume the pass's flag
-// counter; the last block to finish resets it (and the blocks-done counter) to
-// zero, so the next pass needs no memset of its own (flag_count[1] keeps the
-// total).  Every block reads the count before it signals completion, so the
-// reset can never race a read.
+// fb_exact_kernel: reference-order recursion for flagged pairs, ONE WAVEFRONT per
+// pair (exact_pair_wave: the element loops of mex.c:715-1298 over the lanes, every
+// sum in the reference's order; Theta in the wave's global scratch slot, the pair's
+// small arrays in the wave's LDS region), wavefronts grid-striding over the list.
+// kExactBlocks blocks of kExactBlock threads: one scratch slot per wavefront.  The
+// blocks consume the pass's flag counter; the last block to finish resets it (and the
+// blocks-done counter) to zero, so the next pass needs no memset of its own
+// (flag_count[1] keeps the total).  Every block reads the count before it signals
+// completion, so the reset can never race a read.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kExactBlock) void fb_exact_kernel(const FbArgs p, double *scratch,
+__global__ __launch_bounds__(kExactBlock) __attribute__((amdgpu_waves_per_eu(4))) void fb_exact_kernel(
+    const FbArgs p, double *scratch,
                                                       size_t scratch_stride) {
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nt = gridDim.x * blockDim.x;
+  extern __shared__ double xlds[];
   const int cnt = __atomic_load_n(p.flag_count, __ATOMIC_RELAXED);
   // nothing flagged (the usual case): every block reads 0 -- nobody writes the
   // counter while it is 0 -- so all leave at once, with no reset to do
   if (cnt == 0) return;
-  double *w = scratch + (size_t)gt * scratch_stride;
-  for (int idx = gt; idx < cnt; idx += nt) exact_pair(p, p.flag_list[idx], w);
+  const int wpb = kExactBlock / 64, wave = threadIdx.x >> 6;
+  const int gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
+  double *w = scratch + (size_t)gw * scratch_stride;
+  if (exact_wave_in_lds(p.S, p.SB)) {
+    double *lw = xlds + (size_t)wave * exact_wave_lds(p.S, p.SB);
+    for (int idx = gw; idx < cnt; idx += nw) exact_pair_wave<false>(p, p.flag_list[idx], w, lw);
+  } else {
+    for (int idx = gw; idx < cnt; idx += nw) exact_pair_wave<true>(p, p.flag_list[idx], w, nullptr);
+  }
   __syncthreads();  // every thread of this block has read the count
   if (threadIdx.x == 0) {
     const int done = atomicAdd(p.flag_count + 2, 1);
@@ -462,11 +471,16 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
   }
 }
 
-hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nthreads,
+hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nslots,
                            hipStream_t st) {
-  // the scratch holds kExactBlocks * kExactBlock thread slots (vbhem_capi.hip)
-  if (nthreads != kExactBlock * kExactBlocks) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fb_exact_kernel, dim3(kExactBlocks), dim3(kExactBlock), 0, st, a, scratch,
+  // the scratch holds kExactSlots slots, one per wavefront (vbhem_capi.hip)
+  if (nslots != kExactSlots) return hipErrorInvalidValue;
+  const size_t lds = exact_wave_in_lds(a.S, a.SB)
+                         ? (size_t)(kExactBlock / 64) * exact_wave_lds(a.S, a.SB) * sizeof(double)
+                         : 0;
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&fb_exact_kernel), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fb_exact_kernel, dim3(kExactBlocks), dim3(kExactBlock), lds, st, a, scratch,
                      stride);
   return hipGetLastError();
 }

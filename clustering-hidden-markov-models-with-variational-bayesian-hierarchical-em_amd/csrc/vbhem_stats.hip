@@ -73,6 +73,7 @@ constexpr double kGateZ = 1e-8;  // vbhem_compute_Statistics.m:35  (Z_Ni(i) > 1e
 #define VBHEM_RESP_THREADS 512  // 8 waves per chunk block: 2x the bases in flight (C4 -10 us)
 #endif
 constexpr int kRespThreads = VBHEM_RESP_THREADS;
+constexpr int kRespFoldWaves = 4;  // folded fallback: worker wavefronts per chunk block
 
 __device__ __forceinline__ double group_max(double v, int G) {
   for (int off = G >> 1; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
@@ -88,7 +89,12 @@ __device__ __forceinline__ double group_sum(double v, int G) {
 #endif
 
 // G = lanes per base (power of two >= K, <= 64): 64/G bases per wavefront step.
-__global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
+// (4 waves per SIMD: two chunk blocks per CU; the folded fallback must not raise it)
+#ifndef VBHEM_RESP_WPE
+#define VBHEM_RESP_WPE 4
+#endif
+__global__ __launch_bounds__(kRespThreads) __attribute__((amdgpu_waves_per_eu(VBHEM_RESP_WPE))) void resp_kernel(
+    const StatsArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = kRespThreads / 64;
@@ -112,10 +118,15 @@ __global__ __launch_bounds__(kRespThreads) void resp_kernel(const StatsArgs p) {
     const int cnt = __atomic_load_n(fc, __ATOMIC_RELAXED);
     if (blockIdx.x == 0 && tid == 0) fc[3] = cnt;
     if (cnt > 0) {  // block-uniform
-      const int nw = min(kRespThreads, max(1, p.xslots / (int)gridDim.x));
+      const int nw = min(kRespFoldWaves, max(1, p.xslots / (int)gridDim.x));
       int *q = reinterpret_cast<int *>(lds), *qn = q + kRespThreads;
-      fold_exact(p.fx, 0, cnt, [&](int pair) { const int i = pair / K; return i >= b0 && i < b1; },
-                 p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn);
+      auto mine = [&](int pair) { const int i = pair / K; return i >= b0 && i < b1; };
+      if (exact_wave_in_lds(p.fx.S, p.fx.SB))
+        fold_exact<false>(p.fx, 0, cnt, mine, p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn,
+                          lds + fold_lds_bytes(kRespThreads, 0, 1, 1) / sizeof(double));
+      else
+        fold_exact<true>(p.fx, 0, cnt, mine, p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn,
+                         nullptr);
     }
   }
   for (int x = tid; x < NW * BPW * K + 2 * NW; x += kRespThreads) accNj[x] = 0.0;
@@ -900,7 +911,9 @@ size_t resp_lds(int K, int KT) {
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
   // per-wave Nj accumulators of all K clusters in LDS (past 64 KB at K ~ 960: the
   // launch sets the dynamic-LDS attribute; the caller rejects K past a CU's LDS)
-  const size_t lds = resp_lds(a.K, a.KT);
+  size_t lds = resp_lds(a.K, a.KT);
+  // the folded fallback borrows the accumulators' space first (queue + worker regions)
+  if (a.fold) lds = std::max(lds, fold_lds_bytes(kRespThreads, kRespFoldWaves, a.fx.S, a.fx.SB));
   if (a.KT != a.K) {  // batched trials
     if (a.K > kRespSlots * 64 || a.KT < 1 || a.K % a.KT != 0) return hipErrorInvalidValue;
     hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&resp_trials_kernel), lds);
@@ -1224,11 +1237,15 @@ __global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const Stats
       // xslots / gridDim scratch slots per block (the launch caps gridDim at xslots);
       // the queue sits past the kernel's own LDS
       const int ilo = lst[n0], ihi = lst[n1 - 1];
-      const int nw = min(64 * kSmWaves, max(1, p.xslots / (int)gridDim.x));
+      const int nw = 1;  // one worker wave (its LDS region must not cost residency)
       int *q = reinterpret_cast<int *>(zs + d), *qn = q + 64 * kSmWaves;
-      fold_exact(p.fx, c1, cnt,
-                 [&](int pair) { const int i = pair / K; return pair - i * K == j && i >= ilo && i <= ihi; },
-                 p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn);
+      auto mine = [&](int pair) { const int i = pair / K; return pair - i * K == j && i >= ilo && i <= ihi; };
+      if (exact_wave_in_lds(p.fx.S, p.fx.SB))
+        fold_exact<false>(p.fx, c1, cnt, mine, p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn,
+                          zs + d + fold_lds_bytes(64 * kSmWaves, 0, 1, 1) / sizeof(double));
+      else
+        fold_exact<true>(p.fx, c1, cnt, mine, p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn,
+                         nullptr);
     }
   }
   // one pair's operands: A values per k-slice, B values per (tile, k-slice), its Z and
@@ -1508,9 +1525,9 @@ static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st
 
 template <int NTW, int G, int KSM, int NXR, int PD>
 static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
-  // (+ the folded fallback's queue: one int per thread and its count)
+  // (+ the folded fallback's queue and its one worker wave's region)
   const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double) +
-                     (a.fold ? (64 * kSmWaves + 1) * sizeof(int) : 0);
+                     (a.fold ? fold_lds_bytes(64 * kSmWaves, 1, a.fx.S, a.fx.SB) : 0);
   auto *fn = &stats_list_m_kernel<NTW, G, KSM, NXR, PD>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
@@ -1649,7 +1666,7 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   // the other kernels do not fold the fallback: the exact kernel first (it redoes the
   // backward pass's entries too, which resp_kernel already fixed: same values)
   if (a.fold) {
-    hipError_t e = launch_fb_exact(a.fx, a.xscratch, (size_t)a.xstride, kExactBlock * kExactBlocks, st);
+    hipError_t e = launch_fb_exact(a.fx, a.xscratch, (size_t)a.xstride, kExactSlots, st);
     if (e != hipSuccess) return e;
   }
   // on the prepared operand's tile layout when the call has one (S <= 16: the split

@@ -151,6 +151,32 @@ def test_exact_fallback_pairs(vb, vo, cov):
         assert rel_err(got[k].cpu().numpy(), ref[k]) < RTOL_PAIRS, k
 
 
+@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}])
+def test_exact_fallback_large_states(vb, vo, env, monkeypatch):
+    """S = 20, Sb = 18: a flagged pair's small arrays (6 S Sb + S^2 + Sb doubles) no
+    longer fit the wavefront's LDS region, so exact_pair_wave keeps them in the tail of
+    its global scratch slot (agent-scope fences between its exchange steps)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cs, consts = adversarial_case(1, S=20, Sb=18, d=3, N=6, K=2, T=5)
+    consts["c"][1:] = 1.0e4
+    base, T = cs["base"], cs["T"]
+    N, K, S, d = 6, 2, 20, 3
+    ref = vo.c_estep_pairs(base, consts, T, want_tnu=True)
+    eng = engine(vb, base, consts, T)
+    got = eng.pairs(want_tnu=True)
+    assert eng.fallback_count() > 0
+    for k in PAIR_KEYS + ("sum_t_nu",):
+        assert rel_err(got[k].cpu().numpy(), ref[k]) < RTOL_PAIRS, k
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(ref["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, ref, 1)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, k
+
+
 def test_exact_fallback_fused(vb, vo, fused_mode):
     cs, consts = adversarial_case(1)
     base, T = cs["base"], cs["T"]
@@ -168,7 +194,7 @@ def test_exact_fallback_fused(vb, vo, fused_mode):
         assert stat_err(got[k], st[k]) < 1e-9, k
 
 
-@pytest.mark.parametrize("N,K", [(4, 1), (300, 2)])
+@pytest.mark.parametrize("N,K", [(4, 1), (300, 2), (3000, 2)])
 @pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}, {"VBHEM_NO_STATS_M": "1"}])
 def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
     """The adversarial cluster wins every base (the other cluster's emissions are far
