@@ -70,12 +70,18 @@ def transcendentals_per_pair(S, Sb, T):
     return T * S * S * Sb, T * S * Sb
 
 
-def fb_bytes_per_pair(S, Sb, d, covmode, K, split=True, backward_only=False):
+def fb_bytes_per_pair(S, Sb, d, covmode, K, split=True, backward_only=False, k1_fused=False):
     """Algorithmic HBM bytes of one fb-kernel pair.  Split path: its 1/K share
     of the base transitions/prior + its E tile (emission_kernel output) + its
     outputs (LL, nu_1, sum_xi, sum_t_nu; LL alone for the backward pass).
-    Generic path: base emissions instead of E."""
+    With K1 inside the kernel (k1_fused) the 1/K share of the base's prepared
+    operand U (Sb x kdp doubles) replaces the E tile.  Generic path: base
+    emissions instead of E."""
     out = 8 if backward_only else (1 + S + S * S + S * Sb) * 8
+    if split and k1_fused:
+        kd = d * (d + 1) // 2 + d if covmode == 1 else 2 * d
+        kdp = (kd + 3) // 4 * 4
+        return (Sb + Sb * Sb + Sb * kdp) * 8 / K + out
     if split:
         return (Sb + Sb * Sb) * 8 / K + S * Sb * 8 + out
     dC = d * d if covmode == 1 else d
@@ -506,12 +512,16 @@ def main():
     pairs_per_launch = tk["fb_pairs"] / max(1, tk["fb_launches"])
     split = S <= 16 and Sb <= S and d <= 64
     gated = split and tkb["gated_fwd_launches"] > 0
+    # K1 inside fb_bwd4_kernel / fb_list4_kernel: no emission GEMM launch was timed
+    k1_fused = gated and tkb["em_launches"] == 0
     if gated:
         fpp = bwd_flops_per_pair(S, Sb, T)
+        if k1_fused:
+            fpp += emission_flops_per_pair(S, Sb, d, cov)
     else:
         fpp = fb_flops_per_pair(S, Sb, T) if split else flops_per_pair(S, Sb, d, T, cov)
     achieved = fpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e12
-    bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split, backward_only=gated)
+    bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split, backward_only=gated, k1_fused=k1_fused)
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
     lpc = 1 if S <= 4 else 2 if S <= 8 else 4      # split_lpc (dense / list modes)
     lpc_bwd = 1 if S <= 8 else 2                    # split_lpc_bwd (backward mode)
@@ -580,7 +590,8 @@ def main():
                      "78.6 TF/s (vector = matrix rate); achievable_peak = the sustained "
                      "v_fma_f64 rate measured on this chip by scripts/ubench_valu.hip "
                      "(4 waves/SIMD, independent chains); flops counted on the reference "
-                     "recurrences this kernel runs (" + ("K2 backward + K3 termination, every "
+                     "recurrences this kernel runs (" + ("K1 emission GEMM + " if k1_fused else "")
+                     + ("K2 backward + K3 termination, every "
                      "pair" if gated else "K2-K4") + "), excluding exp/log"),
             "hbm": {"algorithmic_bytes_per_launch": bpp * pairs_per_launch,
                     "achieved_GBs": bpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e9,
@@ -613,6 +624,11 @@ def main():
                            "achieved_TFLOPs": dense_ach,
                            "flops_per_pair": dense_fpp},
         "emission_kernel_ms": tkb["em_ms"] / max(1, tkb["em_launches"]),
+        "k1_in_backward": k1_fused,
+        "k1_note": ("K1 (the emission GEMM, mex.c:715-865) runs inside the recursion kernels "
+                    "(fb_bwd2_kernel, fb_split_kernel list mode; kdp <= 8 fmas per entry): no emission "
+                    "kernel, no E buffer; emission_kernel_ms is 0" if k1_fused else
+                    "K1 in emission_u_kernel (E written to HBM, read by the recursion)"),
         "stats_kernels_ms_per_step": tkb["stats_ms"] / bd_steps,
         "breakdown_steps": bd_steps,
         "em_math_kernel_ms": em_it["math_kernel_ms"] if em_it else None,

@@ -402,6 +402,10 @@ struct FbCtx {
   bool bwd12 = false;  // S = 12, SB <= 12: fb_bwd12_kernel (MFMA contractions) instead
   bool bwd4 = false;  // S = 8, SB <= 8: fb_bwd4_kernel (MFMA contractions) instead
   bool list4 = false;  // S = 8, SB <= 8, T = 10: fb_list4_kernel for the gate-list pass
+  // gated schedule on fb_bwd2_kernel + fb_split_kernel's list mode with a short K1
+  // (kdp <= 8: C2, C3): both evaluate E from the prepared operand (SplitArgs::eU);
+  // no emission GEMM launch, no E traffic
+  bool k1_in_kernel = false;
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
   // emission_u_kernel: on the prepared operand (base->U) or one built per call in u_ws
@@ -455,8 +459,28 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
       c.bwd12 = vbhem::bwd12_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD12");
       c.list4 = vbhem::list4_supported(cl->S, b->SB, T, cl->K) && !std::getenv("VBHEM_NO_LIST4");
     }
+    c.k1_in_kernel = c.use_u && c.bwd2_lds && !c.bwd4 && !c.bwd12 && !c.list4 &&
+                     c.em.kdp <= vbhem::kK1InKernelMaxKdp && !std::getenv("VBHEM_NO_K1_IN_KERNEL");
   }
   return VBHEM_OK;
+}
+
+// the in-kernel K1's operands (FbCtx::k1_in_kernel): the prepared operand, or this
+// call's (run_fb builds it for bases from i_begin: tile 0 at column i_begin SB rounded
+// down to 16)
+void set_k1_operands(const FbCtx &c, int i_begin, vbhem::SplitArgs &ca) {
+  if (c.base->U) {
+    ca.eU = c.base->U;
+    ca.e_col0 = 0;
+  } else {
+    ca.eU = c.u_ws;
+    ca.e_col0 = (long long)i_begin * c.base->SB / 16 * 16;
+  }
+  ca.eW = c.em.W;
+  ca.ebias = c.em.bias;
+  ca.ekdp = c.em.kdp;
+  ca.eksp = c.em.ksp;
+  ca.esmooth = c.em.smooth;
 }
 
 // W, bias, shift of the emission GEMM: once per call (depends on the clusters only)
@@ -502,11 +526,12 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
     e = vbhem::launch_list4(ca, grid, st);
     if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
   } else {
+    if (c.k1_in_kernel) set_k1_operands(c, i_begin, ca);
     e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_l), c.split.lds_l, st);
     if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
   }
   if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
-  if (fold) return VBHEM_OK;  // the statistics kernel takes the flagged pairs (StatsArgs::fold)
+  if (fold) return VBHEM_OK;  // launch_stats_list runs fb_exact_kernel from flag_count[3]
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin; a.i_end = i_end; a.i_buf0 = i_buf0;
   a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
@@ -531,6 +556,8 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   a.flag_count = flags;
   a.flag_list = flags + vbhem::kFlagHead;
   hipError_t e = hipSuccess;
+  // K1 inside fb_bwd2_kernel (and the list pass after it): no emission GEMM
+  const bool k1 = c.k1_in_kernel && mode == vbhem::kFbBackward;
   if (!c.split.ok) {  // split path: zeroed by emission_prep_kernel, reset by fb_exact_kernel
     e = hipMemsetAsync(flags, 0, sizeof(int), st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
@@ -539,7 +566,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     vbhem::EmissionArgs ea = c.em;
     ea.i_begin = i_begin; ea.i_end = i_end; ea.i_buf0 = i_buf0; ea.E = Ebuf; ea.e_ld = e_ld;
     size_t em_lds = c.em_lds;
-    hipEvent_t em0 = timing_on(st) ? timing_event(st) : nullptr;
+    hipEvent_t em0 = !k1 && timing_on(st) ? timing_event(st) : nullptr;
     if (c.use_u) {
       em_lds = c.em_lds_u;
       if (c.base->U) {
@@ -560,9 +587,11 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
         ea.u_col0 = ua.u_col0;
       }
     }
-    e = vbhem::launch_emission(ea, em_lds, st);
-    if (e != hipSuccess) return hip_fail(e, "emission_kernel");
-    if (em0) g_timing.em.emplace_back(em0, timing_event(st));
+    if (!k1) {
+      e = vbhem::launch_emission(ea, em_lds, st);
+      if (e != hipSuccess) return hip_fail(e, "emission_kernel");
+      if (em0) g_timing.em.emplace_back(em0, timing_event(st));
+    }
   }
   hipEvent_t ev0 = timing_on(st, true) ? timing_event(st) : nullptr;
   if (c.split.ok) {
@@ -596,6 +625,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     } else if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
       ca.nwb = c.bwd2_nwb;
+      if (k1) set_k1_operands(c, i_begin, ca);
       const unsigned nt2 = (unsigned)((i_end - i_begin + c.bwd2_ppb - 1) / c.bwd2_ppb);
       const unsigned all = (unsigned)(vbhem::device_cus() *
                                       std::max(1, vbhem::bwd2_resident_blocks(ca.S, ca.nwb, c.bwd2_lds)));
@@ -853,11 +883,10 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
                          gated ? w.Atg : nullptr,
                          clus->logA);
   if (rc != VBHEM_OK) return rc;
-  // the exact fallback folded into resp_kernel and the statistics kernel (one base
-  // group, one trial: two fb_exact_kernel launches less per E-step)
-  // (the statistics kernel needs a block, and so a scratch slot, per cluster: K below
-  // the slot count)
-  // (and resp_kernel needs one per chunk block: at most kExactThreads chunks)
+  // the backward pass's exact fallback folded into resp_kernel (one base group, one
+  // trial: one fb_exact_kernel launch less per E-step; the gate-list pass's flags get
+  // their launch in launch_stats_list, from flag_count[3]); resp_kernel needs a
+  // scratch slot per chunk block: at most kExactThreads chunks
   const bool fold = gated && R == 1 && base->N <= w.group && ctx.split.ok && K < kExactThreads &&
                     w.nslab <= kExactThreads && !std::getenv("VBHEM_NO_FOLD_EXACT");
   sa.fold = 0;

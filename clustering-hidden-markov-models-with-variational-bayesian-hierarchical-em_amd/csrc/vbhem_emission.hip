@@ -563,8 +563,11 @@ __global__ __launch_bounds__(kUThreads) void us_build_kernel(UPrepArgs p, double
   }
 }
 
+#ifndef UNWAVE_MAXT
+#define UNWAVE_MAXT 512  // launch bound of emission_u_kernel (threads per block)
+#endif
 template <int KQB, int RC, int NTW, bool EXACT, bool PF = false>
-__global__ __launch_bounds__(512) void emission_u_kernel(EmissionArgs p) {
+__global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NT = blockDim.x, NW = NT >> 6;

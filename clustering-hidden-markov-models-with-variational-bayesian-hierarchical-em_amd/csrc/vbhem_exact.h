@@ -1,7 +1,7 @@
 // vbhem_exact.h -- the reference-order recursion of one flagged pair (mex.c:715-1298
 // step by step: K1, the backward LSE with stored Theta, termination, the forward sweep),
 // shared by fb_exact_kernel and the kernels that fold the fallback into their prologue
-// (resp_kernel, stats_list_m_kernel, through fold_exact): one wavefront per pair
+// (resp_kernel, through fold_exact): one wavefront per pair
 // (exact_pair_wave).  Internal.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -216,8 +216,8 @@ static __host__ __device__ inline size_t fold_lds_bytes(int threads, int nw, int
   return qb + (exact_wave_in_lds(S, SB) ? (size_t)nw * exact_wave_lds(S, SB) * sizeof(double) : 0);
 }
 
-// The exact fallback folded into a consumer kernel's prologue (resp_kernel,
-// stats_list_m_kernel): the flagged pairs flag_list[x0, x1) that `mine` accepts are
+// The exact fallback folded into a consumer kernel's prologue (resp_kernel):
+// the flagged pairs flag_list[x0, x1) that `mine` accepts are
 // found by the whole block, blockDim entries per round (coalesced), queued in LDS
 // (q [blockDim], *qn), and recomputed by the block's first `nw` WAVEFRONTS
 // (exact_pair_wave), wave k on scratch slot slot0 + k and LDS region lw + k *

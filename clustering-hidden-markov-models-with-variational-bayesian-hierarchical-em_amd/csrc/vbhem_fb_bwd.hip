@@ -105,7 +105,9 @@ struct Bwd2Layout {
   static constexpr int XCS = (S + 1) / 2 * 2 + 2;    // slab column stride (even: 16-B rows)
   static constexpr int XP = SP * XCS + 2;            // per-pair slab (doubles)
   static constexpr int OFF_CL = 0;                   // amax [S], lpi [S] (dynamic LDS)
-  static constexpr int OFF_X = (2 * S + 1) / 2 * 2;
+  // the in-kernel K1's cluster operands (SplitArgs::eU): W' [kdp <= 8][S], bias' [S]
+  static constexpr int OFF_K1 = 2 * S;
+  static constexpr int OFF_X = (2 * S + (kK1InKernelMaxKdp + 1) * S + 1) / 2 * 2;
 };
 
 }  // namespace
@@ -150,6 +152,16 @@ void fb_bwd2_kernel(const SplitArgs p) {
     for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
     amax[tid] = mx;
     lpi[tid] = p.logPi[(size_t)j * S + tid];
+  }
+  // in-kernel K1 (p.eU): cluster j's W' columns and bias' staged once per block, read
+  // as LDS broadcasts by every tile's prologue
+  double *k1w = lds + LY::OFF_K1;  // [kdp][S], then bias' [S]
+  if (p.eU) {
+    for (int x = tid; x < p.ekdp * S; x += NT) {
+      const int e = x / S, k = x - e * S;
+      k1w[x] = p.eW[(size_t)e * p.eksp + (size_t)j * S + k];
+    }
+    for (int k = tid; k < S; k += NT) k1w[p.ekdp * S + k] = p.ebias[(size_t)j * S + k];
   }
   __syncthreads();
 
@@ -203,11 +215,27 @@ void fb_bwd2_kernel(const SplitArgs p) {
         arow[c][be] = (bv[c] && be < SB) ? a : 0.0;
         rs += arow[c][be];
       }
+      if (p.eU) {  // K1 here (short inner dimension): no E buffer
+        double u[kK1InKernelMaxKdp];
+        k1_column(p, (long long)ic * SB + bc, u);
+        const int kdp = p.ekdp;
 #pragma unroll
-      for (int k = 0; k < S; ++k) {
-        const double e = Ep[(size_t)k * p.e_ld];
-        Ef[c][k] = e + amax[k] * rs;
-        V[c][k] = e;
+        for (int k = 0; k < S; ++k) {
+          double e = k1w[kdp * S + k];  // bias', then W' u in e order
+#pragma unroll
+          for (int x = 0; x < kK1InKernelMaxKdp; ++x)
+            if (x < kdp) e = fma(k1w[x * S + k], u[x], e);
+          if (p.esmooth != 1.0) e = e / p.esmooth;
+          Ef[c][k] = e + amax[k] * rs;
+          V[c][k] = e;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const double e = Ep[(size_t)k * p.e_ld];
+          Ef[c][k] = e + amax[k] * rs;
+          V[c][k] = e;
+        }
       }
       const double pr = p.prior[(size_t)ic * SB + bc];
       pb[c] = bv[c] ? pr : 0.0;
@@ -368,7 +396,8 @@ size_t bwd2_lds(int S, int nwb) {
   if (S < 1 || S > kBwd2MaxS) return 0;
   const int CPL = S <= 8 ? 2 : 1, LPP = (S + CPL - 1) / CPL, PPW = 64 / LPP;
   const int XCS = (S + 1) / 2 * 2 + 2, XP = CPL * LPP * XCS + 2;
-  const int off_x = (2 * S + 1) / 2 * 2;  // dynamic part only: the tables are static
+  // dynamic part only (the tables are static): amax, lpi, the in-kernel K1's W' and bias'
+  const int off_x = (2 * S + (kK1InKernelMaxKdp + 1) * S + 1) / 2 * 2;
   const int ppb = nwb * PPW;
   return ((size_t)off_x + (size_t)ppb * XP + (ppb + 1) / 2 + 1) * sizeof(double);
 }

@@ -266,7 +266,16 @@ void fb_split_kernel(const SplitArgs p) {
     if (valid && w == 0) F[q] = 0;  // read back only after this pair's later syncs
     // per-pair inputs: E (K1, precomputed), Ab row/column, prior
     double E[SH];
-    {
+    if (pa.eU) {  // K1 here (short inner dimension): no E buffer
+      double u[kK1InKernelMaxKdp];
+      k1_column(pa, (long long)ic * SB + bc, u);
+#pragma unroll
+      for (int k = 0; k < SH; ++k) {
+        const bool rv = r0 + k < S;
+        const double v = k1_entry(pa, j * S + (rv ? r0 + k : S - 1), u);
+        E[k] = rv ? v : -INFINITY;
+      }
+    } else {
       const double *Ep = pa.E + (size_t)j * S * pa.e_ld + (size_t)(ic - pa.i_buf0) * SB + bc;
 #pragma unroll
       for (int k = 0; k < SH; ++k) {

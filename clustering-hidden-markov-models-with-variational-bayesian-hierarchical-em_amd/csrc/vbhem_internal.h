@@ -123,9 +123,10 @@ struct StatsArgs {
   int nzero;             // stats_list_u_kernel with assign: slabs [gridDim.x, nzero) get zeros
   const double *Us;      // the statistics copy of the prepared operand (us_doubles), or null
   int nzero_m;           // stats_list_m_kernel: at most this many parts (slabs) per cluster (0: nzero)
-  // the exact fallback folded into resp_kernel (the backward pass's flagged pairs of each
-  // block's bases) and stats_list_m_kernel (the gate-list pass's flagged pairs of each
-  // block's part) instead of two fb_exact_kernel launches (fold = 1; one base group)
+  // the backward pass's exact fallback folded into resp_kernel (the flagged pairs of
+  // each block's bases; the gate-list pass's then get an fb_exact_kernel launch from
+  // flag_count[3] in launch_stats_list) instead of a launch after each pass (fold = 1;
+  // one base group)
   int fold;
   FbArgs fx;                 // the exact recursion's arguments (outputs, flag counter / list)
   double *xscratch;          // its scratch: xslots slots of xstride doubles
@@ -258,7 +259,38 @@ struct SplitArgs {
   const int *list, *list_tot;  // kFbList: gated bases per cluster (gate_list_kernel)
   int list_cap;
   const double *Atg;           // kFbBackward, LPC 1: [K][S][S] A' (emission_prep_kernel)
+  // K1 inside the recursion kernel (eU set; fb_bwd2_kernel and fb_split_kernel's list
+  // mode, for a short GEMM inner dimension, kdp <= kK1InKernelMaxKdp): E = bias' + W'^T u
+  // per entry from the prepared operand U (u_prep layout, tile 0 at column e_col0,
+  // ekdp / 4 k-steps) and emission_prep_kernel's W' [ekdp][eksp], bias' [eksp],
+  // instead of reading emission_kernel's E
+  const double *eU, *eW, *ebias;
+  long long e_col0;
+  int ekdp, eksp;
+  double esmooth;
 };
+
+constexpr int kK1InKernelMaxKdp = 8;  // d = 2 full / d <= 4 diag: at most 8 fmas per entry
+
+// the kdp <= 8 operand values u_e of one column (i SB + b) of U (zero past kdp)
+__device__ __forceinline__ void k1_column(const SplitArgs &p, long long col,
+                                          double (&u)[kK1InKernelMaxKdp]) {
+  const long long c = col - p.e_col0;
+  const double *Ut = p.eU + kUHead + (size_t)(c >> 4) * (p.ekdp / 4) * 64 + (int)(c & 15);
+#pragma unroll
+  for (int e = 0; e < kK1InKernelMaxKdp; ++e)
+    u[e] = e < p.ekdp ? Ut[(e >> 2) * 64 + (e & 3) * 16] : 0.0;
+}
+// E of cluster row jr = j S + sigma at that column: bias' + sum_e W'[e][jr] u_e in e
+// order (the GEMM's sums, blocked differently: equal to rounding)
+__device__ __forceinline__ double k1_entry(const SplitArgs &p, int jr,
+                                           const double (&u)[kK1InKernelMaxKdp]) {
+  double acc = p.ebias[jr];
+#pragma unroll
+  for (int e = 0; e < kK1InKernelMaxKdp; ++e)
+    if (e < p.ekdp) acc = fma(p.eW[(size_t)e * p.eksp + jr], u[e], acc);
+  return p.esmooth != 1.0 ? acc / p.esmooth : acc;
+}
 bool split_supported(int S, int SB, int d);
 int split_lpc(int S);      // lanes per column
 int split_lpc_bwd(int S);  // lanes per column, alternative for kFbBackward (BwdLPC)
@@ -312,15 +344,16 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 // EM trial) are not flagged: their L_elbo is written as NaN, as the reference's
 // arithmetic would produce, and they cost the fallback nothing.
 //   [3] the first entry of the gate-list pass (written by resp_kernel when the fallback
-//       is folded into the consumers: resp_kernel takes [0, [3]), stats_list_m_kernel
-//       the rest)
+//       is folded: resp_kernel takes [0, [3]), the fb_exact_kernel launch before the
+//       statistics the rest)
 constexpr int kFlagHead = 4;
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
 constexpr int kExactBlock = 256;   // fb_exact_kernel: threads per block (4 wavefronts)
 constexpr int kExactBlocks = 512;  // fb_exact_kernel: blocks (wavefronts grid-stride over the list)
 constexpr int kExactSlots = kExactBlocks * kExactBlock / 64;  // scratch slots: one per wavefront
+// from_fold: start at flag_count[3] (the entries before it were folded into resp_kernel)
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nslots,
-                           hipStream_t st);
+                           hipStream_t st, bool from_fold = false);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t st);
 bool plan_stats(StatsArgs &a, size_t &lds, int &ngroups);
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st);

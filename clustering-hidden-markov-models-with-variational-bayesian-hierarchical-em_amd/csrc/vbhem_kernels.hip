@@ -375,22 +375,23 @@ __global__ __launch_bounds__(512) void fb_pairs_kernel(const FbArgs p) {
 // (flag_count[1] keeps the total).  Every block reads the count before it signals
 // completion, so the reset can never race a read.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kExactBlock) __attribute__((amdgpu_waves_per_eu(4))) void fb_exact_kernel(
-    const FbArgs p, double *scratch,
-                                                      size_t scratch_stride) {
+__global__ __launch_bounds__(kExactBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void fb_exact_kernel(const FbArgs p, double *scratch, size_t scratch_stride, int from_fold) {
   extern __shared__ double xlds[];
   const int cnt = __atomic_load_n(p.flag_count, __ATOMIC_RELAXED);
   // nothing flagged (the usual case): every block reads 0 -- nobody writes the
   // counter while it is 0 -- so all leave at once, with no reset to do
   if (cnt == 0) return;
+  // from_fold: resp_kernel took the backward pass's entries [0, flag_count[3])
+  const int x0 = from_fold ? p.flag_count[3] : 0;
   const int wpb = kExactBlock / 64, wave = threadIdx.x >> 6;
   const int gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
   double *w = scratch + (size_t)gw * scratch_stride;
   if (exact_wave_in_lds(p.S, p.SB)) {
     double *lw = xlds + (size_t)wave * exact_wave_lds(p.S, p.SB);
-    for (int idx = gw; idx < cnt; idx += nw) exact_pair_wave<false>(p, p.flag_list[idx], w, lw);
+    for (int idx = x0 + gw; idx < cnt; idx += nw) exact_pair_wave<false>(p, p.flag_list[idx], w, lw);
   } else {
-    for (int idx = gw; idx < cnt; idx += nw) exact_pair_wave<true>(p, p.flag_list[idx], w, nullptr);
+    for (int idx = x0 + gw; idx < cnt; idx += nw) exact_pair_wave<true>(p, p.flag_list[idx], w, nullptr);
   }
   __syncthreads();  // every thread of this block has read the count
   if (threadIdx.x == 0) {
@@ -472,7 +473,7 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 }
 
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nslots,
-                           hipStream_t st) {
+                           hipStream_t st, bool from_fold) {
   // the scratch holds kExactSlots slots, one per wavefront (vbhem_capi.hip)
   if (nslots != kExactSlots) return hipErrorInvalidValue;
   const size_t lds = exact_wave_in_lds(a.S, a.SB)
@@ -481,7 +482,7 @@ hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int 
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&fb_exact_kernel), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(fb_exact_kernel, dim3(kExactBlocks), dim3(kExactBlock), lds, st, a, scratch,
-                     stride);
+                     stride, (int)from_fold);
   return hipGetLastError();
 }
 

@@ -1228,26 +1228,6 @@ __global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const Stats
   const int tot = p.list_tot[j];
   const int n0 = (int)((long long)tot * c / nch), n1 = (int)((long long)tot * (c + 1) / nch);
   const int *lst = p.list + (size_t)j * p.list_cap;
-  if (p.fold) {
-    // the folded fallback: the gate-list pass's flagged pairs of this part (cluster j,
-    // bases lst[n0] .. lst[n1 - 1]) get their exact outputs before they are read
-    const int *fc = p.fx.flag_count;
-    const int c1 = fc[3], cnt = __atomic_load_n(fc, __ATOMIC_RELAXED);
-    if (cnt > c1 && n0 < n1) {  // block-uniform
-      // xslots / gridDim scratch slots per block (the launch caps gridDim at xslots);
-      // the queue sits past the kernel's own LDS
-      const int ilo = lst[n0], ihi = lst[n1 - 1];
-      const int nw = 1;  // one worker wave (its LDS region must not cost residency)
-      int *q = reinterpret_cast<int *>(zs + d), *qn = q + 64 * kSmWaves;
-      auto mine = [&](int pair) { const int i = pair / K; return pair - i * K == j && i >= ilo && i <= ihi; };
-      if (exact_wave_in_lds(p.fx.S, p.fx.SB))
-        fold_exact<false>(p.fx, c1, cnt, mine, p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn,
-                          zs + d + fold_lds_bytes(64 * kSmWaves, 0, 1, 1) / sizeof(double));
-      else
-        fold_exact<true>(p.fx, c1, cnt, mine, p.xscratch, p.xstride, (int)blockIdx.x * nw, nw, q, qn,
-                         nullptr);
-    }
-  }
   // one pair's operands: A values per k-slice, B values per (tile, k-slice), its Z and
   // its sum_nu_1 / sum_xi entries; a ring of PD of them (PD - 1 pairs' loads in flight
   // while a pair's MFMAs run)
@@ -1525,9 +1505,7 @@ static hipError_t launch_su(const StatsArgs &a, const dim3 &grid, hipStream_t st
 
 template <int NTW, int G, int KSM, int NXR, int PD>
 static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
-  // (+ the folded fallback's queue and its one worker wave's region)
-  const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double) +
-                     (a.fold ? fold_lds_bytes(64 * kSmWaves, 1, a.fx.S, a.fx.SB) : 0);
+  const size_t lds = ((size_t)a.S * a.NU + a.S + (size_t)a.S * a.S + a.d) * sizeof(double);
   auto *fn = &stats_list_m_kernel<NTW, G, KSM, NXR, PD>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
@@ -1539,7 +1517,6 @@ static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t
                  device_cus();
   if (const char *ev = std::getenv("VBHEM_SU_BLOCKS")) nb = std::atoll(ev);  // A/B
   nb = std::min<long long>(std::max<long long>(nb, a.K + 1), grid.x);
-  if (a.fold) nb = std::min<long long>(nb, a.xslots);  // one fallback scratch slot per block
   hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(64 * kSmWaves), lds, st, a);
   return hipGetLastError();
 }
@@ -1650,6 +1627,15 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   StatsArgs b = a;
   b.nzero = nchunk;
   const int lg = a.U ? sg_lanes(a) : 0;
+  // the gate-list pass's flagged pairs (resp_kernel folded the backward pass's): an
+  // fb_exact_kernel launch from flag_count[3] before any statistics kernel reads them.
+  // (Folded into stats_list_m_kernel as well it measured no faster when nothing is
+  // flagged -- its inlined fallback cost the kernel ~9 us at C4 -- and 3x slower when
+  // every base is flagged: one worker wave per block there)
+  if (a.fold) {
+    hipError_t e = launch_fb_exact(a.fx, a.xscratch, (size_t)a.xstride, kExactSlots, st, true);
+    if (e != hipSuccess) return e;
+  }
   // the MFMA kernel on the statistics copy Us (prepared base sets; S <= 16 rows of one
   // MFMA tile, SB <= 16, at most 12 feature tiles over 4 waves); also for the small
   // moment vectors of the grouped kernel (C3: statistics 0.039 -> 0.032 ms per step)
@@ -1662,12 +1648,6 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
     if (stats_slabs) *stats_slabs = b.nzero;
     const dim3 g1((unsigned)std::min<long long>((long long)nchunk * a.K, 1ll << 30));
     return us_sbp(a.SB) <= 8 ? launch_sm_k<2>(b, g1, st) : launch_sm_k<4>(b, g1, st);
-  }
-  // the other kernels do not fold the fallback: the exact kernel first (it redoes the
-  // backward pass's entries too, which resp_kernel already fixed: same values)
-  if (a.fold) {
-    hipError_t e = launch_fb_exact(a.fx, a.xscratch, (size_t)a.xstride, kExactSlots, st);
-    if (e != hipSuccess) return e;
   }
   // on the prepared operand's tile layout when the call has one (S <= 16: the split
   // kernel's range) (NU > 64, e.g. d = 16 full at C5: the covariance gather of

@@ -123,6 +123,44 @@ def test_fused_multigroup(vb, vo, fused_mode, monkeypatch):
     assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
+@pytest.mark.parametrize("S,Sb,d,cov", [(5, 5, 2, 0), (3, 3, 2, 1), (6, 4, 4, 0)])
+def test_k1_in_recursion_kernels(vb, vo, S, Sb, d, cov, monkeypatch):
+    """Gated schedule with a short K1 (kdp <= 8: d = 2 full, d <= 4 diag -- C2, C3):
+    fb_bwd2_kernel and fb_split_kernel's list mode evaluate E from the prepared
+    operand, with no emission GEMM and no E buffer.  Statistics, hat_Z and L_elbo
+    against the oracle, and against the same call through the emission GEMM
+    (VBHEM_NO_K1_IN_KERNEL=1): the same sums blocked differently, equal to rounding."""
+    from vbhem_amd import _capi
+    prev = _capi.set_fused_mode(_capi.FUSED_GATED)
+    try:
+        N, K, T = 777, 5, 10
+        cs = make_case(N, K, S, Sb, d, cov, seed=17 + S, ragged=True, tau=T)
+        base, consts = cs["base"], cs["consts"]
+        pairs = vo.c_estep_pairs(base, consts, T, nthreads=8)
+        tN = 100.0 * N * base["omega"]
+        logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+        st = vo.c_statistics(Z, pairs, cov)
+        out = {}
+        for label in ("in_kernel", "gemm"):
+            if label == "gemm":
+                monkeypatch.setenv("VBHEM_NO_K1_IN_KERNEL", "1")
+            eng = engine(vb, base, consts, T)
+            eng.set_log_omega(logOmega)
+            raw = eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy()
+            out[label] = (vb.host.unpack_stats(raw, K, S, d, cov), eng.LL.cpu().numpy(),
+                          eng.hatZ.cpu().numpy())
+            del eng
+        got, LL, hzg = out["in_kernel"]
+        for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+            assert stat_err(got[k], st[k]) < 1e-9, k
+            assert stat_err(got[k], out["gemm"][0][k]) < 1e-12, k
+        assert elem_err(LL, pairs["LL_elbo"]) < RTOL_PAIRS
+        assert elem_err(LL, out["gemm"][1]) < 1e-13
+        assert hatz_err(hzg, hz) < RTOL_NORTH_STAR
+    finally:
+        _capi.set_fused_mode(prev)
+
+
 def adversarial_case(cov=1, S=4, Sb=4, d=3, N=4, K=3, T=6):
     """Cluster 0's transitions put all mass on sigma+1 while its emissions put
     all mass on state 0: the factorised normaliser Z ~ e^-600 underflows the
