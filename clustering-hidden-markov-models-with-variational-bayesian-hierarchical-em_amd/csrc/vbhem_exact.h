@@ -19,10 +19,11 @@ static __host__ __device__ inline int exact_wave_lds(int S, int SB) {
   return 6 * S * SB + 2 * S * S + S + SB * SB + 2 * SB;
 }
 
-// the pair's small arrays live in LDS when a 4-wave block's regions fit in 80 KB
-// (S = SB = 16 and below), else in the tail of the wave's global scratch slot
+// the pair's small arrays live in LDS when they take at most 16 KB per wavefront (S = SB
+// = 15 and below: 128 KB for fb_exact_kernel's 8 waves, 64 KB for resp_kernel's 4
+// workers), else in the tail of the wave's global scratch slot
 static __host__ __device__ inline bool exact_wave_in_lds(int S, int SB) {
-  return exact_wave_lds(S, SB) <= 2560;
+  return exact_wave_lds(S, SB) <= 2048;
 }
 
 // wave-level ordering of the exchanges below (one wavefront works on one pair):

@@ -348,8 +348,13 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 //       statistics the rest)
 constexpr int kFlagHead = 4;
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
-constexpr int kExactBlock = 256;   // fb_exact_kernel: threads per block (4 wavefronts)
-constexpr int kExactBlocks = 512;  // fb_exact_kernel: blocks (wavefronts grid-stride over the list)
+#ifndef VBHEM_EXACT_BLOCK
+#define VBHEM_EXACT_BLOCK 512
+#endif
+// fb_exact_kernel: threads per block (8 wavefronts: half the workgroups of 4-wave blocks
+// to dispatch for the same slots -- the launch is paid every E-step, flags or not)
+constexpr int kExactBlock = VBHEM_EXACT_BLOCK;
+constexpr int kExactBlocks = 131072 / kExactBlock;  // blocks (wavefronts grid-stride over the list)
 constexpr int kExactSlots = kExactBlocks * kExactBlock / 64;  // scratch slots: one per wavefront
 // from_fold: start at flag_count[3] (the entries before it were folded into resp_kernel)
 hipError_t launch_fb_exact(const FbArgs &a, double *scratch, size_t stride, int nslots,
