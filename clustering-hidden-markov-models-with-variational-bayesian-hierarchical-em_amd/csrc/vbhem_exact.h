@@ -20,7 +20,7 @@ static __host__ __device__ inline int exact_wave_lds(int S, int SB) {
 }
 
 // the pair's small arrays live in LDS when they take at most 16 KB per wavefront (S = SB
-// = 15 and below: 128 KB for fb_exact_kernel's 8 waves, 64 KB for resp_kernel's 4
+// = 14 and below: 128 KB for fb_exact_kernel's 8 waves, 64 KB for resp_kernel's 4
 // workers), else in the tail of the wave's global scratch slot
 static __host__ __device__ inline bool exact_wave_in_lds(int S, int SB) {
   return exact_wave_lds(S, SB) <= 2048;
