@@ -507,7 +507,7 @@ unsigned list_grid(const vbhem::SplitArgs &a, size_t lds) {
 int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1, double *xi,
                 double *tnu, const double *Ebuf, long long e_ld, const int *list,
                 const int *list_tot, int list_cap, int *flags, double *scratch, double *LL,
-                hipStream_t st, bool fold = false) {
+                hipStream_t st, bool fold = false, bool *inlined = nullptr) {
   if (i_end <= i_begin) return VBHEM_OK;
   // flags[0] is zero here: the backward pass's fb_exact_kernel reset it
   if (!c.split.lds_l) return fail(VBHEM_ERR_UNSUPPORTED, "gate-list pass does not fit LDS");
@@ -518,6 +518,20 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   ca.LL = nullptr; ca.nu1 = nu1; ca.xi = xi; ca.tnu = tnu;
   ca.flag_count = flags; ca.flag_list = flags + vbhem::kFlagHead;
   ca.list = list; ca.list_tot = list_tot; ca.list_cap = list_cap;
+  // folded fallback: the list kernel recomputes its own flagged pairs when its
+  // persistent grid has a scratch slot per wavefront (then no launch after the pass)
+  ca.xinline = 0;
+  auto set_inline = [&](long long waves) {
+    if (!fold || waves > kExactThreads || std::getenv("VBHEM_NO_LIST_INLINE")) return;
+    ca.xinline = 1;
+    ca.xscr = scratch;
+    ca.xstride = (long long)exact_stride(c.plan.a.S, c.plan.a.SB, c.plan.a.T);
+    vbhem::FbArgs &x = ca.xf;
+    x = c.plan.a;
+    x.i_begin = i_begin; x.i_end = i_end; x.i_buf0 = i_buf0;
+    x.LL = LL; x.nu1 = nu1; x.xi = xi; x.tnu = tnu;
+    x.flag_count = flags; x.flag_list = flags + vbhem::kFlagHead;
+  };
   hipEvent_t ev0 = timing_on(st) ? timing_event(st) : nullptr;
   hipError_t e;
   if (c.list4) {  // S = 8, SB <= 8, T = 10: fb_list4_kernel (MFMA), one wave per quad item
@@ -527,11 +541,15 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
     if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
   } else {
     if (c.k1_in_kernel) set_k1_operands(c, i_begin, ca);
-    e = vbhem::launch_split(ca, list_grid(ca, c.split.lds_l), c.split.lds_l, st);
+    const unsigned grid = list_grid(ca, c.split.lds_l);
+    if (ca.S >= vbhem::kSplitInlineMinS && ca.S <= vbhem::kSplitInlineMaxS)
+      set_inline((long long)grid * ca.nwb);
+    e = vbhem::launch_split(ca, grid, c.split.lds_l, st);
     if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
   }
   if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
-  if (fold) return VBHEM_OK;  // launch_stats_list runs fb_exact_kernel from flag_count[3]
+  if (inlined) *inlined = ca.xinline != 0;
+  if (fold) return VBHEM_OK;  // inline, or launch_stats_list runs fb_exact_kernel from flag_count[3]
   vbhem::FbArgs a = c.plan.a;
   a.i_begin = i_begin; a.i_end = i_end; a.i_buf0 = i_buf0;
   a.LL = LL; a.nu1 = nu1; a.xi = xi; a.tnu = tnu;
@@ -924,9 +942,11 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
       e = vbhem::launch_gate_list(sa, nchunk, st);
       if (e != hipSuccess) return hip_fail(e, "gate_list_kernel");
       if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
+      bool inl = false;
       rc = run_fb_list(ctx, g0, g1, g0, w.nu1, w.xi, w.tnu, w.E, e_ld, w.list, w.list_tot,
-                       w.group, w.flags, w.scratch, LL_elbo_dev, st, fold);
+                       w.group, w.flags, w.scratch, LL_elbo_dev, st, fold, &inl);
       if (rc != VBHEM_OK) return rc;
+      if (fold) sa.fold = inl ? 2 : 1;  // 2: no fb_exact_kernel launch before the statistics
       ev0 = timing_on(st) ? timing_event(st) : nullptr;
       int ss = nchunk;
       e = vbhem::launch_stats_list(sa, nchunk, sl_lds, st, &ss);

@@ -365,6 +365,7 @@ void fb_list4_kernel(const SplitArgs p) {
         for (int i3 = 0; i3 < 2; ++i3) p.xi[(lp * S + 4 * i2 + r) * S + 4 * i3 + c] = Ap[i2][i3] * H[i2][i3];
       if (pbad && !pnf && lane == 4 * b) {
         // underflow or range with finite inputs: the exact kernel recomputes the pair
+        // (not inline: the exact recursion would take this kernel past 256 VGPRs)
         const int slot = atomicAdd(p.flag_count, 1);
         atomicAdd(p.flag_count + 1, 1);
         p.flag_list[slot] = (int)((size_t)i * K + j);

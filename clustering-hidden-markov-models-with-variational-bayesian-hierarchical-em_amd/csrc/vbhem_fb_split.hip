@@ -29,6 +29,7 @@
 #include <cmath>
 
 #include "vbhem_internal.h"
+#include "vbhem_exact.h"
 #include "vbhem_log_table.h"
 #include "vbhem_math.h"
 
@@ -593,14 +594,34 @@ void fb_split_kernel(const SplitArgs p) {
       atomicOr(&F[q], kFlagBad | (nf ? kFlagNonFinite : 0));
     }
     pair_sync<kWaveLocal>();
+    // inline only for 4 <= S <= 6 (kSplitInline*): past 6 the exact recursion's
+    // registers would push the list kernel into scratch, below 4 they would cost it
+    // occupancy (S = 3: 139 -> 197 VGPRs); at 4..6 the kernel stays at 2 waves per SIMD
+    constexpr bool kXin = MODE == kFbList && S >= kSplitInlineMinS && S <= kSplitInlineMaxS;
+    const bool xin = kXin && pa.xinline;
     if (active && w == 0) {
       const int f = F[q];
       if (f == kFlagBad) {
-        const int slot = atomicAdd(pa.flag_count, 1);
         atomicAdd(pa.flag_count + 1, 1);
-        pa.flag_list[slot] = (int)pair;
+        if (!xin) {
+          const int slot = atomicAdd(pa.flag_count, 1);
+          pa.flag_list[slot] = (int)pair;
+        }
       } else if ((f & kFlagNonFinite) && MODE != kFbList) {
         pa.LL[pair] = __builtin_nan("");
+      }
+    }
+    if constexpr (kXin) {
+      if (xin) {  // wave-uniform: this wave's flagged pairs, recomputed by the whole wave
+        unsigned long long fm = __ballot(active && w == 0 && F[q] == kFlagBad);
+        while (fm) {
+          const int l = __builtin_ctzll(fm);
+          fm &= fm - 1;
+          const int pl = __builtin_amdgcn_readlane((int)pair, l);
+          exact_pair_wave<true>(pa.xf, pl,
+                                pa.xscr + ((size_t)blockIdx.x * (NT >> 6) + (tid >> 6)) * pa.xstride,
+                                nullptr);
+        }
       }
     }
   };

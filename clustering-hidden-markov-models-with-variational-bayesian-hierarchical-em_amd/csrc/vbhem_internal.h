@@ -124,9 +124,10 @@ struct StatsArgs {
   const double *Us;      // the statistics copy of the prepared operand (us_doubles), or null
   int nzero_m;           // stats_list_m_kernel: at most this many parts (slabs) per cluster (0: nzero)
   // the backward pass's exact fallback folded into resp_kernel (the flagged pairs of
-  // each block's bases; the gate-list pass's then get an fb_exact_kernel launch from
-  // flag_count[3] in launch_stats_list) instead of a launch after each pass (fold = 1;
-  // one base group)
+  // each block's bases) instead of a launch after the pass (fold != 0; one base group);
+  // the gate-list pass's flagged pairs: recomputed by the list kernel itself (fold = 2,
+  // SplitArgs::xinline) or an fb_exact_kernel launch from flag_count[3] in
+  // launch_stats_list (fold = 1)
   int fold;
   FbArgs fx;                 // the exact recursion's arguments (outputs, flag counter / list)
   double *xscratch;          // its scratch: xslots slots of xstride doubles
@@ -268,9 +269,19 @@ struct SplitArgs {
   long long e_col0;
   int ekdp, eksp;
   double esmooth;
+  // the gate-list pass's exact fallback inline (xinline; fb_list4_kernel and
+  // fb_split_kernel's list mode): a wavefront that flags a pair recomputes it itself
+  // (exact_pair_wave, vbhem_exact.h; Theta and the small arrays in the wavefront's
+  // scratch slot xscr + wave * xstride, one slot per wavefront of the persistent grid)
+  // instead of listing it for an fb_exact_kernel launch after the pass
+  int xinline;  // fb_split_kernel list mode, kSplitInlineMinS <= S <= kSplitInlineMaxS only
+  double *xscr;
+  long long xstride;
+  FbArgs xf;
 };
 
-constexpr int kK1InKernelMaxKdp = 8;  // d = 2 full / d <= 4 diag: at most 8 fmas per entry
+constexpr int kK1InKernelMaxKdp = 8;
+constexpr int kSplitInlineMinS = 4, kSplitInlineMaxS = 6;  // SplitArgs::xinline: list kernels that take it  // d = 2 full / d <= 4 diag: at most 8 fmas per entry
 
 // the kdp <= 8 operand values u_e of one column (i SB + b) of U (zero past kdp)
 __device__ __forceinline__ void k1_column(const SplitArgs &p, long long col,

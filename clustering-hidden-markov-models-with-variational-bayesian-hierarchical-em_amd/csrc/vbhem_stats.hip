@@ -1632,7 +1632,7 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   // (Folded into stats_list_m_kernel as well it measured no faster when nothing is
   // flagged -- its inlined fallback cost the kernel ~9 us at C4 -- and 3x slower when
   // every base is flagged: one worker wave per block there)
-  if (a.fold) {
+  if (a.fold == 1) {  // (2: the list kernel recomputed its flagged pairs itself)
     hipError_t e = launch_fb_exact(a.fx, a.xscratch, (size_t)a.xstride, kExactSlots, st, true);
     if (e != hipSuccess) return e;
   }

@@ -233,14 +233,16 @@ def test_exact_fallback_fused(vb, vo, fused_mode):
 
 
 @pytest.mark.parametrize("N,K", [(4, 1), (300, 2), (3000, 2)])
-@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}, {"VBHEM_NO_STATS_M": "1"}])
+@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}, {"VBHEM_NO_STATS_M": "1"},
+                                 {"VBHEM_NO_LIST_INLINE": "1"}])
 def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
     """The adversarial cluster wins every base (the other cluster's emissions are far
     worse), so its pairs are flagged by the backward pass AND are gated: the gate-list
-    pass flags them again.  Default: both passes' fallbacks folded into resp_kernel and
-    the MFMA statistics kernel (several resp chunks and statistics parts at N = 300);
-    VBHEM_NO_FOLD_EXACT: two fb_exact_kernel launches; VBHEM_NO_STATS_M: folded into
-    resp_kernel, the exact kernel before the other statistics kernels."""
+    pass flags them again.  Default: the backward pass's fallback folded into resp_kernel
+    (several chunks at N = 300), the list pass's recomputed by the list kernel itself
+    (fb_split_kernel, S = 4: SplitArgs::xinline); VBHEM_NO_LIST_INLINE: an fb_exact_kernel
+    launch for the list pass's instead; VBHEM_NO_FOLD_EXACT: a launch after each pass;
+    VBHEM_NO_STATS_M: the other statistics kernels."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     cs, consts = adversarial_case(1, N=N, K=K)
