@@ -306,7 +306,11 @@ void fb_split_kernel(const SplitArgs p) {
     // ---------------- K2: backward recursion -----------------------------------------------
     // A'(rows of every owner block, my columns r0..r0+SH): register-resident for both sweeps
     // (occupancy is bounded by LDS, not registers)
-    constexpr bool kAtReg = LPC * SH * SH <= 48;  // <= 96 VGPRs
+#ifndef VBHEM_SPLIT_LIST_ATREG_MAXS
+#define VBHEM_SPLIT_LIST_ATREG_MAXS 16
+#endif
+    constexpr bool kAtReg = LPC * SH * SH <= 48 &&  // <= 96 VGPRs
+                            (MODE != kFbList || S <= VBHEM_SPLIT_LIST_ATREG_MAXS);
     // LPC = 1 (one lane per column, rows uniform across the wave): A' is read as
     // scalar operands from global memory (s_load, scalar cache) instead of LDS
     constexpr bool kAtScalar = MODE == kFbBackward && LPC == 1 && !kAtReg;
