@@ -65,7 +65,8 @@ bool timing_on(hipStream_t st, bool fb_launch = false) {
   return cs == hipStreamCaptureStatusNone;
 }
 
-hipEvent_t timing_event(hipStream_t st) {
+// a timing event from the pool, not recorded (st == nullptr), or recorded on st
+hipEvent_t timing_event(hipStream_t st, bool record = true) {
   hipEvent_t ev = nullptr;
   if (!g_timing.pool.empty()) {
     ev = g_timing.pool.back();
@@ -75,7 +76,7 @@ hipEvent_t timing_event(hipStream_t st) {
     // per record, ~6 us of idle GPU around each timed kernel at N = 12,500)
     return nullptr;
   }
-  (void)hipEventRecord(ev, st);
+  if (record) (void)hipEventRecord(ev, st);
   return ev;
 }
 void timing_recycle(hipEvent_t ev) {
@@ -611,7 +612,13 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       if (em0) g_timing.em.emplace_back(em0, timing_event(st));
     }
   }
-  hipEvent_t ev0 = timing_on(st, true) ? timing_event(st) : nullptr;
+  // the backward-only kernels take their timing events into the dispatch itself
+  // (hipExtLaunchKernelGGL: start / end of the kernel, no marker packets around it);
+  // the others are bracketed by two event records
+  const bool ext_timed = c.split.ok && mode == vbhem::kFbBackward && (c.bwd4 || c.bwd12 || c.bwd2_lds);
+  const bool timed = timing_on(st, true);
+  hipEvent_t ev0 = timed ? timing_event(st, !ext_timed) : nullptr;
+  hipEvent_t ev1 = timed && ext_timed ? timing_event(st, false) : nullptr;
   if (c.split.ok) {
     const SplitPlan &sp = mode == vbhem::kFbBackward ? c.bwd : c.split;
     vbhem::SplitArgs ca = sp.a;
@@ -629,7 +636,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       const unsigned all = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::bwd4_resident_blocks()));
       unsigned nb = std::max(1u, std::min(nt4, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
-      e = vbhem::launch_bwd4(ca, (unsigned)ca.K * nb, st);
+      e = vbhem::launch_bwd4(ca, (unsigned)ca.K * nb, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd4_kernel");
     } else if (mode == vbhem::kFbBackward && c.bwd12) {
       // fb_bwd12_kernel, persistent: NB blocks per cluster (x8 when possible)
@@ -638,7 +645,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       const unsigned all = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::bwd12_resident_blocks()));
       unsigned nb = std::max(1u, std::min(nt12, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
-      e = vbhem::launch_bwd12(ca, (unsigned)ca.K * nb, st);
+      e = vbhem::launch_bwd12(ca, (unsigned)ca.K * nb, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd12_kernel");
     } else if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
@@ -649,7 +656,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
                                       std::max(1, vbhem::bwd2_resident_blocks(ca.S, ca.nwb, c.bwd2_lds)));
       unsigned nb = std::max(1u, std::min(nt2, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
-      e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, c.bwd2_lds, st);
+      e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, c.bwd2_lds, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd2_kernel");
     } else {
       if (mode == vbhem::kFbBackward) {  // persistent: NB blocks per cluster (x8 when possible)
@@ -667,7 +674,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
     if (e != hipSuccess) return hip_fail(e, "fb_pairs_kernel");
   }
   if (ev0) {
-    g_timing.fb.emplace_back(ev0, timing_event(st));
+    g_timing.fb.emplace_back(ev0, ev1 ? ev1 : timing_event(st));
     g_timing.fb_pairs.push_back((long long)(i_end - i_begin) * a.K);
   }
   if (fold) {  // resp_kernel takes the flagged pairs (StatsArgs::fold): no exact launch

@@ -28,6 +28,7 @@
 // sv_ref = sv + amax, so L_ref = Lf + amax * rowsum(Ab) and E + L_ref = Ef + Lf
 // with Ef = E + amax * rowsum(Ab) (once per pair).  exp / log are the
 // short-series exp_tabe_n / log_tabe_n (vbhem_math.h): 8 fp64 operations each.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -439,7 +440,8 @@ int bwd2_resident_blocks(int S, int nwb, size_t lds) {
   return fn ? resident_per_cu(fn, nwb * 64, lds) : 1;
 }
 
-hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st) {
+hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st, hipEvent_t t0,
+                       hipEvent_t t1) {
   const void *fn = bwd2_fn_s(a.S);
   if (!fn || a.SB > a.S || !a.Atg) return hipErrorInvalidValue;
   hipError_t e = set_dyn_lds(fn, lds);
@@ -447,7 +449,10 @@ hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_
   switch (a.S) {
 #define VBHEM_B2(s)                                                                         \
   case s:                                                                                   \
-    hipLaunchKernelGGL(fb_bwd2_kernel<s>, dim3(grid), dim3(a.nwb * 64), lds, st, a); \
+    if (t0)                                                                                 \
+      hipExtLaunchKernelGGL(fb_bwd2_kernel<s>, dim3(grid), dim3(a.nwb * 64), lds, st, t0, t1, 0, a); \
+    else                                                                                    \
+      hipLaunchKernelGGL(fb_bwd2_kernel<s>, dim3(grid), dim3(a.nwb * 64), lds, st, a);     \
     break;
     VBHEM_B2(1) VBHEM_B2(2) VBHEM_B2(3) VBHEM_B2(4) VBHEM_B2(5) VBHEM_B2(6) VBHEM_B2(7) VBHEM_B2(8)
     VBHEM_B2(9) VBHEM_B2(10) VBHEM_B2(11) VBHEM_B2(12) VBHEM_B2(13) VBHEM_B2(14) VBHEM_B2(15)

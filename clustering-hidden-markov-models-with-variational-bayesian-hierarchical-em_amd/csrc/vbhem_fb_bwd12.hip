@@ -23,6 +23,7 @@
 // whose inputs could leave the integer range of the maxima, or whose Z underflowed,
 // is flagged to the exact fallback; the per-step underflow test runs only for a
 // cluster with an A' entry below 2^-600.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -331,9 +332,13 @@ int bwd12_resident_blocks() {
   return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd12_kernel), 64 * kNWB12, 0);
 }
 
-hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st) {
+hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0,
+                        hipEvent_t t1) {
   if (!bwd12_supported(a.S, a.SB) || !a.Atg) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fb_bwd12_kernel, dim3(grid), dim3(64 * kNWB12), 0, st, a);
+  if (t0)  // timing events recorded by the dispatch itself (the bench's roofline)
+    hipExtLaunchKernelGGL(fb_bwd12_kernel, dim3(grid), dim3(64 * kNWB12), 0, st, t0, t1, 0, a);
+  else
+    hipLaunchKernelGGL(fb_bwd12_kernel, dim3(grid), dim3(64 * kNWB12), 0, st, a);
   return hipGetLastError();
 }
 

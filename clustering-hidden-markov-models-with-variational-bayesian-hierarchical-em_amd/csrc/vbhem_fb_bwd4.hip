@@ -32,6 +32,7 @@
 // by one ds_bpermute per column block.  This needs |V| < 2^31 ln2/2048 (7.3e5);
 // pairs whose inputs could exceed 7e5 over T steps (|V| <= T (max |E| + log S) for
 // row sums <= 1) go to the exact fallback.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -416,9 +417,13 @@ int bwd4_resident_blocks() {
   return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd4_kernel), 64 * kNWB, 0);
 }
 
-hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st) {
+hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0,
+                       hipEvent_t t1) {
   if (!bwd4_supported(a.S, a.SB) || !a.Atg) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fb_bwd4_kernel, dim3(grid), dim3(64 * kNWB), 0, st, a);
+  if (t0)  // timing events recorded by the dispatch itself (the bench's roofline)
+    hipExtLaunchKernelGGL(fb_bwd4_kernel, dim3(grid), dim3(64 * kNWB), 0, st, t0, t1, 0, a);
+  else
+    hipLaunchKernelGGL(fb_bwd4_kernel, dim3(grid), dim3(64 * kNWB), 0, st, a);
   return hipGetLastError();
 }
 

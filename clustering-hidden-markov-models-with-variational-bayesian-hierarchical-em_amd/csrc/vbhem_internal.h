@@ -317,7 +317,10 @@ int bwd2_waves(int S);            // waves per block (one block per CU)
 size_t bwd2_lds(int S, int nwb);  // dynamic LDS bytes (0: S unsupported)
 int bwd2_ppb(int S, int nwb);     // pairs per block
 int bwd2_resident_blocks(int S, int nwb, size_t lds);
-hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st);
+// t0 / t1 (optional): timing events recorded by the dispatch itself at the kernel's
+// start and end (hipExtLaunchKernelGGL): no marker packets, no idle GPU around it
+hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_t st,
+                       hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 
 // kernel timing hooks for code outside vbhem_capi.hip (null when timing is off)
 void *timing_begin(hipStream_t st);
@@ -329,12 +332,14 @@ bool bwd4_supported(int S, int SB);
 int bwd4_waves();            // waves per block
 int bwd4_ppb();              // pairs per block (one tile per wavefront)
 int bwd4_resident_blocks();  // per CU
-hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st);
+hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0 = nullptr,
+                       hipEvent_t t1 = nullptr);
 // fb_bwd12_kernel (vbhem_fb_bwd12.hip): the same pass for S = 12, SB <= 12 (3 x 3 blocks)
 bool bwd12_supported(int S, int SB);
 int bwd12_ppb();              // pairs per block (one quad per wavefront)
 int bwd12_resident_blocks();  // per CU
-hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st);
+hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0 = nullptr,
+                        hipEvent_t t1 = nullptr);
 
 // fb_list4_kernel (vbhem_fb_list4.hip): the gate-list pass for S = 8, SB <= 8, T = 10
 // with every contraction on v_mfma_f64_4x4x4f64; SplitArgs fields as fb_split_kernel's
