@@ -7,10 +7,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <random>
 #include <string>
 #include <utility>
 #include <vector>
@@ -90,6 +92,16 @@ namespace vbhem {
 void *timing_begin(hipStream_t st) { return timing_on(st) ? timing_event(st) : nullptr; }
 void timing_end_em_math(void *ev0, hipStream_t st) {
   if (ev0) g_timing.emd.emplace_back(static_cast<hipEvent_t>(ev0), timing_event(st));
+}
+// this process's clean tag of the flag head (kFlagPre): random, never 0 (a zeroed head)
+unsigned long long flag_tag() {
+  static const unsigned long long t = [] {
+    std::random_device rd;
+    unsigned long long v = ((unsigned long long)rd() << 32) ^ rd();
+    v ^= (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count();
+    return v | 1ull;
+  }();
+  return t;
 }
 }  // namespace vbhem
 
@@ -315,6 +327,7 @@ bool u_gemm_ok(const vbhem_base_t *b) {
 bool need_u_ws(const vbhem_base_t *b) { return !b->U && u_gemm_ok(b); }
 
 struct PairsWs {
+  int *fpre;   // the flag head (vbhem_internal.h kFlagPre), then
   int *flags;  // [0]=count [1]=total [2..] list
   double *scratch;
   double *tnu;
@@ -330,7 +343,8 @@ size_t carve_pairs(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
                    PairsWs &w) {
   Carver cv(ws);
   const size_t np = (size_t)b->N * c->K;
-  w.flags = cv.take<int>(vbhem::kFlagHead + np);
+  w.fpre = cv.take<int>(vbhem::kFlagPre + vbhem::kFlagHead + np);  // first: see kFlagPre
+  w.flags = w.fpre + vbhem::kFlagPre;
   w.tnu = need_tnu ? cv.take<double>(np * c->S * b->SB) : nullptr;
   w.E = cv.take<double>(np * c->S * b->SB);
   w.W = cv.take<double>(emission_w_doubles(b->d, b->covmode, c->K, c->S));
@@ -348,7 +362,7 @@ struct FusedWs {
   int group;  // bases per group
   int nslab;
   int slab_len;
-  int *flags;
+  int *fpre, *flags;                // the flag head (kFlagPre), the counters and list after it
   int *gate_cnt, *list, *list_tot;  // gated schedule: [nslab][K], [K][group], [K]
   double *Atg;                      // gated schedule: [K][S][S] A' for the backward pass
   double *scratch, *nu1, *xi, *tnu, *Z, *slabs;
@@ -372,7 +386,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.slab_len = R * (int)vbhem_stats_len(K / R, S, b->d, b->covmode);
   // flagged-pair list: with the fallback folded into the consumers the backward pass's
   // entries stay while the gate-list pass appends its own (at most g K + g K)
-  w.flags = cv.take<int>(vbhem::kFlagHead + 2 * g * K);
+  w.fpre = cv.take<int>(vbhem::kFlagPre + vbhem::kFlagHead + 2 * g * K);  // first: see kFlagPre
+  w.flags = w.fpre + vbhem::kFlagPre;
   w.nu1 = cv.take<double>(g * K * S);
   w.xi = cv.take<double>(g * K * S * S);
   w.tnu = cv.take<double>(g * K * S * SB);
@@ -407,6 +422,10 @@ struct FbCtx {
   // (kdp <= 8: C2, C3): both evaluate E from the prepared operand (SplitArgs::eU);
   // no emission GEMM launch, no E traffic
   bool k1_in_kernel = false;
+  // ... and emission_prep_kernel's work inside fb_bwd2_kernel (SplitArgs::prep): set by
+  // the fused call for a prepared operand; fpre = the workspace's flag head
+  bool bwd2_prep = false;
+  int *fpre = nullptr;
   vbhem::EmissionArgs em{};  // K1 GEMM feeding the split kernel
   size_t em_lds = 0;
   // emission_u_kernel: on the prepared operand (base->U) or one built per call in u_ws
@@ -651,6 +670,12 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
       ca.nwb = c.bwd2_nwb;
       if (k1) set_k1_operands(c, i_begin, ca);
+      if (k1 && c.bwd2_prep) {
+        ca.prep = 1;
+        ca.pm = c.em.m; ca.pP = c.em.P; ca.pc = c.em.c; ca.pz = c.em.zfix; ca.pshift = c.em.shift;
+        ca.ftag = reinterpret_cast<unsigned long long *>(c.fpre);
+        ca.ftag_val = vbhem::flag_tag();
+      }
       const unsigned nt2 = (unsigned)((i_end - i_begin + c.bwd2_ppb - 1) / c.bwd2_ppb);
       const unsigned all = (unsigned)(vbhem::device_cus() *
                                       std::max(1, vbhem::bwd2_resident_blocks(ca.S, ca.nwb, c.bwd2_lds)));
@@ -769,10 +794,10 @@ int estep_pairs_impl(const vbhem_base_t *base, const vbhem_cluster_t *clus, int 
   if (rc != VBHEM_OK) return rc;
   ctx.u_ws = w.U;
   if (!ctx.split.ok) {
-    hipError_t e0 = hipMemsetAsync(w.flags, 0, vbhem::kFlagHead * sizeof(int), st);
+    hipError_t e0 = hipMemsetAsync(w.fpre, 0, (vbhem::kFlagPre + vbhem::kFlagHead) * sizeof(int), st);
     if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
   }
-  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, vbhem::kFlagHead);
+  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.fpre, vbhem::kFlagPre + vbhem::kFlagHead);
   if (rc != VBHEM_OK) return rc;
   rc = run_fb(ctx, 0, base->N, 0, LL_elbo_dev, sum_nu_1_dev, sum_xi_dev, tnu, w.E,
               (long long)base->N * base->SB, w.flags,
@@ -899,15 +924,31 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     e = hipMemsetAsync(w.slabs, 0, sizeof(double) * (size_t)nslab_used * w.slab_len, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(slabs)");
   }
+  // a call that returns early leaves the flag head zeroed (tag included): the next
+  // call's in-kernel preparation then zeroes the counters itself
+  struct HeadGuard {
+    int *fpre;
+    hipStream_t st;
+    ~HeadGuard() {
+      if (fpre) (void)hipMemsetAsync(fpre, 0, (vbhem::kFlagPre + vbhem::kFlagHead) * sizeof(int), st);
+    }
+  } guard{w.fpre, st};
   if (!ctx.split.ok) {
-    e = hipMemsetAsync(w.flags, 0, vbhem::kFlagHead * sizeof(int), st);
+    e = hipMemsetAsync(w.fpre, 0, (vbhem::kFlagPre + vbhem::kFlagHead) * sizeof(int), st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(flags)");
   }
   if (gated) ctx.bwd.a.Atg = w.Atg;
-  rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.flags, vbhem::kFlagHead,
-                         gated ? w.Atg : nullptr,
-                         clus->logA);
-  if (rc != VBHEM_OK) return rc;
+  // K1 inside fb_bwd2_kernel on a prepared operand: W' / bias' / A' and the counters'
+  // reset inside that kernel too (no emission_prep_kernel launch)
+  if (gated && ctx.k1_in_kernel && ctx.em.zfix && !std::getenv("VBHEM_NO_BWD2_PREP")) {
+    ctx.em.W = w.W; ctx.em.bias = w.bias; ctx.em.shift = w.shift;
+    ctx.bwd2_prep = true;
+    ctx.fpre = w.fpre;
+  } else {
+    rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.fpre, vbhem::kFlagPre + vbhem::kFlagHead,
+                           gated ? w.Atg : nullptr, clus->logA);
+    if (rc != VBHEM_OK) return rc;
+  }
   // the backward pass's exact fallback folded into resp_kernel (one base group, one
   // trial: one fb_exact_kernel launch less per E-step; the gate-list pass's flags get
   // their launch in launch_stats_list, from flag_count[3]); resp_kernel needs a
@@ -966,8 +1007,9 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
   e = vbhem::launch_stats_final(w.slabs, nslab_used, stats_slabs, w.slab_len, sa.KT, S, sa.SL,
-                                stats_dev, st);
+                                stats_dev, st, w.fpre);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
+  guard.fpre = nullptr;
   return VBHEM_OK;
 }
 
@@ -1067,15 +1109,16 @@ int vbhem_timing_read_emission(double *em_ms, long long *em_launches) {
 }
 
 int vbhem_last_fallback_count(void *stream, const void *workspace_dev) {
-  // flags[1] accumulates over groups of the last fused call; flags[0] is the
-  // last group's (== whole call for the pairs path).
-  int v[2] = {0, 0};
+  // the flag head leads the workspace (vbhem_internal.h kFlagPre): a fused call
+  // leaves its total in [2] and the counters zeroed; the pairs path zeroes [2] and
+  // leaves its count in the counters ([1] the total, [0] the last pass's)
+  int v[vbhem::kFlagPre + 2] = {0};
   if (!workspace_dev) return fail(VBHEM_ERR_ARG, "null workspace");
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e = hipMemcpyAsync(v, workspace_dev, sizeof(v), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "vbhem_last_fallback_count");
-  return std::max(v[0], v[1]);
+  return std::max(v[2], std::max(v[vbhem::kFlagPre], v[vbhem::kFlagPre + 1]));
 }
 
 int vbhem_host_device_pointer(void *host_ptr, void **dev_ptr) {

@@ -33,7 +33,6 @@ namespace vbhem {
 
 namespace {
 typedef double double4_t __attribute__((ext_vector_type(4)));
-constexpr double kLog2PiE = 1.8378770664093454835606594728112353;
 
 __device__ __forceinline__ void packed_ab(int e, int d, int &a, int &b) {
   a = 0;
@@ -116,25 +115,20 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
   if (full) {
     const double *P = p.P + (size_t)r * d * d;
     for (int a = tid; a < d; a += kPrepThreads) {
-      double v = 0.0;  // (P_sym m')_a
-      for (int b = 0; b < d; ++b) {
-        const double ps = 0.5 * (P[a * d + b] + P[b * d + a]);
-        v = fma(ps, mr[b] - zs[b], v);
-      }
+      const double v = em_pm_full(P, mr, zs, a, d);  // (P_sym m')_a
       pm[a] = v;
       Wc[(size_t)(NPF + a) * KSP] = v;  // -(1/2)(-2 v)
     }
     for (int e = tid; e < NPF; e += kPrepThreads) {
       int a, b;
       packed_ab(e, d, a, b);
-      Wc[(size_t)e * KSP] =
-          -0.5 * ((a == b) ? P[a * d + a] : 0.5 * (P[a * d + b] + P[b * d + a]));
+      Wc[(size_t)e * KSP] = em_w_full(P, a, b, d);
     }
     __syncthreads();
     if (tid == 0) {
       double q = 0.0;
       for (int a = 0; a < d; ++a) q = fma(mr[a] - zs[a], pm[a], q);
-      p.bias[r] = -0.5 * (d * kLog2PiE + p.c[r] + q);
+      p.bias[r] = em_bias(d, p.c[r], q);
     }
   } else {
     const double *P = p.P + (size_t)r * d;
@@ -149,7 +143,7 @@ __global__ __launch_bounds__(kPrepThreads) void emission_prep_kernel(EmissionArg
         const double ma = mr[a] - zs[a];
         q = fma(P[a] * ma, ma, q);
       }
-      p.bias[r] = -0.5 * (d * kLog2PiE + p.c[r] + q);
+      p.bias[r] = em_bias(d, p.c[r], q);
     }
   }
 }

@@ -157,14 +157,88 @@ void fb_bwd2_kernel(const SplitArgs p) {
   // in-kernel K1 (p.eU): cluster j's W' columns and bias' staged once per block, read
   // as LDS broadcasts by every tile's prologue
   double *k1w = lds + LY::OFF_K1;  // [kdp][S], then bias' [S]
-  if (p.eU) {
-    for (int x = tid; x < p.ekdp * S; x += NT) {
-      const int e = x / S, k = x - e * S;
-      k1w[x] = p.eW[(size_t)e * p.eksp + (size_t)j * S + k];
+  // cluster j's A' = exp(logA - rowmax) (prep: computed here, else staged from Atg) in
+  // the lattice space until the tiles start
+  double *Ast = Xall;
+  if (p.eU && p.prep) {
+    // emission_prep_kernel's work for cluster j (same arithmetic, vbhem_internal.h em_*):
+    // wave 1 the W' columns and bias' of rows j S + s, waves 2.. A', wave 7 the flag head
+    const int s = tid - 64, d = p.d, kdp = p.ekdp;
+    if (s >= 0 && s < S) {
+      const int r = j * S + s;
+      const double *mr = p.pm + (size_t)r * d, *zs = p.pz;
+      double q = 0.0;
+      int e = 0;
+      if (p.covmode == kCovFull) {
+        const double *P = p.pP + (size_t)r * d * d;
+        for (int a = 0; a < d; ++a)  // packed upper (a <= b), row-major
+          for (int b = a; b < d; ++b) k1w[(e++) * S + s] = em_w_full(P, a, b, d);
+        for (int a = 0; a < d; ++a) {
+          const double v = em_pm_full(P, mr, zs, a, d);
+          k1w[(e++) * S + s] = v;
+          q = fma(mr[a] - zs[a], v, q);
+        }
+      } else {
+        const double *P = p.pP + (size_t)r * d;
+        for (int a = 0; a < d; ++a) k1w[(e++) * S + s] = -0.5 * P[a];
+        for (int a = 0; a < d; ++a) {
+          const double ma = mr[a] - zs[a];
+          k1w[(e++) * S + s] = P[a] * ma;
+          q = fma(P[a] * ma, ma, q);
+        }
+      }
+      for (; e < kdp; ++e) k1w[e * S + s] = 0.0;
+      k1w[kdp * S + s] = em_bias(d, p.pc[r], q);
     }
-    for (int k = tid; k < S; k += NT) k1w[p.ekdp * S + k] = p.ebias[(size_t)j * S + k];
+    const int x = tid - 128;
+    if (x >= 0 && x < S * S) {
+      const int r = x / S, k = x - r * S;
+      const double *la = p.logA + ((size_t)j * S + r) * S;
+      double mx = la[0];
+      for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
+      Ast[x] = exp_nonpos(la[k] - mx);
+    }
+    if (tid == 448) {
+      // the counters are clean when the last call closed them (stats_final_kernel wrote
+      // the tag); else block 0 zeroes them and publishes the tag while the other blocks
+      // wait for it (block 0 is dispatched first and never waits)
+      if (__hip_atomic_load(p.ftag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.ftag_val) {
+        if (bk == 0) {
+          for (int c = 0; c < kFlagHead; ++c)
+            __hip_atomic_store(p.flag_count + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.ftag, p.ftag_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          while (__hip_atomic_load(p.ftag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != p.ftag_val)
+            __builtin_amdgcn_s_sleep(4);
+        }
+      }
+    }
+  } else {
+    if (p.eU) {
+      for (int x = tid; x < p.ekdp * S; x += NT) {
+        const int e = x / S, k = x - e * S;
+        k1w[x] = p.eW[(size_t)e * p.eksp + (size_t)j * S + k];
+      }
+      for (int k = tid; k < S; k += NT) k1w[p.ekdp * S + k] = p.ebias[(size_t)j * S + k];
+    }
+    for (int x = tid; x < S * S; x += NT) Ast[x] = p.Atg[(size_t)j * S * S + x];
   }
   __syncthreads();
+  const bool prep = p.eU && p.prep;
+  if (prep && t0 == 0) {
+    // the first block of cluster j: its W' / bias' / A' for the gate-list pass (and the
+    // padding k-rows of W'), block 0 the shift
+    double *gW = const_cast<double *>(p.eW), *gb = const_cast<double *>(p.ebias);
+    double *gA = const_cast<double *>(p.Atg);
+    for (int x = tid; x < p.ekdp * S; x += NT) {
+      const int e = x / S, k = x - e * S;
+      gW[(size_t)e * p.eksp + (size_t)j * S + k] = k1w[x];
+    }
+    for (int k = tid; k < S; k += NT) gb[(size_t)j * S + k] = k1w[p.ekdp * S + k];
+    for (int x = tid; x < S * S; x += NT) gA[(size_t)j * S * S + x] = Ast[x];
+    if (bk == 0)
+      for (int a = tid; a < p.d; a += NT) p.pshift[a] = p.pz[a];
+  }
 
   const int lane = tid & 63, wave = tid >> 6;
   const int qw = lane / LPP, w = lane - qw * LPP;
@@ -182,16 +256,18 @@ void fb_bwd2_kernel(const SplitArgs p) {
 #pragma unroll
   for (int x = 0; x < NA; ++x) {
     const int e = NA * (lane & 15) + x;
-    aq[x] = e < S * S ? p.Atg[(size_t)j * S * S + e] : 0.0;
+    aq[x] = e < S * S ? Ast[e] : 0.0;
   }
-  // A'[r][0], block-uniform: scalar loads once, kept in SGPRs
+  // A'[r][0], block-uniform: kept in SGPRs
   double a0[S];
-  {
-    typedef const double __attribute__((address_space(4))) cdouble;
-    const cdouble *Ag = (const cdouble *)(p.Atg + (size_t)j * S * S);
 #pragma unroll
-    for (int r = 0; r < S; ++r) a0[r] = Ag[r * S];
+  for (int r = 0; r < S; ++r) {
+    const long long v = __double_as_longlong(Ast[r * S]);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    a0[r] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
   }
+  __syncthreads();  // A' read before the tiles overwrite the lattice space
 
   for (int tile = wave * NB + t0; tile < ntile; tile += NB * NW) {
     const int i = p.i_begin + tile * PPW + (valid ? qw : 0);
@@ -444,6 +520,10 @@ hipError_t launch_bwd2(const SplitArgs &a, unsigned grid, size_t lds, hipStream_
                        hipEvent_t t1) {
   const void *fn = bwd2_fn_s(a.S);
   if (!fn || a.SB > a.S || !a.Atg) return hipErrorInvalidValue;
+  // prep: threads 64 + S (W' rows), 128 + S^2 (A') and 448 (flag head) must exist
+  if (a.prep && (!a.eU || !a.ftag || !a.pm || !a.pP || !a.pc || !a.pz || !a.pshift ||
+                 a.nwb * 64 < 512 || a.ekdp > kK1InKernelMaxKdp))
+    return hipErrorInvalidValue;
   hipError_t e = set_dyn_lds(fn, lds);
   if (e != hipSuccess) return e;
   switch (a.S) {

@@ -278,7 +278,39 @@ struct SplitArgs {
   double *xscr;
   long long xstride;
   FbArgs xf;
+  // fb_bwd2_kernel with K1 inside and prep set: emission_prep_kernel's work in the
+  // kernel (no launch of its own).  Every block computes its cluster's W' / bias' / A'
+  // from the cluster constants with that kernel's arithmetic (em_* below), the first
+  // block of each cluster writes them to eW / ebias / Atg for the gate-list pass, and
+  // the fallback counters are zeroed in the kernel when the flag head's tag is not
+  // ftag_val (kFlagPre)
+  int prep;
+  const double *pm, *pP, *pc, *pz;  // cluster means [K S][d], precisions, constants [K S], shift [d]
+  double *pshift;                   // the shift, copied for the later kernels
+  unsigned long long *ftag;
+  unsigned long long ftag_val;
 };
+
+// emission_prep_kernel's per-row arithmetic, one definition for it and for
+// fb_bwd2_kernel's in-kernel preparation (the same bits either way)
+constexpr double kLog2PiE = 1.8378770664093454835606594728112353;
+__device__ __forceinline__ double em_psym(const double *P, int a, int b, int d) {
+  return 0.5 * (P[a * d + b] + P[b * d + a]);
+}
+// (P_sym m')_a, m' = m - z
+__device__ __forceinline__ double em_pm_full(const double *P, const double *mr, const double *zs,
+                                             int a, int d) {
+  double v = 0.0;
+  for (int b = 0; b < d; ++b) v = fma(em_psym(P, a, b, d), mr[b] - zs[b], v);
+  return v;
+}
+// W' entry of packed (a, b) of the full-covariance quadratic term
+__device__ __forceinline__ double em_w_full(const double *P, int a, int b, int d) {
+  return -0.5 * ((a == b) ? P[a * d + a] : em_psym(P, a, b, d));
+}
+__device__ __forceinline__ double em_bias(int d, double c, double q) {
+  return -0.5 * (d * kLog2PiE + c + q);
+}
 
 constexpr int kK1InKernelMaxKdp = 8;
 constexpr int kSplitInlineMinS = 4, kSplitInlineMaxS = 6;  // SplitArgs::xinline: list kernels that take it  // d = 2 full / d <= 4 diag: at most 8 fmas per entry
@@ -363,6 +395,15 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 //       is folded: resp_kernel takes [0, [3]), the fb_exact_kernel launch before the
 //       statistics the rest)
 constexpr int kFlagHead = 4;
+// Before the counters (flags - kFlagPre): [0..1] a 64-bit clean tag, [2] the last
+// fused call's total ([1] copied there by stats_final_kernel, which then zeroes
+// [0..3] and writes the tag: the counters are clean between calls), [3] unused.
+// fb_bwd2_kernel's in-kernel preparation (SplitArgs::prep) zeroes the counters only
+// when the tag is not this process's flag_tag(); every other path zeroes the
+// kFlagPre + kFlagHead ints before its first pass (emission_prep_kernel, or a memset).
+// Reuse of the memory by another tensor overwrites the tag first (it leads the buffer).
+constexpr int kFlagPre = 4;
+unsigned long long flag_tag();
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
 #ifndef VBHEM_EXACT_BLOCK
 #define VBHEM_EXACT_BLOCK 512
@@ -389,7 +430,9 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
 // sums slabs [0, nslab) of the Nj / Lt1 / Lt7 columns (resp_kernel's per-chunk partials)
 // and slabs [0, nslab_stats) of the N1 / M / U columns (KT clusters x S states per
 // section of SL doubles)
+// fpre (optional): the flag head (flags - kFlagPre) to close: last total, counters
+// zeroed, tag written (kFlagPre)
 hipError_t launch_stats_final(const double *slabs, int nslab, int nslab_stats, int slab_len, int KT,
-                              int S, int SL, double *out, hipStream_t st);
+                              int S, int SL, double *out, hipStream_t st, int *fpre = nullptr);
 
 }  // namespace vbhem

@@ -807,8 +807,17 @@ __global__ __launch_bounds__(kNmThreads) void nm_kernel(const StatsArgs p) {
 constexpr int kFinalCols = 16, kFinalParts = 16;
 __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab_all,
                                                           int nslab_stats, int slab_len, int KT,
-                                                          int S, int SL, double *out) {
+                                                          int S, int SL, double *out, int *fpre,
+                                                          unsigned long long tag) {
   __shared__ double part[kFinalParts][kFinalCols];
+  // the call's last kernel closes the flag head (kFlagPre): the total kept, the counters
+  // zeroed, the tag written -- the next call's in-kernel preparation finds them clean
+  if (fpre && blockIdx.x == 0 && threadIdx.x == 0) {
+    int *fc = fpre + kFlagPre;
+    fpre[2] = fc[1];
+    for (int c = 0; c < kFlagHead; ++c) fc[c] = 0;
+    *reinterpret_cast<unsigned long long *>(fpre) = tag;
+  }
   const int c = threadIdx.x % kFinalCols, pp = threadIdx.x / kFinalCols;
   const int x = blockIdx.x * kFinalCols + c;
   // resp_kernel's columns (Nj, Lt1, Lt7) have a partial in every chunk's slab; the
@@ -1679,10 +1688,11 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
 }
 
 hipError_t launch_stats_final(const double *slabs, int nslab, int nslab_stats, int slab_len, int KT,
-                              int S, int SL, double *out, hipStream_t st) {
+                              int S, int SL, double *out, hipStream_t st, int *fpre) {
   if (nslab_stats < 1 || nslab_stats > nslab || SL < 1 || slab_len % SL != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + kFinalCols - 1) / kFinalCols), dim3(256),
-                     0, st, slabs, nslab, nslab_stats, slab_len, KT, S, SL, out);
+                     0, st, slabs, nslab, nslab_stats, slab_len, KT, S, SL, out, fpre,
+                     fpre ? flag_tag() : 0ull);
   return hipGetLastError();
 }
 

@@ -161,6 +161,68 @@ def test_k1_in_recursion_kernels(vb, vo, S, Sb, d, cov, monkeypatch):
         _capi.set_fused_mode(prev)
 
 
+@pytest.mark.parametrize("S,Sb,d,cov,adv", [(5, 5, 2, 0, False), (3, 3, 2, 1, False),
+                                            (4, 4, 1, 1, False), (6, 4, 4, 0, False),
+                                            (4, 4, 2, 1, True), (5, 3, 2, 0, True)])
+def test_bwd2_in_kernel_prep(vb, vo, S, Sb, d, cov, adv, monkeypatch):
+    """emission_prep_kernel's work inside fb_bwd2_kernel (SplitArgs::prep: the short-K1
+    gated schedule on a prepared operand, C2 / C3): W', bias', A' computed per block with
+    the same arithmetic, the fallback counters zeroed in the kernel unless the previous
+    call left them closed (vbhem_internal.h kFlagPre).  Bit for bit the launch path's
+    outputs (VBHEM_NO_BWD2_PREP=1) over repeated calls, after a call on the other path
+    (its zeroed head) and after garbage in the counters with the tag cleared; the
+    fallback count with them.  adv: cluster 0 underflows for every base (both passes
+    flag it; the exact fallback runs inside the steps)."""
+    from vbhem_amd import _capi
+    prev = _capi.set_fused_mode(_capi.FUSED_GATED)
+    try:
+        N, K, T = 333, 4, 6 if adv else 10
+        if adv:
+            cs, consts = adversarial_case(cov, S=S, Sb=Sb, d=d, N=N, K=K, T=T)
+            consts["c"][1:] = 1.0e4  # cluster 0 wins (gated) for every base
+        else:
+            cs = make_case(N, K, S, Sb, d, cov, seed=5 + S + d, ragged=True, tau=T)
+            consts = cs["consts"]
+        base = cs["base"]
+        tN = torch.as_tensor(100.0 * N * base["omega"], device=DEV)
+        logOmega = np.log(np.full(K, 1.0 / K))
+
+        def run(eng):
+            eng.fused(tN)
+            torch.cuda.synchronize()
+            return (eng.stats.cpu().numpy().copy(), eng.LL.cpu().numpy().copy(),
+                    eng.hatZ.cpu().numpy().copy(), eng.fallback_count())
+
+        monkeypatch.setenv("VBHEM_NO_BWD2_PREP", "1")
+        e0 = engine(vb, base, consts, T)
+        e0.set_log_omega(logOmega)
+        ref = run(e0)
+        del e0
+        monkeypatch.delenv("VBHEM_NO_BWD2_PREP")
+        eng = engine(vb, base, consts, T)
+        eng.set_log_omega(logOmega)
+        outs = [run(eng), run(eng)]
+        monkeypatch.setenv("VBHEM_NO_BWD2_PREP", "1")
+        outs.append(run(eng))  # the launch path: its head zeroed, tag included
+        monkeypatch.delenv("VBHEM_NO_BWD2_PREP")
+        outs.append(run(eng))
+        head = eng._ws_fused.view(torch.int32)
+        head[:2] = 0               # the tag cleared ...
+        head[4:8] = 987654         # ... and garbage in the counters
+        outs.append(run(eng))
+        outs.append(run(eng))
+        for o in outs:
+            for a, b in zip(o[:3], ref[:3]):
+                assert np.array_equal(a, b, equal_nan=True)
+            assert o[3] == ref[3]
+        if adv:
+            assert ref[3] >= N
+        else:
+            assert ref[3] == 0
+    finally:
+        _capi.set_fused_mode(prev)
+
+
 def adversarial_case(cov=1, S=4, Sb=4, d=3, N=4, K=3, T=6):
     """Cluster 0's transitions put all mass on sigma+1 while its emissions put
     all mass on state 0: the factorised normaliser Z ~ e^-600 underflows the
