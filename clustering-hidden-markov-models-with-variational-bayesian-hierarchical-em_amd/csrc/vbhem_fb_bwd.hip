@@ -43,6 +43,10 @@
 #ifndef VBHEM_BWD2_WAVES
 #define VBHEM_BWD2_WAVES(S) ((S) <= 12 ? 3 : 2)
 #endif
+// slab column padding past the even row length (doubles; build switch for A/B)
+#ifndef VBHEM_BWD2_XPAD
+#define VBHEM_BWD2_XPAD(S) 2
+#endif
 
 namespace vbhem {
 
@@ -103,7 +107,7 @@ struct Bwd2Layout {
   static constexpr int PPW = 64 / LPP;               // pairs per wavefront
   static constexpr int NA = (S * S + 15) / 16 > 4 ? (S * S + 15) / 16 : 4;  // A' doubles per lane
   static constexpr int SP = CPL * LPP;               // slab columns (padded)
-  static constexpr int XCS = (S + 1) / 2 * 2 + 2;    // slab column stride (even: 16-B rows)
+  static constexpr int XCS = (S + 1) / 2 * 2 + VBHEM_BWD2_XPAD(S);  // slab column stride (even: 16-B rows)
   static constexpr int XP = SP * XCS + 2;            // per-pair slab (doubles)
   static constexpr int OFF_CL = 0;                   // amax [S], lpi [S] (dynamic LDS)
   // the in-kernel K1's cluster operands (SplitArgs::eU): W' [kdp <= 8][S], bias' [S]
@@ -472,7 +476,7 @@ int bwd2_waves(int S) { return 4 * VBHEM_BWD2_WAVES(S); }
 size_t bwd2_lds(int S, int nwb) {
   if (S < 1 || S > kBwd2MaxS) return 0;
   const int CPL = S <= 8 ? 2 : 1, LPP = (S + CPL - 1) / CPL, PPW = 64 / LPP;
-  const int XCS = (S + 1) / 2 * 2 + 2, XP = CPL * LPP * XCS + 2;
+  const int XCS = (S + 1) / 2 * 2 + VBHEM_BWD2_XPAD(S), XP = CPL * LPP * XCS + 2;
   // dynamic part only (the tables are static): amax, lpi, the in-kernel K1's W' and bias'
   const int off_x = (2 * S + (kK1InKernelMaxKdp + 1) * S + 1) / 2 * 2;
   const int ppb = nwb * PPW;
