@@ -212,8 +212,12 @@ void fb_bwd2_kernel(const SplitArgs p) {
             __hip_atomic_store(p.flag_count + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(p.ftag, p.ftag_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-          while (__hip_atomic_load(p.ftag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != p.ftag_val)
+          // bounded (a lost tag must not hang the device): ~2^22 polls
+          for (int g = 0; g < (1 << 22) &&
+                          __hip_atomic_load(p.ftag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.ftag_val;
+               ++g)
             __builtin_amdgcn_s_sleep(4);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
       }
     }

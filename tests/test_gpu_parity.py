@@ -161,22 +161,26 @@ def test_k1_in_recursion_kernels(vb, vo, S, Sb, d, cov, monkeypatch):
         _capi.set_fused_mode(prev)
 
 
-@pytest.mark.parametrize("S,Sb,d,cov,adv", [(5, 5, 2, 0, False), (3, 3, 2, 1, False),
-                                            (4, 4, 1, 1, False), (6, 4, 4, 0, False),
-                                            (4, 4, 2, 1, True), (5, 3, 2, 0, True)])
-def test_bwd2_in_kernel_prep(vb, vo, S, Sb, d, cov, adv, monkeypatch):
+@pytest.mark.parametrize("S,Sb,d,cov,adv,N,group", [
+    (5, 5, 2, 0, False, 333, None), (3, 3, 2, 1, False, 333, None), (4, 4, 1, 1, False, 333, None),
+    (6, 4, 4, 0, False, 333, None), (4, 4, 2, 1, True, 333, None), (5, 3, 2, 0, True, 333, None),
+    (5, 5, 2, 0, False, 40000, None), (5, 5, 2, 0, True, 5000, None), (5, 5, 2, 0, False, 5000, 1200)])
+def test_bwd2_in_kernel_prep(vb, vo, S, Sb, d, cov, adv, N, group, monkeypatch):
     """emission_prep_kernel's work inside fb_bwd2_kernel (SplitArgs::prep: the short-K1
     gated schedule on a prepared operand, C2 / C3): W', bias', A' computed per block with
     the same arithmetic, the fallback counters zeroed in the kernel unless the previous
-    call left them closed (vbhem_internal.h kFlagPre).  Bit for bit the launch path's
-    outputs (VBHEM_NO_BWD2_PREP=1) over repeated calls, after a call on the other path
-    (its zeroed head) and after garbage in the counters with the tag cleared; the
-    fallback count with them.  adv: cluster 0 underflows for every base (both passes
-    flag it; the exact fallback runs inside the steps)."""
+    call left them closed (vbhem_internal.h kFlagPre); 6 to 512 statistics chunks,
+    several base groups with `group`.  Bit for bit the launch path's outputs
+    (VBHEM_NO_BWD2_PREP=1) over repeated calls, after a call on the other path (its
+    zeroed head), after garbage in the counters with the tag cleared and after garbage
+    in the whole workspace; the fallback count with them.  adv: cluster 0 underflows
+    for every base (both passes flag it; the exact fallback runs inside the steps)."""
     from vbhem_amd import _capi
+    if group:
+        monkeypatch.setenv("VBHEM_GROUP_BASES", str(group))
     prev = _capi.set_fused_mode(_capi.FUSED_GATED)
     try:
-        N, K, T = 333, 4, 6 if adv else 10
+        K, T = 4, 6 if adv else 10
         if adv:
             cs, consts = adversarial_case(cov, S=S, Sb=Sb, d=d, N=N, K=K, T=T)
             consts["c"][1:] = 1.0e4  # cluster 0 wins (gated) for every base
@@ -209,6 +213,8 @@ def test_bwd2_in_kernel_prep(vb, vo, S, Sb, d, cov, adv, monkeypatch):
         head = eng._ws_fused.view(torch.int32)
         head[:2] = 0               # the tag cleared ...
         head[4:8] = 987654         # ... and garbage in the counters
+        outs.append(run(eng))
+        eng._ws_fused.fill_(1)     # garbage everywhere: tag, counters, chunk flags, buffers
         outs.append(run(eng))
         outs.append(run(eng))
         for o in outs:
