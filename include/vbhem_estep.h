@@ -30,6 +30,12 @@
  *     allocation, no host synchronisation, no per-call host state in device
  *     memory), so a call may be captured into a HIP graph and replayed; the
  *     workspace's fallback counters reset themselves on the device.
+ *   - A workspace's contents on entry are arbitrary.  Its first 32 bytes carry the
+ *     fallback counters and a per-process tag from one fused call to the next: a
+ *     call that finds the tag skips zeroing the counters (the short-K1 schedule
+ *     zeroes them inside its first kernel otherwise).  Memory reused for anything
+ *     else overwrites the leading tag first; a caller that writes into a live
+ *     workspace between calls should clear its first 8 bytes.
  */
 #ifndef VBHEM_ESTEP_H
 #define VBHEM_ESTEP_H
