@@ -128,6 +128,7 @@ EXPORTS = {
     "vbhem_rccl_comm_init": (_c_int, [_c_int, _c_int, _vp, _c_int, ctypes.POINTER(_vp)]),
     "vbhem_rccl_comm_destroy": (_c_int, [_vp]),
     "vbhem_rccl_allreduce_sum": (_c_int, [_vp, _vp, _c_size, _vp]),
+    "vbhem_rccl_allreduce_to": (_c_int, [_vp, _vp, _c_size, _vp, _vp]),
     "vbhmm_fb_workspace_bytes": (_c_size, [ctypes.POINTER(SeqsT), _c_int]),
     "vbhmm_fb": (_c_int, [ctypes.POINTER(SeqsT), ctypes.POINTER(HmmParamsT), _vp, _vp, _vp, _vp, _vp,
                           _c_size, _vp]),

@@ -70,6 +70,15 @@ int need_rccl() {
 
 }  // namespace
 
+namespace {
+// the reduced statistics into their destination (mapped pinned host memory): a
+// grid-stride copy, vector stores
+__global__ __launch_bounds__(256) void stats_copy_kernel(double *dst, const double *src, size_t n) {
+  for (size_t x = blockIdx.x * (size_t)blockDim.x + threadIdx.x; x < n; x += (size_t)gridDim.x * blockDim.x)
+    dst[x] = src[x];
+}
+}  // namespace
+
 extern "C" {
 
 int vbhem_rccl_unique_id(void *id) {
@@ -113,6 +122,18 @@ int vbhem_rccl_allreduce_sum(void *comm, double *buf, size_t n, void *stream) {
   const ncclResult_t e = rccl().all_reduce(buf, buf, n, ncclFloat64, ncclSum, static_cast<ncclComm_t>(comm),
                                            static_cast<hipStream_t>(stream));
   return e == ncclSuccess ? VBHEM_OK : rccl_fail(e, "ncclAllReduce");
+}
+
+int vbhem_rccl_allreduce_to(void *comm, double *buf, size_t n, double *out_dev, void *stream) {
+  if (!out_dev && n) return vbhem::set_error(VBHEM_ERR_ARG, "vbhem_rccl_allreduce_to: null destination");
+  if (int rc = vbhem_rccl_allreduce_sum(comm, buf, n, stream)) return rc;
+  if (n == 0) return VBHEM_OK;
+  const unsigned grid = (unsigned)std::min<size_t>(64, (n + 255) / 256);
+  hipLaunchKernelGGL(stats_copy_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     out_dev, buf, n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? VBHEM_OK
+                         : vbhem::set_error(VBHEM_ERR_HIP, std::string("stats_copy_kernel: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

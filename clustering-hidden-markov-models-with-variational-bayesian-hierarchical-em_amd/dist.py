@@ -10,6 +10,7 @@ runs the identical host M-step.  On ROCm the "nccl" backend is RCCL (xGMI);
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Tuple
 
 import torch
@@ -94,6 +95,17 @@ class RcclComm:
         st = torch.cuda.current_stream(t.device).cuda_stream
         _capi.check(self._lib.vbhem_rccl_allreduce_sum(self.handle, _capi.ptr(t), t.numel(), st),
                     "vbhem_rccl_allreduce_sum")
+
+    def allreduce_to(self, t: torch.Tensor, out_dev: int) -> None:
+        """allreduce, then the reduced vector copied in-stream by a kernel to the device
+        address out_dev (EStepEngine.stats_address: the statistics' pinned host buffer)."""
+        from . import _capi
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("RcclComm.allreduce_to: a contiguous fp64 device tensor")
+        st = torch.cuda.current_stream(t.device).cuda_stream
+        _capi.check(self._lib.vbhem_rccl_allreduce_to(self.handle, _capi.ptr(t), t.numel(),
+                                                      ctypes.c_void_p(out_dev), st),
+                    "vbhem_rccl_allreduce_to")
 
     def close(self) -> None:
         if self.handle:

@@ -145,6 +145,11 @@ class EStepEngine:
                                                        ctypes.byref(p)), "vbhem_host_device_pointer")
         return int(p.value)
 
+    def stats_address(self, out: torch.Tensor) -> int:
+        """The device address a kernel writes ``out`` (a statistics vector: device, or
+        pinned host from host_stats_buffer) through."""
+        return self._out_ptr(out)
+
     def _out_ptr(self, out: torch.Tensor) -> int:
         if out.dtype != F64 or not out.is_contiguous() or out.numel() != self.stats_len:
             raise ValueError(f"out must be a contiguous fp64 vector of {self.stats_len} entries")

@@ -36,6 +36,12 @@ int vbhem_rccl_comm_destroy(void *comm);
 /* In-place SUM all-reduce of n doubles on `stream` (asynchronous). */
 int vbhem_rccl_allreduce_sum(void *comm, double *buf, size_t n, void *stream);
 
+/* The same, then the reduced vector copied by a kernel on `stream` into out_dev: the
+ * device address of pinned host memory (vbhem_host_device_pointer), where the host
+ * M-step reads it after one event -- as the one-rank fused call's statistics kernel
+ * writes it there -- with no hipMemcpy between the E-steps of a paced loop. */
+int vbhem_rccl_allreduce_to(void *comm, double *buf, size_t n, double *out_dev, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

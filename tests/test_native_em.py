@@ -177,6 +177,15 @@ def test_native_em_rccl_one_rank(vb):
         comm.allreduce(x)
         torch.cuda.synchronize()
         assert torch.equal(x, torch.arange(10, dtype=torch.float64, device="cuda:0"))
+        # allreduce_to (bench.py's multi-rank E-step tail): the reduced statistics
+        # written by a kernel into the engine's pinned host buffer
+        st = eng.fused(torch.full((300,), 100.0, dtype=torch.float64, device="cuda:0"))
+        want = st.clone()
+        hs = eng.host_stats_buffer()
+        hs.fill_(-1.0)
+        comm.allreduce_to(st, eng.stats_address(hs))
+        torch.cuda.synchronize()
+        assert torch.equal(hs, want.cpu()) and torch.equal(st, want)
     finally:
         comm.close()
     assert got.iters == ref.iters and got.LogLs == ref.LogLs
