@@ -97,7 +97,13 @@ def committed_traffic(config, N, world, want):
     full-size launches are taken alone when the summary separates them (a bench
     run under the profiler also launches the kernel at the shard size)."""
     import glob
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config.lower()}.json")))
+    import re
+
+    def tag_order(path):  # r04z < r04z3 < r04z4 (a plain sort puts r04z_ last)
+        m = re.match(r"r(\d+)([a-z]*)(\d*)_", os.path.basename(path))
+        return (int(m.group(1)), m.group(2), int(m.group(3) or 0)) if m else (-1, "", 0)
+
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config.lower()}.json")), key=tag_order)
     short = want.split("::")[-1].split("<")[0]
     for path in reversed(cands):
         try:
