@@ -263,7 +263,10 @@ def main():
     # all-reduce the device vector, then copy it
     # two of them: with one E-step of run-ahead the next step writes the other one
     hbufs = [eng.host_stats_buffer(), eng.host_stats_buffer()]
-    hs_dev = [eng.stats_address(h) for h in hbufs]
+    try:  # the buffers' device addresses (the kernel copy after the all-reduce)
+        hs_dev = [eng.stats_address(h) for h in hbufs]
+    except Exception:  # noqa: BLE001 -- not mappable here: the stream copy instead
+        hs_dev = None
     host_stats = hbufs[0]
     done = [torch.cuda.Event(), torch.cuda.Event()]
     stream = torch.cuda.current_stream(dev)
@@ -275,11 +278,14 @@ def main():
             eng.fused(tN, out=hs)
         else:
             st = eng.fused(tN)
-            if rccl is not None:
+            if rccl is not None and hs_dev is not None:
                 # reduced, then written into the pinned buffer by a kernel on the same
                 # stream (a hipMemcpy here broke the run-ahead: 0.34 -> 0.63 ms per
                 # 12,500-base step, profiles/r04v2_rccl_pacing.txt)
                 rccl.allreduce_to(st, hs_dev[k % 2])
+            elif rccl is not None:
+                rccl.allreduce(st)
+                hs.copy_(st, non_blocking=True)
             else:
                 allreduce(st)
                 hs.copy_(st, non_blocking=True)
@@ -569,8 +575,10 @@ def main():
                                 f"Nv={opt['Nv']}"),
                    "N": N, "K": K, "S": S, "Sb": Sb, "d": d, "tau": T,
                    "parallelism": f"bases sharded over {world} GPU(s), 1 RCCL all-reduce/E-step"},
-        "collective": ({"kind": "native RCCL communicator (vbhem_rccl_allreduce_to: all-reduce, then "
-                                "an in-stream kernel copy into the pinned statistics buffer)",
+        "collective": ({"kind": ("native RCCL communicator (vbhem_rccl_allreduce_to: all-reduce, then "
+                                 "an in-stream kernel copy into the pinned statistics buffer)"
+                                 if hs_dev is not None else
+                                 "native RCCL communicator (vbhem_rccl_allreduce_sum, then a stream copy)"),
                         "ranks": world}
                        if rccl is not None else
                        {"kind": "torch.distributed all_reduce" if world > 1 else "none (one rank)",
