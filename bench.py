@@ -9,12 +9,15 @@ the packed statistics across ranks, and the statistics' copy to the host
 resident in HBM before the timed region.
 
 Single GPU:   python bench.py [--steps K --warmup W --config C4]
-Multi GPU:    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Multi GPU:    python bench.py --gpus N   (starts N rank processes itself), or
+              python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 Rank 0 prints one JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -182,9 +185,57 @@ def cpu_baseline(vo, base_np, consts, T, N_total, K, target_s):
                 seconds=t, n_sample=n, multi=multi), pr, n
 
 
+def rank_launch_command(n, argv, port):
+    """The torch.distributed.run command that starts n rank processes of this script
+    with the same arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def resolve_world(gpus, env):
+    """How this process runs, from --gpus and the launcher's environment:
+    ("launch", n) -- no WORLD_SIZE and n > 1 ranks asked for: start them;
+    ("rank", world) -- one rank of a world of `world` processes.
+    A --gpus that disagrees with WORLD_SIZE is refused (ValueError)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if gpus is None else int(gpus)
+        if n < 1:
+            raise ValueError(f"--gpus {n}: at least one GPU")
+        return ("launch", n) if n > 1 else ("rank", 1)
+    world = int(ws)
+    if gpus is not None and int(gpus) != world:
+        raise ValueError(f"--gpus {gpus} disagrees with WORLD_SIZE={world} set by the launcher")
+    return ("rank", world)
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes as children (torch.distributed.run) and return their
+    exit status.  Runs before anything in this process touches the GPU; the
+    parent only waits (never exec: see the box rules on processes that have
+    initialised the GPU)."""
+    backend = os.environ.get("VBHEM_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: only {have} GPU(s) visible; RCCL needs one GPU per "
+                  f"rank (VBHEM_BENCH_BACKEND=gloo rehearses several ranks on fewer GPUs)",
+                  file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(rank_launch_command(n, argv, port), env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE set, N > 1 starts them")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4")
@@ -199,13 +250,19 @@ def main():
     ap.add_argument("--no-shard-sim", action="store_true",
                     help="skip the single-GPU run at the 8-GPU shard size (N/8 bases)")
     args = ap.parse_args()
+    try:
+        mode, world = resolve_world(args.gpus, os.environ)
+    except ValueError as ex:
+        print(f"bench.py: {ex}", file=sys.stderr)
+        return 2
+    if mode == "launch":
+        return launch_ranks(world, sys.argv[1:])
 
     import numpy as np
     import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     # one rank per GPU over RCCL ("nccl"); VBHEM_BENCH_BACKEND=gloo rehearses the
     # multi-rank path with several ranks sharing the GPUs there are (host-staged)
@@ -271,24 +328,46 @@ def main():
     done = [torch.cuda.Event(), torch.cuda.Event()]
     stream = torch.cuda.current_stream(dev)
 
+    # the collective's own time, taken only in the instrumented breakdown pass (never
+    # in the timed region): HIP events around the in-stream RCCL call, or the host
+    # clock around a host-staged (gloo) all-reduce
+    ar_timing = {"on": False, "ms": []}
+
+    def collective(st, k, hs):
+        if ar_timing["on"]:
+            if rccl is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            else:
+                torch.cuda.synchronize()
+                h0 = time.perf_counter()
+        if rccl is not None and hs_dev is not None:
+            # reduced, then written into the pinned buffer by a kernel on the same
+            # stream (a hipMemcpy here broke the run-ahead: 0.34 -> 0.63 ms per
+            # 12,500-base step, profiles/r04v2_rccl_pacing.txt)
+            rccl.allreduce_to(st, hs_dev[k % 2])
+        elif rccl is not None:
+            rccl.allreduce(st)
+        else:
+            allreduce(st)
+        if ar_timing["on"]:
+            if rccl is not None:
+                e1.record(stream)
+                e1.synchronize()
+                ar_timing["ms"].append(e0.elapsed_time(e1))
+            else:
+                torch.cuda.synchronize()
+                ar_timing["ms"].append((time.perf_counter() - h0) * 1e3)
+        if not (rccl is not None and hs_dev is not None):
+            hs.copy_(st, non_blocking=True)
+
     def launch(k):
         """Enqueue E-step k: statistics into pinned host buffer k % 2, then an event."""
         hs = hbufs[k % 2]
         if world == 1 and rccl is None and not os.environ.get("VBHEM_BENCH_COPY"):
             eng.fused(tN, out=hs)
         else:
-            st = eng.fused(tN)
-            if rccl is not None and hs_dev is not None:
-                # reduced, then written into the pinned buffer by a kernel on the same
-                # stream (a hipMemcpy here broke the run-ahead: 0.34 -> 0.63 ms per
-                # 12,500-base step, profiles/r04v2_rccl_pacing.txt)
-                rccl.allreduce_to(st, hs_dev[k % 2])
-            elif rccl is not None:
-                rccl.allreduce(st)
-                hs.copy_(st, non_blocking=True)
-            else:
-                allreduce(st)
-                hs.copy_(st, non_blocking=True)
+            collective(eng.fused(tN), k, hs)
         done[k % 2].record(stream)
         return hs
 
@@ -331,9 +410,12 @@ def main():
     if world > 1:
         dist.barrier()
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    per_rank_s = [float(dt.item())]
     if world > 1:
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt.item())
+        gath = [torch.zeros_like(dt) for _ in range(world)]
+        dist.all_gather(gath, dt)
+        per_rank_s = [float(g.item()) for g in gath]
+    dt = max(per_rank_s)
     tk = _capi.timing_read()
     # the same steps with the host waiting on each before launching the next (the
     # rate of an E-step whose statistics must be on the host before anything else)
@@ -351,11 +433,23 @@ def main():
     # with every launch timed (not part of `value`)
     bd_steps = max(1, min(args.steps, 5))
     _capi.timing_enable(True)
+    ar_timing["on"] = True
     for _ in range(bd_steps):
         step()
     torch.cuda.synchronize()
+    ar_timing["on"] = False
     tkb = _capi.timing_read()
     _capi.timing_enable(False)
+    # the kernels the library launched for the two recursion passes (named by the launch)
+    bwd_kernel_launched, list_kernel_launched = _capi.last_kernel(0), _capi.last_kernel(1)
+    # the all-reduce's time per E-step on every rank (breakdown pass), max over ranks
+    ar_ms = float(np.mean(ar_timing["ms"])) if ar_timing["ms"] else None
+    per_rank_ar = [ar_ms]
+    if world > 1:
+        t_ = torch.tensor([ar_ms if ar_ms is not None else -1.0], dtype=torch.float64, device=dev)
+        gath = [torch.zeros_like(t_) for _ in range(world)]
+        dist.all_gather(gath, t_)
+        per_rank_ar = [float(g.item()) if g.item() >= 0 else None for g in gath]
     # fraction of pairs the gate Z > 1e-8 keeps (the gated schedule's second pass)
     zk = (eng.hatZ * tN.view(-1, 1)) > 1e-8
     n_gated = int(zk.sum().item())
@@ -388,6 +482,7 @@ def main():
     torch.cuda.synchronize()
     tkd = _capi.timing_read()
     _capi.timing_enable(False)
+    dense_kernel_launched = _capi.last_kernel(0)
     _capi.set_fused_mode(prev_mode)
     dense_rel = float((dstats - stats).abs().max() / stats.abs().max().clamp_min(1e-300))
 
@@ -528,7 +623,8 @@ def main():
     pairs_per_launch = tk["fb_pairs"] / max(1, tk["fb_launches"])
     split = S <= 16 and Sb <= S and d <= 64
     gated = split and tkb["gated_fwd_launches"] > 0
-    # K1 inside fb_bwd4_kernel / fb_list4_kernel: no emission GEMM launch was timed
+    # K1 inside the recursion kernels (fb_bwd2_kernel and fb_split_kernel's list mode, short
+    # K1 inner dimension): no emission GEMM launch was timed
     k1_fused = gated and tkb["em_launches"] == 0
     if gated:
         fpp = bwd_flops_per_pair(S, Sb, T)
@@ -539,21 +635,13 @@ def main():
     achieved = fpp * pairs_per_launch / (fb_launch_ms * 1e-3) / 1e12
     bpp = fb_bytes_per_pair(S, Sb, d, cov, K, split, backward_only=gated, k1_fused=k1_fused)
     n_exp, n_log = transcendentals_per_pair(S, Sb, T)
-    lpc = 1 if S <= 4 else 2 if S <= 8 else 4      # split_lpc (dense / list modes)
-    lpc_bwd = 1 if S <= 8 else 2                    # split_lpc_bwd (backward mode)
-    if gated and S == 8 and Sb <= 8 and not os.environ.get("VBHEM_NO_BWD4") \
-            and not os.environ.get("VBHEM_NO_BWD2"):
-        kname = "vbhem::fb_bwd4_kernel"   # MFMA contractions (S = 8)
-    elif gated and S == 12 and Sb <= 12 and not os.environ.get("VBHEM_NO_BWD12") \
-            and not os.environ.get("VBHEM_NO_BWD2"):
-        kname = "vbhem::fb_bwd12_kernel"  # MFMA contractions (S = 12)
-    elif gated and S <= 16 and not os.environ.get("VBHEM_NO_BWD2"):
-        kname = f"vbhem::fb_bwd2_kernel<{S}>"
-    else:
-        kname = (f"vbhem::fb_split_kernel<{S}, {lpc_bwd if gated else lpc}, {1 if gated else 0}>"
-                 if split else "vbhem::fb_pairs_kernel")
+    kname = bwd_kernel_launched
     traffic, traffic_src = committed_traffic(args.config, N, world, kname)
+    # the gate-list pass: one launch per base group (14 at C5's N = 10^6); its rate is the
+    # step's gated pairs over the step's summed list-pass time
+    gf_launches_per_step = tkb["gated_fwd_launches"] / bd_steps
     gf_ms = tkb["gated_fwd_ms"] / max(1, tkb["gated_fwd_launches"])
+    gf_step_ms = tkb["gated_fwd_ms"] / bd_steps
     dense_ms = tkd["fb_ms"] / max(1, tkd["fb_launches"])
     dense_fpp = fb_flops_per_pair(S, Sb, T) if split else flops_per_pair(S, Sb, d, T, cov)
     dense_ach = dense_fpp * tkd["fb_pairs"] / max(1, tkd["fb_launches"]) / (dense_ms * 1e-3) / 1e12
@@ -575,14 +663,29 @@ def main():
                                 f"Nv={opt['Nv']}"),
                    "N": N, "K": K, "S": S, "Sb": Sb, "d": d, "tau": T,
                    "parallelism": f"bases sharded over {world} GPU(s), 1 RCCL all-reduce/E-step"},
-        "collective": ({"kind": ("native RCCL communicator (vbhem_rccl_allreduce_to: all-reduce, then "
-                                 "an in-stream kernel copy into the pinned statistics buffer)"
-                                 if hs_dev is not None else
-                                 "native RCCL communicator (vbhem_rccl_allreduce_sum, then a stream copy)"),
-                        "ranks": world}
-                       if rccl is not None else
-                       {"kind": "torch.distributed all_reduce" if world > 1 else "none (one rank)",
-                        "ranks": world, "rccl_error": rccl_err}),
+        "collective": dict(
+            ({"kind": ("native RCCL communicator (vbhem_rccl_allreduce_to: all-reduce, then "
+                       "an in-stream kernel copy into the pinned statistics buffer)"
+                       if hs_dev is not None else
+                       "native RCCL communicator (vbhem_rccl_allreduce_sum, then a stream copy)"),
+              "ranks": world}
+             if rccl is not None else
+             {"kind": ("torch.distributed all_reduce (%s backend)" % backend
+                       if world > 1 else "none (one rank)"),
+              "ranks": world, "rccl_error": rccl_err}),
+            allreduce_ms=(max(a for a in per_rank_ar if a is not None)
+                          if any(a is not None for a in per_rank_ar) else None),
+            allreduce_ms_per_rank=per_rank_ar,
+            allreduce_timing=("HIP events around the in-stream all-reduce call (+ its copy to "
+                              "the pinned buffer), mean over the %d-step breakdown pass; max over "
+                              "ranks" % bd_steps if rccl is not None else
+                              "host clock around the host-staged all-reduce with device syncs, "
+                              "mean over the %d-step breakdown pass; max over ranks" % bd_steps
+                              if world > 1 else None),
+            statistics_doubles=int(stats.numel()),
+            shard_bases_per_rank=[shard_range(N, r, world)[1] - shard_range(N, r, world)[0]
+                                  for r in range(world)],
+            ms_per_step_per_rank=[s / args.steps * 1e3 for s in per_rank_s]),
         "pacing": ("one E-step of run-ahead (the C++ EM loop's): step k+1 is enqueued before "
                    "the host waits for step k's statistics in pinned memory"),
         "synchronous": {"value": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
@@ -627,18 +730,20 @@ def main():
                               "ELBO partials, the all-reduce and the copy to the host; outputs "
                               "equal the dense schedule's (dense_schedule.max_rel_diff_vs_gated)"),
         "gated_pairs_frac": n_gated / float(N * K),
-        "gated_forward": ({"kernel": ("vbhem::fb_list4_kernel<10>" if S == 8 and Sb <= 8 and T == 10
-                                      and not os.environ.get("VBHEM_NO_LIST4")
-                                      else f"vbhem::fb_split_kernel<{S}, {lpc}, 2>"),
+        "gated_forward": ({"kernel": list_kernel_launched,
                            "kernel_ms": gf_ms,
-                           "pairs_per_launch": n_gated / world,
+                           "launches_per_step": gf_launches_per_step,
+                           "ms_per_step": gf_step_ms,
+                           "pairs_per_step": n_gated / world,
                            "flops_per_pair": fb_flops_per_pair(S, Sb, T),
                            "achieved_TFLOPs": fb_flops_per_pair(S, Sb, T) * n_gated / world
-                           / max(gf_ms * 1e-3, 1e-12) / 1e12} if gated else None),
+                           / max(gf_step_ms * 1e-3, 1e-12) / 1e12,
+                           "note": "achieved = the step's gated pairs (this rank) x K2-K4 flops "
+                                   "over the step's summed list-pass launch time"}
+                          if gated else None),
         "dense_schedule": {"value": dense_steps / float(dtd.item()), "unit": "E-steps/s",
                            "steps": dense_steps, "max_rel_diff_vs_gated": dense_rel,
-                           "fb_kernel": (f"vbhem::fb_split_kernel<{S}, {lpc}, 0>" if split
-                                         else "vbhem::fb_pairs_kernel"),
+                           "fb_kernel": dense_kernel_launched,
                            "fb_kernel_ms": dense_ms,
                            "roofline_frac": dense_ach / PEAK_FP64_TFLOPS,
                            "achieved_TFLOPs": dense_ach,
@@ -708,4 +813,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

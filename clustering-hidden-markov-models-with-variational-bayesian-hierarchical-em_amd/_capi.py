@@ -124,6 +124,7 @@ EXPORTS = {
     "vbhem_em_lower_bound_derivs": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp,
                                              _vp, _vp, _vp, _vp]),
     "vbhem_hmms_to_h3m": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_vp] * 15),
+    "vbhem_rccl_available": (_c_int, []),
     "vbhem_rccl_unique_id": (_c_int, [_vp]),
     "vbhem_rccl_comm_init": (_c_int, [_c_int, _c_int, _vp, _c_int, ctypes.POINTER(_vp)]),
     "vbhem_rccl_comm_destroy": (_c_int, [_vp]),
@@ -135,6 +136,7 @@ EXPORTS = {
     "vbhmm_fb_host": (_c_int, [_c_int, ctypes.POINTER(SeqsT), ctypes.POINTER(HmmParamsT), _vp, _vp,
                                _vp, _vp]),
     "vbhem_last_error": (ctypes.c_char_p, []),
+    "vbhem_last_kernel": (ctypes.c_char_p, [_c_int]),
     "vbhem_version": (ctypes.c_char_p, []),
 }
 
@@ -197,6 +199,12 @@ def timing_read() -> dict:
                 stats_ms=st.value, stats_launches=ns.value, em_ms=em.value, em_launches=ne.value,
                 gated_fwd_ms=gf.value, gated_fwd_launches=ng.value, em_math_ms=mm.value,
                 em_math_launches=nm.value)
+
+
+def last_kernel(pass_: int) -> str:
+    """The kernel this thread's last E-step ran for recursion pass 0 (every pair) or
+    1 (the gate-list pass), as the kernel trace names it ("" before any)."""
+    return lib().vbhem_last_kernel(int(pass_)).decode()
 
 
 FUSED_GATED, FUSED_DENSE = 0, 1

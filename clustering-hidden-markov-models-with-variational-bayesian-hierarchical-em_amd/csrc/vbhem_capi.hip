@@ -50,6 +50,14 @@ struct TimingState {
 };
 thread_local TimingState g_timing;
 
+// the kernels the last call of this host thread ran for its recursion passes
+// (vbhem_last_kernel: what a benchmark line names, taken from the launch itself)
+thread_local std::string g_last_kernel[2];
+std::string split_name(const vbhem::SplitArgs &a) {
+  return "vbhem::fb_split_kernel<" + std::to_string(a.S) + ", " + std::to_string(a.lpc) + ", " +
+         std::to_string(a.mode) + ">";
+}
+
 // fused schedule of this host thread (vbhem_set_fused_mode; VBHEM_FUSED_DENSE=1
 // in the environment sets every thread's default)
 int default_fused_mode() {
@@ -109,6 +117,11 @@ namespace {
 
 int fail(int code, const std::string &msg) {
   g_err = msg;
+  // a refused launch (too much LDS, a bad grid) also leaves HIP's per-thread last
+  // error set; left pending it would surface in the caller's next, unrelated HIP
+  // call (torch checks hipGetLastError after each of its launches).  The error is
+  // reported here, through the status and vbhem_last_error(), so it is consumed.
+  if (code == VBHEM_ERR_HIP) (void)hipGetLastError();
   return code;
 }
 
@@ -559,6 +572,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
     const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list4_resident_blocks()));
     e = vbhem::launch_list4(ca, grid, st);
     if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
+    g_last_kernel[1] = "vbhem::fb_list4_kernel<" + std::to_string(ca.T) + ">";
   } else {
     if (c.k1_in_kernel) set_k1_operands(c, i_begin, ca);
     const unsigned grid = list_grid(ca, c.split.lds_l);
@@ -566,6 +580,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
       set_inline((long long)grid * ca.nwb);
     e = vbhem::launch_split(ca, grid, c.split.lds_l, st);
     if (e != hipSuccess) return hip_fail(e, "fb_split_kernel(list)");
+    g_last_kernel[1] = split_name(ca);
   }
   if (ev0) g_timing.gf.emplace_back(ev0, timing_event(st));
   if (inlined) *inlined = ca.xinline != 0;
@@ -657,6 +672,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       if (nb >= 8) nb = nb / 8 * 8;
       e = vbhem::launch_bwd4(ca, (unsigned)ca.K * nb, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd4_kernel");
+      g_last_kernel[0] = "vbhem::fb_bwd4_kernel";
     } else if (mode == vbhem::kFbBackward && c.bwd12) {
       // fb_bwd12_kernel, persistent: NB blocks per cluster (x8 when possible)
       const int ppb = vbhem::bwd12_ppb();
@@ -666,6 +682,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       if (nb >= 8) nb = nb / 8 * 8;
       e = vbhem::launch_bwd12(ca, (unsigned)ca.K * nb, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd12_kernel");
+      g_last_kernel[0] = "vbhem::fb_bwd12_kernel";
     } else if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
       ca.nwb = c.bwd2_nwb;
@@ -681,8 +698,13 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
                                       std::max(1, vbhem::bwd2_resident_blocks(ca.S, ca.nwb, c.bwd2_lds)));
       unsigned nb = std::max(1u, std::min(nt2, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
-      e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, c.bwd2_lds, st, ev1 ? ev0 : nullptr, ev1);
+      // VBHEM_DEBUG_EXTRA_LDS=n: n more bytes of dynamic LDS -- fault injection for the
+      // tests of a refused launch (tests/test_robustness.py), never set in production
+      const char *xl = std::getenv("VBHEM_DEBUG_EXTRA_LDS");
+      const size_t lds2 = c.bwd2_lds + (xl ? (size_t)std::strtoull(xl, nullptr, 10) : 0);
+      e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, lds2, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd2_kernel");
+      g_last_kernel[0] = "vbhem::fb_bwd2_kernel<" + std::to_string(ca.S) + ">";
     } else {
       if (mode == vbhem::kFbBackward) {  // persistent: NB blocks per cluster (x8 when possible)
         unsigned nb = std::max(1u, std::min(ntile, list_grid(ca, sp.lds_bwd) / (unsigned)ca.K));
@@ -691,12 +713,14 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       }
       e = vbhem::launch_split(ca, grid, mode == vbhem::kFbBackward ? sp.lds_bwd : sp.lds, st);
       if (e != hipSuccess) return hip_fail(e, "fb_split_kernel");
+      g_last_kernel[0] = split_name(ca);
     }
   } else {
     const int nib = (i_end - i_begin + a.BI - 1) / a.BI;
     const dim3 grid((unsigned)nib * (unsigned)a.njb);
     e = vbhem::launch_fb(a, grid, c.plan.block, c.plan.lds, st);
     if (e != hipSuccess) return hip_fail(e, "fb_pairs_kernel");
+    g_last_kernel[0] = "vbhem::fb_pairs_kernel";
   }
   if (ev0) {
     g_timing.fb.emplace_back(ev0, ev1 ? ev1 : timing_event(st));
@@ -716,6 +740,10 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
 extern "C" {
 
 const char *vbhem_last_error(void) { return g_err.c_str(); }
+
+const char *vbhem_last_kernel(int pass) {
+  return (pass == 0 || pass == 1) ? g_last_kernel[pass].c_str() : "";
+}
 
 const char *vbhem_version(void) { return "vbhem-mi355x 0.1.0 (gfx950)"; }
 
@@ -940,7 +968,10 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
   if (gated) ctx.bwd.a.Atg = w.Atg;
   // K1 inside fb_bwd2_kernel on a prepared operand: W' / bias' / A' and the counters'
   // reset inside that kernel too (no emission_prep_kernel launch)
-  if (gated && ctx.k1_in_kernel && ctx.em.zfix && !std::getenv("VBHEM_NO_BWD2_PREP")) {
+  // (thread 448 of the block runs the flag-head handshake: blocks of >= 8 waves only;
+  // smaller ones, e.g. a VBHEM_BWD2_WAVES build, take the emission_prep_kernel path)
+  if (gated && ctx.k1_in_kernel && ctx.em.zfix && ctx.bwd2_nwb * 64 >= 512 &&
+      !std::getenv("VBHEM_NO_BWD2_PREP")) {
     ctx.em.W = w.W; ctx.em.bias = w.bias; ctx.em.shift = w.shift;
     ctx.bwd2_prep = true;
     ctx.fpre = w.fpre;
@@ -1118,6 +1149,9 @@ int vbhem_last_fallback_count(void *stream, const void *workspace_dev) {
   hipError_t e = hipMemcpyAsync(v, workspace_dev, sizeof(v), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "vbhem_last_fallback_count");
+  if (v[vbhem::kFlagLost] != 0)
+    return fail(VBHEM_ERR_WORKSPACE, "fb_bwd2_kernel lost the flag-head handshake: the fused "
+                                     "call's statistics are NaN (results untrusted)");
   return std::max(v[2], std::max(v[vbhem::kFlagPre], v[vbhem::kFlagPre + 1]));
 }
 

@@ -213,11 +213,18 @@ void fb_bwd2_kernel(const SplitArgs p) {
           __hip_atomic_store(p.ftag, p.ftag_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         } else {
           // bounded (a lost tag must not hang the device): ~2^22 polls
-          for (int g = 0; g < (1 << 22) &&
-                          __hip_atomic_load(p.ftag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.ftag_val;
-               ++g)
-            __builtin_amdgcn_s_sleep(4);
+          bool seen = false;
+          for (int g = 0; g < (1 << 22) && !seen; ++g) {
+            seen = __hip_atomic_load(p.ftag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.ftag_val;
+            if (!seen) __builtin_amdgcn_s_sleep(4);
+          }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          // timed out: pairs this block flags may be zeroed away by block 0, so the
+          // call's results cannot be trusted -- the sticky word [3] of the flag head
+          // makes stats_final_kernel write NaN statistics (loud, never silent)
+          if (!seen)
+            __hip_atomic_store(reinterpret_cast<int *>(p.ftag) + kFlagLost, 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }

@@ -397,12 +397,16 @@ hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStre
 constexpr int kFlagHead = 4;
 // Before the counters (flags - kFlagPre): [0..1] a 64-bit clean tag, [2] the last
 // fused call's total ([1] copied there by stats_final_kernel, which then zeroes
-// [0..3] and writes the tag: the counters are clean between calls), [3] unused.
+// [0..3] and writes the tag: the counters are clean between calls), [3] kFlagLost:
+// sticky, set by an fb_bwd2_kernel block that gave up waiting for block 0's tag (its
+// flagged pairs may have been zeroed away); stats_final_kernel then writes NaN
+// statistics, every call, until a path that zeroes the head runs.
 // fb_bwd2_kernel's in-kernel preparation (SplitArgs::prep) zeroes the counters only
 // when the tag is not this process's flag_tag(); every other path zeroes the
 // kFlagPre + kFlagHead ints before its first pass (emission_prep_kernel, or a memset).
 // Reuse of the memory by another tensor overwrites the tag first (it leads the buffer).
 constexpr int kFlagPre = 4;
+constexpr int kFlagLost = 3;
 unsigned long long flag_tag();
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
 #ifndef VBHEM_EXACT_BLOCK

@@ -81,6 +81,8 @@ __global__ __launch_bounds__(256) void stats_copy_kernel(double *dst, const doub
 
 extern "C" {
 
+int vbhem_rccl_available(void) { return need_rccl(); }
+
 int vbhem_rccl_unique_id(void *id) {
   if (!id) return vbhem::set_error(VBHEM_ERR_ARG, "vbhem_rccl_unique_id: null id");
   if (int rc = need_rccl()) return rc;

@@ -54,13 +54,46 @@ class RcclComm:
         self.rank = (dist.get_rank(group) if inited else 0) if rank is None else int(rank)
         self.world = (dist.get_world_size(group) if inited else 1) if world is None else int(world)
         self.device = torch.device(device)
+        # 'cuda' without an index: the rank's current device (torch.cuda.set_device),
+        # not GPU 0
+        self.device_index = (self.device.index if self.device.index is not None
+                             else torch.cuda.current_device())
+        self.handle = None
+        self.check_ranks_ready(self.rank, self.world, self.device_index, group)
         idb = (ctypes.c_char * _capi.RCCL_ID_BYTES).from_buffer_copy(
             self.exchange_id(self.rank, self.world, group))
         h = ctypes.c_void_p()
         _capi.check(self._lib.vbhem_rccl_comm_init(self.world, self.rank, idb,
-                                                   int(self.device.index or 0), ctypes.byref(h)),
+                                                   int(self.device_index), ctypes.byref(h)),
                     "vbhem_rccl_comm_init")
         self.handle = h
+
+    @staticmethod
+    def local_status(device_index: int):
+        """None when this process can bind RCCL and use `device_index`, else why not."""
+        from . import _capi
+        lib = _capi.lib()
+        if lib.vbhem_rccl_available() != 0:
+            return lib.vbhem_last_error().decode(errors="replace")
+        if not (0 <= device_index < torch.cuda.device_count()):
+            return f"device {device_index} not visible ({torch.cuda.device_count()} GPUs)"
+        return None
+
+    @classmethod
+    def check_ranks_ready(cls, rank: int, world: int, device_index: int, group=None) -> None:
+        """Every rank's local status gathered on every rank before any collective
+        initialisation; if one rank cannot take part, all of them raise (none is left
+        waiting in ncclCommInitRank for it)."""
+        from . import _capi
+        st = cls.local_status(device_index)
+        every = [st]
+        if world > 1:
+            every = [None] * world
+            dist.all_gather_object(every, st, group=group)
+        bad = [(r, s) for r, s in enumerate(every) if s is not None]
+        if bad:
+            raise _capi.VbhemError("RCCL communicator not created: " +
+                                   "; ".join(f"rank {r}: {s}" for r, s in bad))
 
     @staticmethod
     def exchange_id(rank: int, world: int, group=None) -> bytes:

@@ -24,6 +24,12 @@ extern "C" {
 
 #define VBHEM_RCCL_ID_BYTES 128 /* NCCL_UNIQUE_ID_BYTES */
 
+/* VBHEM_OK when RCCL can be bound in this process (else VBHEM_ERR_UNSUPPORTED):
+ * every rank checks it, and the ranks agree on the result, before any of them
+ * enters the collective initialisation (a rank that cannot would leave the others
+ * waiting inside ncclCommInitRank). */
+int vbhem_rccl_available(void);
+
 /* A communicator id (rank 0 makes it, the caller hands the bytes to every rank). */
 int vbhem_rccl_unique_id(void *id /* [VBHEM_RCCL_ID_BYTES] */);
 

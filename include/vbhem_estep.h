@@ -267,6 +267,12 @@ int vbhem_timing_read_em_math(double *ms, long long *launches);
 
 const char *vbhem_last_error(void);
 const char *vbhem_version(void);
+/* The kernel the calling thread's last E-step ran for a recursion pass, as the
+ * kernel trace names it: pass 0 the every-pair pass (backward-only in the gated
+ * schedule, K2-K4 in the dense one), pass 1 the gated schedule's gate-list pass;
+ * "" before any such launch.  Benchmark labelling only (no reference
+ * counterpart). */
+const char *vbhem_last_kernel(int pass);
 
 #ifdef __cplusplus
 }

@@ -30,3 +30,58 @@ def test_committed_traffic_takes_newest_tag(tmp_path, monkeypatch):
     t, src = bench.committed_traffic("C4", 100000, 1, "vbhem::fb_bwd4_kernel")
     assert t == 4.0 and src == os.path.join("profiles", "r04z4_c4.json")
     assert bench.committed_traffic("C4", 100000, 2, "vbhem::fb_bwd4_kernel") == (None, None)
+
+
+def test_resolve_world_launches_or_runs_as_rank():
+    """--gpus N without WORLD_SIZE starts N ranks; under a launcher the rank count is
+    WORLD_SIZE and a disagreeing --gpus is refused."""
+    import pytest
+
+    import bench
+    assert bench.resolve_world(None, {}) == ("rank", 1)
+    assert bench.resolve_world(1, {}) == ("rank", 1)
+    assert bench.resolve_world(8, {}) == ("launch", 8)
+    assert bench.resolve_world(None, {"WORLD_SIZE": "4"}) == ("rank", 4)
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == ("rank", 4)
+    with pytest.raises(ValueError):
+        bench.resolve_world(2, {"WORLD_SIZE": "4"})
+    with pytest.raises(ValueError):
+        bench.resolve_world(0, {})
+
+
+def test_rank_launch_command_is_torchrun_on_loopback():
+    import bench
+    cmd = bench.rank_launch_command(4, ["--gpus", "4", "--steps", "3"], 29511)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29511"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert os.path.basename(cmd[-5]) == "bench.py"
+
+
+def test_bench_refuses_mismatched_world(monkeypatch):
+    """A --gpus that disagrees with the launcher's WORLD_SIZE exits with status 2
+    before touching torch or the GPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "bench.py"), "--gpus", "2"], env=env,
+        capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "disagrees with WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_nccl_launch_needs_a_gpu_per_rank():
+    """Without enough GPUs the RCCL launch is refused up front (the gloo backend
+    rehearses several ranks on fewer GPUs)."""
+    import subprocess
+
+    import torch
+    if torch.cuda.device_count() >= 2:
+        return
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["VBHEM_BENCH_BACKEND"] = "nccl"
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "bench.py"), "--gpus", "2"], env=env,
+        capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "RCCL needs one GPU per rank" in r.stderr

@@ -215,3 +215,51 @@ def test_c4_shard_sizes_vs_oracle(vb, vo, N):
     run: every pair, hat_Z entry and statistic against the oracle.  (Regression
     for the mid-round-3 two-rank C4 failure)"""
     assert _full_size_vs_oracle(vb, vo, "C4", N=N, chunk=512, nthreads=8) == N
+
+
+@pytest.mark.gpu
+def test_c5_full_size_sampled_vs_oracle(vb, vo):
+    """C5 at its full size (N = 10^6, K = 32, S = Sb = 12, d = 16 full: 14 base groups of
+    <= 74 k bases, 32 M pairs) in one fused call, checked three ways:
+    * L_elbo (elementwise 1e-10) and hat_Z (1e-5) against the oracle on 4,000 bases
+      spread evenly over all N, so every base group is sampled (hat_Z of a base depends
+      on its own L_elbo row only, vbhem_h3m_c_step_fc.m:275-276);
+    * determinism: a second call gives bit-identical statistics, L_elbo and hat_Z;
+    * the gated schedule equals the dense one (every pair's forward sweep,
+      vbhem_compute_Statistics.m:33-55) on the whole statistics vector (1e-9)."""
+    from vbhem_amd import _capi
+    from vbhem_amd.em import tilde_n
+    from vbhem_amd.estep import EStepEngine
+    BaseSet = vb.BaseSet
+    base, P, opt = vb.synth_workload("C5", device=DEV)
+    assert base.N == 1_000_000
+    cov = base.covmode
+    consts = vb.host.cluster_constants(P, cov)
+    logOm = vb.host.log_omega_tilde(P.alpha)
+    eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+    eng.set_clusters(consts)
+    eng.set_log_omega(logOm)
+    tN = tilde_n(eng, opt["Nv"], base.N)
+    vec = eng.fused(tN).clone()
+    LL, hZ = eng.LL.clone(), eng.hatZ.clone()
+    assert eng.fallback_count() == 0
+    vec2 = eng.fused(tN).clone()
+    assert torch.equal(vec, vec2) and torch.equal(eng.LL, LL) and torch.equal(eng.hatZ, hZ)
+    prev = _capi.set_fused_mode(_capi.FUSED_DENSE)
+    try:
+        dvec = eng.fused(tN).clone()
+    finally:
+        _capi.set_fused_mode(prev)
+    K, S, d = P.K, P.S, base.d
+    got, dense = (vb.host.unpack_stats(v.cpu().numpy(), K, S, d, cov) for v in (vec, dvec))
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], dense[k]) < 1e-9, (k, stat_err(got[k], dense[k]))
+    idx = torch.linspace(0, base.N - 1, 4000, device=DEV).round().long().unique()
+    sub = BaseSet(*(t[idx] for t in (base.nstates, base.prior, base.A, base.centres,
+                                     base.covars, base.omega)), cov).numpy()
+    del eng
+    ref = vo.c_estep_pairs(sub, consts, opt["tau"], nthreads=16)
+    ii = idx.cpu().numpy()
+    hz_ref, _ = vo.c_responsibilities(ref["LL_elbo"], tN.cpu().numpy()[ii], logOm)
+    assert elem_err(LL.cpu().numpy()[ii], ref["LL_elbo"]) < RTOL_PAIRS
+    assert hatz_err(hZ.cpu().numpy()[ii], hz_ref) < RTOL_NORTH_STAR
