@@ -5,7 +5,7 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
 LIBDIR   := $(PKG)/lib
-SRCS     := $(PKG)/csrc/vbhem_kernels.hip $(PKG)/csrc/vbhem_fb_split.hip $(PKG)/csrc/vbhem_fb_bwd.hip $(PKG)/csrc/vbhem_fb_bwd4.hip $(PKG)/csrc/vbhem_fb_bwd12.hip $(PKG)/csrc/vbhem_fb_list4.hip $(PKG)/csrc/vbhem_emission.hip $(PKG)/csrc/vbhem_stats.hip $(PKG)/csrc/vbhem_capi.hip $(PKG)/csrc/vbhem_em.hip $(PKG)/csrc/vbhem_em_dev.hip $(PKG)/csrc/vbhem_rccl.hip $(PKG)/csrc/vbhem_h3m.hip $(PKG)/csrc/vbhmm_fb.hip
+SRCS     := $(PKG)/csrc/vbhem_kernels.hip $(PKG)/csrc/vbhem_fb_split.hip $(PKG)/csrc/vbhem_fb_bwd.hip $(PKG)/csrc/vbhem_fb_bwd4.hip $(PKG)/csrc/vbhem_fb_bwd12.hip $(PKG)/csrc/vbhem_fb_list4.hip $(PKG)/csrc/vbhem_fb_list12.hip $(PKG)/csrc/vbhem_emission.hip $(PKG)/csrc/vbhem_stats.hip $(PKG)/csrc/vbhem_capi.hip $(PKG)/csrc/vbhem_em.hip $(PKG)/csrc/vbhem_em_dev.hip $(PKG)/csrc/vbhem_rccl.hip $(PKG)/csrc/vbhem_h3m.hip $(PKG)/csrc/vbhmm_fb.hip
 HDRS     := include/vbhem_estep.h include/vbhem_dist.h include/vbhmm_fb.h $(PKG)/csrc/vbhem_internal.h $(PKG)/csrc/vbhem_math.h $(PKG)/csrc/vbhem_log_table.h include/vbhem_em.h $(PKG)/csrc/vbhem_em_dev.h $(PKG)/csrc/vbhem_exact.h $(PKG)/csrc/vbhem_mfma4.h
 OBJS     := $(patsubst $(PKG)/csrc/%.hip,$(LIBDIR)/%.o,$(SRCS))
 

@@ -431,6 +431,7 @@ struct FbCtx {
   bool bwd12 = false;  // S = 12, SB <= 12: fb_bwd12_kernel (MFMA contractions) instead
   bool bwd4 = false;  // S = 8, SB <= 8: fb_bwd4_kernel (MFMA contractions) instead
   bool list4 = false;  // S = 8, SB <= 8, T = 10: fb_list4_kernel for the gate-list pass
+  bool list12 = false;  // S = 12, SB <= 12, T = 10: fb_list12_kernel for the gate-list pass
   // gated schedule on fb_bwd2_kernel + fb_split_kernel's list mode with a short K1
   // (kdp <= 8: C2, C3): both evaluate E from the prepared operand (SplitArgs::eU);
   // no emission GEMM launch, no E traffic
@@ -491,8 +492,9 @@ int prepare_fb(FbCtx &c, const vbhem_base_t *b, const vbhem_cluster_t *cl, int T
       c.bwd4 = vbhem::bwd4_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD4");
       c.bwd12 = vbhem::bwd12_supported(cl->S, b->SB) && !std::getenv("VBHEM_NO_BWD12");
       c.list4 = vbhem::list4_supported(cl->S, b->SB, T, cl->K) && !std::getenv("VBHEM_NO_LIST4");
+      c.list12 = vbhem::list12_supported(cl->S, b->SB, T, cl->K) && !std::getenv("VBHEM_NO_LIST12");
     }
-    c.k1_in_kernel = c.use_u && c.bwd2_lds && !c.bwd4 && !c.bwd12 && !c.list4 &&
+    c.k1_in_kernel = c.use_u && c.bwd2_lds && !c.bwd4 && !c.bwd12 && !c.list4 && !c.list12 &&
                      c.em.kdp <= vbhem::kK1InKernelMaxKdp && !std::getenv("VBHEM_NO_K1_IN_KERNEL");
   }
   return VBHEM_OK;
@@ -573,6 +575,12 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
     e = vbhem::launch_list4(ca, grid, st);
     if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
     g_last_kernel[1] = "vbhem::fb_list4_kernel<" + std::to_string(ca.T) + ">";
+  } else if (c.list12) {  // S = 12, SB <= 12, T = 10: fb_list12_kernel (MFMA), one wave per quad
+    ca.Atg = c.bwd.a.Atg;
+    const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list12_resident_blocks()));
+    e = vbhem::launch_list12(ca, grid, st);
+    if (e != hipSuccess) return hip_fail(e, "fb_list12_kernel");
+    g_last_kernel[1] = "vbhem::fb_list12_kernel<" + std::to_string(ca.T) + ">";
   } else {
     if (c.k1_in_kernel) set_k1_operands(c, i_begin, ca);
     const unsigned grid = list_grid(ca, c.split.lds_l);

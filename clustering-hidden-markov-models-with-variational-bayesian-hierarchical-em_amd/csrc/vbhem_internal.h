@@ -381,6 +381,12 @@ bool list4_supported(int S, int SB, int T, int K);
 int list4_resident_blocks();  // per CU
 hipError_t launch_list4(const SplitArgs &a, unsigned grid, hipStream_t st);
 
+// fb_list12_kernel (vbhem_fb_list12.hip): the gate-list pass for S = 12, SB <= 12, T = 10
+// (3 x 3 blocks of v_mfma_f64_4x4x4f64, the lattice in registers); fields as fb_list4_kernel
+bool list12_supported(int S, int SB, int T, int K);
+int list12_resident_blocks();  // per CU
+hipError_t launch_list12(const SplitArgs &a, unsigned grid, hipStream_t st);
+
 hipError_t launch_fb(const FbArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t st);
 // Fallback bookkeeping in the workspace's int array `flags`:
 //   [0] pairs flagged by the current pass (consumed and reset by fb_exact_kernel)

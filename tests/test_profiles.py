@@ -1,0 +1,46 @@
+"""The committed profiles reproduce the bench's roofline on their own (CPU).
+
+For every summary under profiles/ written by scripts/prof_summary.py from a
+homogeneous trace (every launch of a kernel the same size, scripts/profile.sh),
+the roofline fraction recomputed from the summary alone -- the traced bench's
+flops per launch over the kernel trace's mean launch time -- agrees with the
+bench line's live-event fraction within 3 %, and the matrix-core counters of the
+MFMA kernels show f64 MFMA work."""
+import glob
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _summaries():
+    out = []
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c*.json"))):
+        if p.endswith("_bench.json"):
+            continue
+        with open(p) as f:
+            s = json.load(f)
+        if "roofline_check" in s and s.get("launch_sizes", "").startswith("homogeneous"):
+            out.append((os.path.basename(p), s))
+    return out
+
+
+def test_some_summary_is_checkable():
+    names = [n for n, _ in _summaries()]
+    assert any(n.endswith("_c4.json") for n in names), names
+
+
+@pytest.mark.parametrize("name,summ", _summaries(), ids=[n for n, _ in _summaries()])
+def test_frac_from_summary_matches_bench(name, summ):
+    c = summ["roofline_check"]
+    # recomputed here from the summary's own numbers (not its stored fraction)
+    frac = c["flops_per_launch"] / (c["trace_mean_ms"] * 1e-3) / 1e12 / c["peak_TFLOPs"]
+    assert abs(frac - c["frac_trace_mean"]) < 1e-12
+    assert abs(frac / c["bench_frac"] - 1.0) < 0.03, (name, frac, c["bench_frac"])
+    k = summ["kernels"][c["kernel"]]
+    assert k["trace_launches_ms"]["n"] == c["trace_launches"]
+    if "mfma" in c["kernel"] or c["kernel"].split("::")[-1].startswith(("fb_bwd4", "fb_bwd12")):
+        if "SQ_INSTS_VALU_MFMA_F64" in c:
+            assert c["SQ_INSTS_VALU_MFMA_F64"] > 0 and c["mfma_f64_flops_per_launch"] > 0
