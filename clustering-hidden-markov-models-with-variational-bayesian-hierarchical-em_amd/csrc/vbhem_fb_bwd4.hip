@@ -71,6 +71,16 @@
 #ifndef VBHEM_BWD4_ZSAFE
 #define VBHEM_BWD4_ZSAFE 1
 #endif
+//   VBHEM_BWD4_SKEW     two quads per wavefront on skewed halves of the step: while
+//                       one quad takes its log and second contraction, the other takes
+//                       its exp and first contraction (independent work side by side
+//                       in every half-step; needs VBHEM_BWD4_QPW=2, BIGLOG, DECOUPLE)
+#ifndef VBHEM_BWD4_SKEW
+#define VBHEM_BWD4_SKEW 0
+#endif
+#if VBHEM_BWD4_SKEW && !(VBHEM_BWD4_QPW == 2 && VBHEM_BWD4_BIGLOG && VBHEM_BWD4_DECOUPLE)
+#error "VBHEM_BWD4_SKEW needs VBHEM_BWD4_QPW=2 with BIGLOG and DECOUPLE"
+#endif
 
 namespace vbhem {
 
@@ -217,6 +227,58 @@ void fb_bwd4_kernel(const SplitArgs p) {
     }
 
     // ---- K2: backward recursion, t = T-1 .. 1 ----
+#if VBHEM_BWD4_SKEW
+    // the first half of a step for quad q: maxima, exp, Z^T = G^T A'^T (-> Zs, mqs)
+    double Zs[kQPW][2][2];
+    int mqs[kQPW][2];
+    auto half_e = [&](int q) {
+      double sf[4], tv[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) sf[x] = red_s(V[q][x / 2][x % 2]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) tv[x] = etab_at(etab, sf[x]);
+      const unsigned w = colmax_rows(max(lo_u(sf[0]), lo_u(sf[2])), max(lo_u(sf[1]), lo_u(sf[3]))) >> 11;
+      const int wq = (int)w - (1 << 20) - 1023;
+      mqs[q][0] = __builtin_amdgcn_ds_bpermute(qsrc0, wq);
+      mqs[q][1] = __builtin_amdgcn_ds_bpermute(qsrc1, wq);
+      unsigned wp0, wp1;
+      split_rows(w - 1010u, wp0, wp1);
+      double vv[4], gg[4];
+      const unsigned wpf[4] = {wp0, wp1, wp0, wp1};
+#pragma unroll
+      for (int x = 0; x < 4; ++x) vv[x] = V[q][x / 2][x % 2];
+      exp_d_n<4>(gg, vv, sf, tv, wpf);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+          Zs[q][jj][i2] = mfma4(gg[2 + jj], AT[1][i2], mfma4(gg[jj], AT[0][i2], 0.0));
+    };
+    // the second half: sv = M + log Z, V = Ef + sv Ab^T
+    auto half_l = [&](int q, auto zs_tag) {
+      constexpr bool ZS_ = decltype(zs_tag)::value;
+      double zf[4], yf[4];
+      const int wqf[4] = {mqs[q][0], mqs[q][0], mqs[q][1], mqs[q][1]};
+#pragma unroll
+      for (int x = 0; x < 4; ++x) zf[x] = Zs[q][x / 2][x % 2];
+      if constexpr (!ZS_)
+        zmin[q] = min(zmin[q], min(min(__double2hiint(zf[0]), __double2hiint(zf[1])),
+                                   min(__double2hiint(zf[2]), __double2hiint(zf[3]))));
+      log_q_n<4, true>(yf, zf, wqf, ltab8);
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          V[q][i2][jj] = mfma4(yf[2 + i2], AbT[q][1][jj], mfma4(yf[i2], AbT[q][0][jj], Ef[q][i2][jj]));
+    };
+    half_e(0);
+    for (int t = T - 1; t >= 1; --t) {
+      half_l(0, zs_tag);
+      half_e(1);
+      if (t > 1) half_e(0);
+      half_l(1, zs_tag);
+    }
+#else
     // each phase over all quads of the wavefront before the next one, so the
     // independent quads sit next to each other in the dependency chain of a step
     // (column maxima -> exp -> MFMA -> log -> MFMA)
@@ -341,6 +403,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) V[q][i2][jj] = mfma4(sv[q][1][i2], AbT[q][1][jj], V[q][i2][jj]);
     }
+#endif
 
     // ---- K3: termination, L_elbo = sum_beta prior_beta log sum_sigma exp(lpi + E + L) ----
 #pragma unroll
