@@ -149,3 +149,44 @@ def test_rccl_id_exchange_two_ranks_gloo(tmp_path):
     mp.spawn(_rccl_id_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     ids = [open(tmp_path / f"id{r}.bin", "rb").read() for r in range(world)]
     assert len(ids[0]) == 128 and ids[0] == ids[1] and any(ids[0])
+
+
+def _ready_worker(rank, world, port, bad_rank, outdir):
+    import torch.distributed as dist
+
+    import pkgload
+    pkgload.load()
+    from vbhem_amd import _capi
+    from vbhem_amd.dist import RcclComm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # this rank's own readiness (RCCL bound, device visible), faked so the test needs
+    # neither a GPU nor RCCL: rank bad_rank cannot take part
+    RcclComm.local_status = staticmethod(lambda dev: "no RCCL here" if rank == bad_rank else None)
+    msg = "ok"
+    try:
+        RcclComm.check_ranks_ready(rank, world, 0)
+    except _capi.VbhemError as ex:
+        msg = str(ex)
+    with open(os.path.join(outdir, f"ready{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("bad_rank", [None, 1])
+def test_rccl_readiness_agreed_before_init(tmp_path, bad_rank):
+    """RcclComm's set-up gathers every rank's readiness before any rank enters
+    ncclCommInitRank: when one rank (here the non-zero one) cannot bind RCCL, every
+    rank raises naming it, instead of rank 0 waiting for it forever."""
+    world = 2
+    mp.spawn(_ready_worker, args=(world, _free_port(), bad_rank, str(tmp_path)), nprocs=world,
+             join=True)
+    msgs = [open(tmp_path / f"ready{r}.txt").read() for r in range(world)]
+    if bad_rank is None:
+        assert msgs == ["ok", "ok"]
+    else:
+        assert all("rank 1: no RCCL here" in m for m in msgs), msgs
