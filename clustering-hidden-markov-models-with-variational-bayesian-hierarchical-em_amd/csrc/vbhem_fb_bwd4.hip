@@ -78,6 +78,10 @@
 #ifndef VBHEM_BWD4_SKEW
 #define VBHEM_BWD4_SKEW 0
 #endif
+//   VBHEM_BWD4_SB       a scheduling barrier right after the exp table reads (A/B)
+#ifndef VBHEM_BWD4_SB
+#define VBHEM_BWD4_SB 0
+#endif
 #if VBHEM_BWD4_SKEW && !(VBHEM_BWD4_QPW == 2 && VBHEM_BWD4_BIGLOG && VBHEM_BWD4_DECOUPLE)
 #error "VBHEM_BWD4_SKEW needs VBHEM_BWD4_QPW=2 with BIGLOG and DECOUPLE"
 #endif
@@ -299,6 +303,11 @@ void fb_bwd4_kernel(const SplitArgs p) {
           for (int jj = 0; jj < 2; ++jj) s[q][i2][jj] = red_s(V[q][i2][jj]);
 #pragma unroll
       for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, s[x / 4][(x / 2) % 2][x % 2]);
+#if VBHEM_BWD4_SB
+      // A/B: every exp table read issued before anything after it (no interleaving that
+      // waits on the first read before the others are out)
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int q = 0; q < kQPW; ++q) {
         const unsigned w = colmax_rows(max(lo_u(s[q][0][0]), lo_u(s[q][1][0])),
