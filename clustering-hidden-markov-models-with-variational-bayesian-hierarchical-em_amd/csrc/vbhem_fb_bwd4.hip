@@ -82,6 +82,11 @@
 #ifndef VBHEM_BWD4_SB
 #define VBHEM_BWD4_SB 0
 #endif
+//   VBHEM_BWD4_PRIO     static priority 1 for the second half of the block's waves
+//                       (MI355X_MICROARCH.md, two waves per SIMD, item 4) (A/B)
+#ifndef VBHEM_BWD4_PRIO
+#define VBHEM_BWD4_PRIO 0
+#endif
 #if VBHEM_BWD4_SKEW && !(VBHEM_BWD4_QPW == 2 && VBHEM_BWD4_BIGLOG && VBHEM_BWD4_DECOUPLE)
 #error "VBHEM_BWD4_SKEW needs VBHEM_BWD4_QPW=2 with BIGLOG and DECOUPLE"
 #endif
@@ -183,6 +188,9 @@ void fb_bwd4_kernel(const SplitArgs p) {
   const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
   const double vlim = kVMax / (double)T - 3.0;
 
+#if VBHEM_BWD4_PRIO
+  if (wave >= kNWB / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // the tile loop, versioned on the underflow test (ZS: the cluster's A' makes it
   // unnecessary, VBHEM_BWD4_ZSAFE)
   auto tiles = [&](auto zs_tag) {
