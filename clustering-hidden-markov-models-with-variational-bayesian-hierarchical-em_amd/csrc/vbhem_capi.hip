@@ -1157,7 +1157,7 @@ int vbhem_last_fallback_count(void *stream, const void *workspace_dev) {
   hipError_t e = hipMemcpyAsync(v, workspace_dev, sizeof(v), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "vbhem_last_fallback_count");
-  if (v[vbhem::kFlagLost] != 0)
+  if (v[vbhem::kFlagLost] == vbhem::kFlagLostMark)
     return fail(VBHEM_ERR_WORKSPACE, "fb_bwd2_kernel lost the flag-head handshake: the fused "
                                      "call's statistics are NaN (results untrusted)");
   return std::max(v[2], std::max(v[vbhem::kFlagPre], v[vbhem::kFlagPre + 1]));

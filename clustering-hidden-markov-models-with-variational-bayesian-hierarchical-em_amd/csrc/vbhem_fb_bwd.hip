@@ -223,7 +223,7 @@ void fb_bwd2_kernel(const SplitArgs p) {
           // call's results cannot be trusted -- the sticky word [3] of the flag head
           // makes stats_final_kernel write NaN statistics (loud, never silent)
           if (!seen)
-            __hip_atomic_store(reinterpret_cast<int *>(p.ftag) + kFlagLost, 1, __ATOMIC_RELAXED,
+            __hip_atomic_store(reinterpret_cast<int *>(p.ftag) + kFlagLost, kFlagLostMark, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }

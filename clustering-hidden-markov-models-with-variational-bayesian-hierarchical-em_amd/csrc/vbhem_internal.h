@@ -404,7 +404,7 @@ constexpr int kFlagHead = 4;
 // Before the counters (flags - kFlagPre): [0..1] a 64-bit clean tag, [2] the last
 // fused call's total ([1] copied there by stats_final_kernel, which then zeroes
 // [0..3] and writes the tag: the counters are clean between calls), [3] kFlagLost:
-// sticky, set by an fb_bwd2_kernel block that gave up waiting for block 0's tag (its
+// sticky, kFlagLostMark set by an fb_bwd2_kernel block that gave up waiting for block 0's tag (its
 // flagged pairs may have been zeroed away); stats_final_kernel then writes NaN
 // statistics, every call, until a path that zeroes the head runs.
 // fb_bwd2_kernel's in-kernel preparation (SplitArgs::prep) zeroes the counters only
@@ -413,6 +413,9 @@ constexpr int kFlagHead = 4;
 // Reuse of the memory by another tensor overwrites the tag first (it leads the buffer).
 constexpr int kFlagPre = 4;
 constexpr int kFlagLost = 3;
+// the value that marks it (not just non-zero: a head of garbage -- memory reused from
+// another tensor, which the in-kernel preparation must accept -- is not a lost handshake)
+constexpr int kFlagLostMark = 0x4C4F5354;
 unsigned long long flag_tag();
 constexpr int kFlagBad = 1, kFlagNonFinite = 2;  // per-pair LDS flag bits
 #ifndef VBHEM_EXACT_BLOCK

@@ -845,7 +845,8 @@ __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, i
 #pragma unroll
     for (int q = 1; q < kFinalParts; ++q) s += part[q][c];
     // a lost flag-head handshake (kFlagLost, fb_bwd2_kernel): results untrusted
-    if (fpre && __hip_atomic_load(fpre + kFlagLost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    if (fpre && __hip_atomic_load(fpre + kFlagLost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    kFlagLostMark)
       s = __builtin_nan("");
     out[x] = s;
   }
