@@ -577,6 +577,7 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
   const int kl = lane >> 4, cl = lane & 15;
   const size_t ldE = (size_t)p.e_ld;
   const double sm = p.smooth;
+  const bool vhem = __builtin_amdgcn_readfirstlane((int)(sm != 1.0)) != 0;
   typedef __attribute__((address_space(3))) void *lds_ptr;
   typedef __attribute__((address_space(1))) void *glb_ptr;
   auto stage = [&](int ch) {
@@ -635,13 +636,25 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
           }
         }
         if (cv) {
+          // the VHEM division (hem_hmm_bwd_fwd_mex.c:848-860) behind a uniform branch:
+          // written as a select, the full fp64 division ran for every stored value
+          if (vhem) {
 #pragma unroll
-          for (int q = 0; q < RC; ++q)
+            for (int q = 0; q < RC; ++q)
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const int row = q * 16 + kl + 4 * v;
-              if (row < KS) Ec[(size_t)row * ldE] = sm != 1.0 ? acc[q][v] / sm : acc[q][v];
-            }
+              for (int v = 0; v < 4; ++v) {
+                const int row = q * 16 + kl + 4 * v;
+                if (row < KS) Ec[(size_t)row * ldE] = acc[q][v] / sm;
+              }
+          } else {
+#pragma unroll
+            for (int q = 0; q < RC; ++q)
+#pragma unroll
+              for (int v = 0; v < 4; ++v) {
+                const int row = q * 16 + kl + 4 * v;
+                if (row < KS) Ec[(size_t)row * ldE] = acc[q][v];
+              }
+          }
         }
 #pragma unroll
         for (int t = 0; t < KQB; ++t) u[t] = un[t];
@@ -693,13 +706,23 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
 #pragma unroll
       for (int n = 0; n < NTW; ++n) {
         if (!cv[n]) continue;
+        if (vhem) {  // (uniform: see above)
 #pragma unroll
-        for (int q = 0; q < RC; ++q)
+          for (int q = 0; q < RC; ++q)
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int row = (ch * RC + q) * 16 + kl + 4 * v;
-            if (row < KS) Ec[n][(size_t)row * ldE] = sm != 1.0 ? acc[n][q][v] / sm : acc[n][q][v];
-          }
+            for (int v = 0; v < 4; ++v) {
+              const int row = (ch * RC + q) * 16 + kl + 4 * v;
+              if (row < KS) Ec[n][(size_t)row * ldE] = acc[n][q][v] / sm;
+            }
+        } else {
+#pragma unroll
+          for (int q = 0; q < RC; ++q)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int row = (ch * RC + q) * 16 + kl + 4 * v;
+              if (row < KS) Ec[n][(size_t)row * ldE] = acc[n][q][v];
+            }
+        }
       }
     }
   }
