@@ -317,10 +317,15 @@ void fb_bwd2_kernel(const SplitArgs p) {
 #pragma unroll
           for (int x = 0; x < kK1InKernelMaxKdp; ++x)
             if (x < kdp) e = fma(k1w[x * S + k], u[x], e);
-          if (p.esmooth != 1.0) e = e / p.esmooth;
-          Ef[c][k] = e + amax[k] * rs;
           V[c][k] = e;
         }
+        // the VHEM division behind a uniform branch (as a select it ran on every entry)
+        if (__builtin_amdgcn_readfirstlane((int)(p.esmooth != 1.0))) {
+#pragma unroll
+          for (int k = 0; k < S; ++k) V[c][k] = V[c][k] / p.esmooth;
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) Ef[c][k] = V[c][k] + amax[k] * rs;
       } else {
 #pragma unroll
         for (int k = 0; k < S; ++k) {

@@ -276,6 +276,10 @@ void fb_split_kernel(const SplitArgs p) {
         const double v = k1_entry(pa, j * S + (rv ? r0 + k : S - 1), u);
         E[k] = rv ? v : -INFINITY;
       }
+      if (__builtin_amdgcn_readfirstlane((int)(pa.esmooth != 1.0))) {  // VHEM (uniform)
+#pragma unroll
+        for (int k = 0; k < SH; ++k) E[k] = E[k] / pa.esmooth;
+      }
     } else {
       const double *Ep = pa.E + (size_t)j * S * pa.e_ld + (size_t)(ic - pa.i_buf0) * SB + bc;
 #pragma unroll

@@ -325,14 +325,16 @@ __device__ __forceinline__ void k1_column(const SplitArgs &p, long long col,
     u[e] = e < p.ekdp ? Ut[(e >> 2) * 64 + (e & 3) * 16] : 0.0;
 }
 // E of cluster row jr = j S + sigma at that column: bias' + sum_e W'[e][jr] u_e in e
-// order (the GEMM's sums, blocked differently: equal to rounding)
+// order (the GEMM's sums, blocked differently: equal to rounding), before the VHEM
+// division by esmooth (the caller applies it behind a uniform branch: written as a
+// select, the fp64 division ran for every entry on the VBHEM path too)
 __device__ __forceinline__ double k1_entry(const SplitArgs &p, int jr,
                                            const double (&u)[kK1InKernelMaxKdp]) {
   double acc = p.ebias[jr];
 #pragma unroll
   for (int e = 0; e < kK1InKernelMaxKdp; ++e)
     if (e < p.ekdp) acc = fma(p.eW[(size_t)e * p.eksp + jr], u[e], acc);
-  return p.esmooth != 1.0 ? acc / p.esmooth : acc;
+  return acc;
 }
 bool split_supported(int S, int SB, int d);
 int split_lpc(int S);      // lanes per column
