@@ -560,7 +560,7 @@ __global__ __launch_bounds__(kUThreads) void us_build_kernel(UPrepArgs p, double
 #ifndef UNWAVE_MAXT
 #define UNWAVE_MAXT 512  // launch bound of emission_u_kernel (threads per block)
 #endif
-template <int KQB, int RC, int NTW, bool EXACT, bool PF = false, bool PIPE = false>
+template <int KQB, int RC, int NTW, bool EXACT, bool PF = false>
 __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -597,105 +597,6 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  if constexpr (PIPE) {
-    // W' in several chunks (C5), one 4-wave block per CU with TWO chunk buffers: the
-    // next chunk's LDS-DMA is issued before this chunk's MFMAs and has landed by their
-    // end, so no wave waits for staging (the single-buffer loop below stages every chunk
-    // behind a barrier and relies on a second block per CU to fill the gap).  One
-    // barrier per chunk: every wave is done with the buffer the next DMA overwrites.
-    const int cw = kq * RC * 64 + RC * 16;  // doubles per buffer: W' chunk, then bias'
-    auto issue = [&](int ch, double *buf) {
-      const int nblk = kq * RC / 2;
-      for (int b = wave; b < nblk; b += NW) {
-        const int x = b * 128 + 2 * lane;
-        const int t = x / (RC * 64), rem = x - t * (RC * 64), rt = rem >> 6, l = rem & 63;
-        const int row = (ch * RC + rt) * 16 + (l & 15), e = 4 * t + (l >> 4);
-        __builtin_amdgcn_global_load_lds((glb_ptr)(p.W + (size_t)e * p.ksp + row),
-                                         (lds_ptr)(buf + (size_t)b * 128), 16, 0, 0);
-      }
-      // bias' of the chunk (RC 16 doubles) by the last wave's lanes, 16 B each
-      if (wave == NW - 1 && lane < RC * 8)
-        __builtin_amdgcn_global_load_lds((glb_ptr)(p.bias + ch * RC * 16 + 2 * lane),
-                                         (lds_ptr)(buf + (size_t)kq * RC * 64), 16, 0, 0);
-    };
-    const long long G = rounds * nchunk;
-    if (G > 0) issue(0, lds);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    double u[NTW][KQB];
-    double *Ec[NTW];
-    bool cv[NTW];
-#pragma unroll 1
-    for (long long g = 0; g < G; ++g) {
-      const long long r = g / nchunk;
-      const int ch = (int)(g - r * nchunk);
-      if (ch == 0) {
-#pragma unroll
-        for (int n = 0; n < NTW; ++n) {
-          const long long tile = t_first + r * per_round + ((long long)blockIdx.x * NW + wave) * NTW + n;
-          const bool tv = tile < t_last;
-          const double *Ut = p.U + kUHead + (size_t)(tv ? tile : t_first) * kq * 64 + lane;
-#pragma unroll
-          for (int t = 0; t < KQB; ++t) {
-            if (t < kq) u[n][t] = Ut[(size_t)t * 64];
-            else u[n][t] = 0.0;
-          }
-          const long long col = p.u_col0 + tile * 16 + cl;
-          cv[n] = tv && col >= c_begin && col < c_end;
-          Ec[n] = p.E + (cv[n] ? col - (long long)p.i_buf0 * SB : 0);
-        }
-      }
-      const double *Wc = lds + (size_t)(g & 1) * cw;
-      if (g + 1 < G) issue((int)((g + 1) % nchunk), lds + (size_t)((g + 1) & 1) * cw);
-      const double *bc = Wc + (size_t)kq * RC * 64;
-      double4_t acc[NTW][RC];
-#pragma unroll
-      for (int q = 0; q < RC; ++q)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const double b = bc[q * 16 + kl + 4 * v];
-#pragma unroll
-          for (int n = 0; n < NTW; ++n) acc[n][q][v] = b;
-        }
-#pragma unroll
-      for (int t = 0; t < KQB; ++t) {
-        if (t < kq) {
-#pragma unroll
-          for (int q = 0; q < RC; ++q) {
-            const double w = Wc[(t * RC + q) * 64 + lane];
-#pragma unroll
-            for (int n = 0; n < NTW; ++n)
-              acc[n][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, u[n][t], acc[n][q], 0, 0, 0);
-          }
-        }
-      }
-      // the next chunk's DMA (issued before the MFMAs) has landed; then the stores
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int n = 0; n < NTW; ++n) {
-        if (!cv[n]) continue;
-        if (vhem) {
-#pragma unroll
-          for (int q = 0; q < RC; ++q)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const int row = (ch * RC + q) * 16 + kl + 4 * v;
-              if (row < KS) Ec[n][(size_t)row * ldE] = acc[n][q][v] / sm;
-            }
-        } else {
-#pragma unroll
-          for (int q = 0; q < RC; ++q)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const int row = (ch * RC + q) * 16 + kl + 4 * v;
-              if (row < KS) Ec[n][(size_t)row * ldE] = acc[n][q][v];
-            }
-        }
-      }
-      __syncthreads();  // every wave done with buffer g & 1 (the DMA after next writes it)
-    }
-    return;
-  }
   if (nchunk == 1) stage(0);
   if constexpr (PF) {  // NTW == 1, W' in one chunk (the launcher checks)
     {
@@ -876,28 +777,20 @@ bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   return true;
 }
 
-template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false, bool PIPE = false>
+template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false>
 static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st) {
   if (EXACT && a.kdp / 4 != KQB) return hipErrorInvalidValue;
   if (PF && (NTW != 1 || a.ksp / 16 != RC)) return hipErrorInvalidValue;
-  EmissionArgs ap = a;
-  if (PIPE) {  // two chunk buffers, one block per CU of 8 waves (VBHEM_EMPIPE_WAVES=4: 4)
-    if (a.ksp / 16 <= RC) return hipErrorInvalidValue;
-    lds = 2 * ((size_t)(a.kdp / 4) * RC * 64 + (size_t)RC * 16) * sizeof(double);
-    const char *ev = std::getenv("VBHEM_EMPIPE_WAVES");
-    ap.nwave = (ev && std::atoi(ev) == 4) ? 4 : 8;
-  }
-  const EmissionArgs &a2 = ap;
-  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF, PIPE>;
+  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
-  const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), a2.nwave * 64, lds);
+  const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), a.nwave * 64, lds);
   const long long c_begin = (long long)a.i_begin * a.SB, c_end = (long long)a.i_end * a.SB;
   const long long ntile = (c_end - a.u_col0 + 15) / 16 - (c_begin - a.u_col0) / 16;
-  const long long want = (ntile + (long long)a2.nwave * NTW - 1) / ((long long)a2.nwave * NTW);
+  const long long want = (ntile + (long long)a.nwave * NTW - 1) / ((long long)a.nwave * NTW);
   const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, (long long)cus * per_cu));
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(a2.nwave * 64), lds, st, a2);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(a.nwave * 64), lds, st, a);
   return hipGetLastError();
 }
 
@@ -967,11 +860,7 @@ hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
     if (a.ukqb == 4) return one ? launch_u_fn<4, 8, 1, false, true>(a, lds, st) : launch_u_fn<4, 8, 1>(a, lds, st);
     if (a.ukqb == 12) return one ? launch_u_fn<12, 8, 1, false, true>(a, lds, st) : launch_u_fn<12, 8, 1>(a, lds, st);
     // W' restaged per chunk: two column tiles per wave halve the staging per column
-    if (a.kdp / 4 == 38) {  // d = 16 full (C5): double-buffered chunks unless VBHEM_NO_EMPIPE
-      if (a.nwave == 4 && !std::getenv("VBHEM_NO_EMPIPE"))
-        return launch_u_fn<38, 4, UNTW, true, false, true>(a, lds, st);
-      return launch_u_fn<38, 4, UNTW, true>(a, lds, st);
-    }
+    if (a.kdp / 4 == 38) return launch_u_fn<38, 4, UNTW, true>(a, lds, st);  // d = 16 full (C5)
     return launch_u_fn<kUMaxKq, 4, UNTW>(a, lds, st);
   }
   if (a.wfull) {
