@@ -17,7 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _summaries():
     out = []
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c*.json"))):
+    paths = glob.glob(os.path.join(ROOT, "profiles", "r*_c*.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "r*_shard.json"))
+    for p in sorted(paths):
         if p.endswith("_bench.json"):
             continue
         with open(p) as f:
@@ -42,7 +44,10 @@ def test_frac_from_summary_matches_bench(name, summ):
     # recomputed here from the summary's own numbers (not its stored fraction)
     frac = c["flops_per_launch"] / (c["trace_mean_ms"] * 1e-3) / 1e12 / c["peak_TFLOPs"]
     assert abs(frac - c["frac_trace_mean"]) < 1e-12
-    assert abs(frac / c["bench_frac"] - 1.0) < 0.03, (name, frac, c["bench_frac"])
+    # 3 % at the configs' sizes; the 12,500-base shard's launch is 0.19 ms, where the
+    # dispatch-recorded events of the bench's live timing add ~7 % to the kernel trace's time
+    tol = 0.10 if name.endswith("_shard.json") else 0.03
+    assert abs(frac / c["bench_frac"] - 1.0) < tol, (name, frac, c["bench_frac"])
     k = summ["kernels"][c["kernel"]]
     assert k["trace_launches_ms"]["n"] == c["trace_launches"]
     if "mfma" in c["kernel"] or c["kernel"].split("::")[-1].startswith(("fb_bwd4", "fb_bwd12")):
