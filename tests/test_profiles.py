@@ -44,9 +44,11 @@ def test_frac_from_summary_matches_bench(name, summ):
     # recomputed here from the summary's own numbers (not its stored fraction)
     frac = c["flops_per_launch"] / (c["trace_mean_ms"] * 1e-3) / 1e12 / c["peak_TFLOPs"]
     assert abs(frac - c["frac_trace_mean"]) < 1e-12
-    # 3 % at the configs' sizes; the 12,500-base shard's launch is 0.19 ms, where the
-    # dispatch-recorded events of the bench's live timing add ~7 % to the kernel trace's time
-    tol = 0.10 if name.endswith("_shard.json") else 0.03
+    # 3 % for launches of a millisecond or more (C4, C5); the bench's live timing takes
+    # its two HIP events from the dispatch itself, which adds the ~5-14 us of wave launch
+    # and drain to the kernel trace's time -- 7 % of the 0.19 ms shard-size launch, 12 %
+    # of C3's 0.047 ms one -- so those are held to 15 %
+    tol = 0.03 if c["trace_mean_ms"] >= 1.0 else 0.15
     assert abs(frac / c["bench_frac"] - 1.0) < tol, (name, frac, c["bench_frac"])
     k = summ["kernels"][c["kernel"]]
     assert k["trace_launches_ms"]["n"] == c["trace_launches"]
