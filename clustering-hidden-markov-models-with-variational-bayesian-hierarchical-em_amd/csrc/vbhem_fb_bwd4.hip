@@ -311,6 +311,10 @@ void fb_bwd4_kernel(const SplitArgs p) {
           for (int jj = 0; jj < 2; ++jj) s[q][i2][jj] = red_s(V[q][i2][jj]);
 #pragma unroll
       for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, s[x / 4][(x / 2) % 2][x % 2]);
+#ifdef VBHEM_ABL_NOETAB  // ablation (timing only, wrong results): no exp table read
+#pragma unroll
+      for (int x = 0; x < NE; ++x) tv[x] = 1.0;
+#endif
 #if VBHEM_BWD4_SB
       // A/B: every exp table read issued before anything after it (no interleaving that
       // waits on the first read before the others are out)

@@ -114,6 +114,9 @@ __device__ __forceinline__ void log_m_n(double (&y)[N], const double (&z)[N], co
 // column maxima of a quad's two column blocks: x0 / x1 = this lane row's maximum of
 // block J = 0 / 1; the result's lane row r holds block J = r & 1 (over all 4 rows)
 __device__ __forceinline__ unsigned colmax_rows(unsigned x0, unsigned x1) {
+#ifdef VBHEM_ABL_NOPERM  // ablation (timing only, wrong results): no cross-row maxima
+  return max(x0, x1);
+#endif
   const auto a = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
   const unsigned u = max((unsigned)a[0], (unsigned)a[1]);
   const auto b = __builtin_amdgcn_permlane32_swap(u, u, false, false);
@@ -197,8 +200,12 @@ __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], co
     asm("" : "+v"(ex));
     const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
     zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+#ifdef VBHEM_ABL_NOLTAB  // ablation (timing only, wrong results): no log table read
+    const double2 e = {1.0, 0.0};
+#else
     const double2 e = *reinterpret_cast<const double2 *>(
         __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 3) & 0x1fff0u), 16));
+#endif
     ic[x] = e.x;
     w[x] = fma((double)kk, DEC ? 0x1.62e42fefa39efp-1 : kLn2N, e.y);
   }
