@@ -560,7 +560,7 @@ __global__ __launch_bounds__(kUThreads) void us_build_kernel(UPrepArgs p, double
 #ifndef UNWAVE_MAXT
 #define UNWAVE_MAXT 512  // launch bound of emission_u_kernel (threads per block)
 #endif
-template <int KQB, int RC, int NTW, bool EXACT, bool PF = false>
+template <int KQB, int RC, int NTW, bool EXACT, bool PF = false, int SPL = 1>
 __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -603,36 +603,46 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
   if constexpr (PF) {  // NTW == 1, W' in one chunk (the launcher checks)
     {
       // W' resident for the whole kernel: the next round's tile of U is loaded while
-      // this round's MFMAs run (one tile per wave, double-buffered in registers)
+      // this round's MFMAs run (one item per wave, double-buffered in registers).  An
+      // item is a 16-column tile's RC / SPL row tiles: SPL = 2 for small base counts
+      // (a 12,500-base shard: 6,250 tiles on 3,072 waves ran as 3 rounds for 2.03 of
+      // work; as 12,500 half-tiles, 5 rounds for 4.07), each half reading the tile's U
+      constexpr int RCI = RC / SPL;
+      const long long nitem = (t_last - t_first) * SPL;
+      const long long rounds_i = (nitem + per_round - 1) / per_round;
+      auto item_at = [&](long long r) { return r * per_round + (long long)blockIdx.x * NW + wave; };
       auto load_u = [&](long long r, double (&u)[KQB]) {
-        const long long tile = t_first + r * per_round + (long long)blockIdx.x * NW + wave;
-        const double *Ut = p.U + kUHead + (size_t)(tile < t_last ? tile : t_first) * kq * 64 + lane;
+        const long long it = item_at(r);
+        const long long tile = t_first + (it < nitem ? it / SPL : 0);
+        const double *Ut = p.U + kUHead + (size_t)tile * kq * 64 + lane;
 #pragma unroll
         for (int t = 0; t < KQB; ++t) u[t] = t < kq ? Ut[(size_t)t * 64] : 0.0;
       };
       double u[KQB], un[KQB];
-      if (rounds > 0) load_u(0, u);
+      if (rounds_i > 0) load_u(0, u);
 #pragma unroll 1
-      for (long long r = 0; r < rounds; ++r) {
-        const long long tile = t_first + r * per_round + (long long)blockIdx.x * NW + wave;
+      for (long long r = 0; r < rounds_i; ++r) {
+        const long long it = item_at(r);
+        const long long tile = t_first + it / SPL;
+        const int q0 = SPL == 1 ? 0 : (int)(it % SPL) * RCI;
         const long long col = p.u_col0 + tile * 16 + cl;
-        const bool cv = tile < t_last && col >= c_begin && col < c_end;
+        const bool cv = it < nitem && col >= c_begin && col < c_end;
         double *Ec = p.E + (cv ? col - (long long)p.i_buf0 * SB : 0);
-        if (r + 1 < rounds) load_u(r + 1, un);
+        if (r + 1 < rounds_i) load_u(r + 1, un);
         // W' is loop-invariant: an opaque offset keeps its LDS reads in the loop
         // (hoisted, 88 values would take 176 VGPRs)
-        int woff = lane, boff = kl;
+        int woff = lane + q0 * 64, boff = kl + q0 * 16;
         asm volatile("" : "+v"(woff), "+v"(boff));
-        double4_t acc[RC];
+        double4_t acc[RCI];
 #pragma unroll
-        for (int q = 0; q < RC; ++q)
+        for (int q = 0; q < RCI; ++q)
 #pragma unroll
           for (int v = 0; v < 4; ++v) acc[q][v] = bl[q * 16 + boff + 4 * v];
 #pragma unroll
         for (int t = 0; t < KQB; ++t) {
           if (t < kq) {
 #pragma unroll
-            for (int q = 0; q < RC; ++q)
+            for (int q = 0; q < RCI; ++q)
               acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(Wl[(t * RC + q) * 64 + woff], u[t], acc[q],
                                                             0, 0, 0);
           }
@@ -642,18 +652,18 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
           // written as a select, the full fp64 division ran for every stored value
           if (vhem) {
 #pragma unroll
-            for (int q = 0; q < RC; ++q)
+            for (int q = 0; q < RCI; ++q)
 #pragma unroll
               for (int v = 0; v < 4; ++v) {
-                const int row = q * 16 + kl + 4 * v;
+                const int row = (q0 + q) * 16 + kl + 4 * v;
                 if (row < KS) Ec[(size_t)row * ldE] = acc[q][v] / sm;
               }
           } else {
 #pragma unroll
-            for (int q = 0; q < RC; ++q)
+            for (int q = 0; q < RCI; ++q)
 #pragma unroll
               for (int v = 0; v < 4; ++v) {
-                const int row = q * 16 + kl + 4 * v;
+                const int row = (q0 + q) * 16 + kl + 4 * v;
                 if (row < KS) Ec[(size_t)row * ldE] = acc[q][v];
               }
           }
@@ -779,18 +789,19 @@ bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   return true;
 }
 
-template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false>
+template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false, int SPL = 1>
 static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st) {
   if (EXACT && a.kdp / 4 != KQB) return hipErrorInvalidValue;
   if (PF && (NTW != 1 || a.ksp / 16 != RC)) return hipErrorInvalidValue;
-  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF>;
+  if (SPL != 1 && !PF) return hipErrorInvalidValue;
+  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF, SPL>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
   const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), a.nwave * 64, lds);
   const long long c_begin = (long long)a.i_begin * a.SB, c_end = (long long)a.i_end * a.SB;
   const long long ntile = (c_end - a.u_col0 + 15) / 16 - (c_begin - a.u_col0) / 16;
-  const long long want = (ntile + (long long)a.nwave * NTW - 1) / ((long long)a.nwave * NTW);
+  const long long want = (ntile * SPL + (long long)a.nwave * NTW - 1) / ((long long)a.nwave * NTW);
   const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, (long long)cus * per_cu));
   EmissionArgs as = a;
   as.stagger_from = cus;
@@ -858,6 +869,16 @@ static hipError_t launch_raw_kq(const EmissionArgs &a, size_t lds, hipStream_t s
             : launch_emission_fn(&emission_raw_kernel<KQ, false, false>, a, lds, st);
 }
 
+// the one-chunk GEMM in half-tiles when the tiles fill fewer than 4 rounds of the
+// device's waves (the last, partial round then costs a smaller share); above that the
+// doubled U reads cost more than the finer tail saves.  VBHEM_EM_SPLIT=0 / 1 forces it.
+static bool use_row_split(const EmissionArgs &a) {
+  if (const char *ev = std::getenv("VBHEM_EM_SPLIT")) return std::atoi(ev) != 0;
+  const long long ntile = ((long long)(a.i_end - a.i_begin) * a.SB + 15) / 16;
+  const long long waves = (long long)device_cus() * 3 * a.nwave;  // 3 blocks per CU
+  return ntile < 4 * waves;
+}
+
 hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
   const int ncols = (a.i_end - a.i_begin) * a.SB;
   if (ncols <= 0) return hipSuccess;
@@ -865,7 +886,11 @@ hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
     // W' in one chunk (K S <= 128): the double-buffered variant
     const bool one = a.ksp / 16 == a.urc && !std::getenv("VBHEM_NO_UPF");
     if (a.ukqb == 4) return one ? launch_u_fn<4, 8, 1, false, true>(a, lds, st) : launch_u_fn<4, 8, 1>(a, lds, st);
-    if (a.ukqb == 12) return one ? launch_u_fn<12, 8, 1, false, true>(a, lds, st) : launch_u_fn<12, 8, 1>(a, lds, st);
+    if (a.ukqb == 12) {
+      if (one && use_row_split(a))  // small base counts (shards): half-tiles, a finer last round
+        return launch_u_fn<12, 8, 1, false, true, 2>(a, lds, st);
+      return one ? launch_u_fn<12, 8, 1, false, true>(a, lds, st) : launch_u_fn<12, 8, 1>(a, lds, st);
+    }
     // W' restaged per chunk: two column tiles per wave halve the staging per column
     if (a.kdp / 4 == 38) return launch_u_fn<38, 4, UNTW, true>(a, lds, st);  // d = 16 full (C5)
     return launch_u_fn<kUMaxKq, 4, UNTW>(a, lds, st);

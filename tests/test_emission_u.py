@@ -168,3 +168,26 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     assert np.isfinite(outs[0]).all()
     for st in outs[1:]:
         assert stat_err(st, outs[0]) < 1e-10, (name, prepare, stat_err(st, outs[0]))
+
+
+@pytest.mark.parametrize("N", [37, 2001, 12500])
+def test_row_split_bit_identical(vb, monkeypatch, N):
+    """The one-chunk GEMM in half-tiles (small base counts, e.g. a 12,500-base shard:
+    each wave takes 4 of a tile's 8 row tiles) computes every E entry with the same MFMA
+    chain as the whole-tile kernel: the fused E-step's outputs are bit-identical with the
+    split forced on and off (VBHEM_EM_SPLIT), at C4's shape."""
+    from vbhem_amd import host
+    from vbhem_amd.estep import EStepEngine
+    base, P, opt = vb.synth_workload("C4", N=N, device=DEV)
+    consts = host.cluster_constants(P, base.covmode)
+    outs = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("VBHEM_EM_SPLIT", split)
+        eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+        eng.set_clusters(consts)
+        eng.set_log_omega(host.log_omega_tilde(P.alpha))
+        tN = (100.0 * N) * eng.base.omega
+        outs.append((eng.fused(tN).clone(), eng.LL.clone(), eng.hatZ.clone()))
+        del eng
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
