@@ -598,8 +598,6 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
     __syncthreads();
   };
   if (nchunk == 1) stage(0);
-  if (p.stagger_sleeps > 0 && (int)blockIdx.x >= p.stagger_from)
-    for (int z = 0; z < p.stagger_sleeps; ++z) __builtin_amdgcn_s_sleep(127);
   if constexpr (PF) {  // NTW == 1, W' in one chunk (the launcher checks)
     {
       // W' resident for the whole kernel: the next round's tile of U is loaded while
@@ -803,12 +801,7 @@ static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st)
   const long long ntile = (c_end - a.u_col0 + 15) / 16 - (c_begin - a.u_col0) / 16;
   const long long want = (ntile * SPL + (long long)a.nwave * NTW - 1) / ((long long)a.nwave * NTW);
   const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, (long long)cus * per_cu));
-  EmissionArgs as = a;
-  as.stagger_from = cus;
-  as.stagger_sleeps = 0;
-  if (a.ksp / 16 > RC && per_cu == 2)  // chunked W', two blocks per CU (C5)
-    if (const char *ev = std::getenv("VBHEM_EM_STAGGER")) as.stagger_sleeps = std::atoi(ev);
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(a.nwave * 64), lds, st, as);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(a.nwave * 64), lds, st, a);
   return hipGetLastError();
 }
 

@@ -191,10 +191,6 @@ struct EmissionArgs {
   double *Atg;               // [K][S][S] A' = exp(logA - rowmax), or null
   int *zero_ints;            // fallback counters zeroed by block 0, or null
   int n_zero;
-  // emission_u_kernel with W' in several chunks and two blocks per CU: blocks from
-  // stagger_from on sleep stagger_sleeps x ~8k cycles first, so the two blocks of a CU
-  // stage their chunks out of phase (each one's MFMAs cover the other's staging)
-  int stagger_from, stagger_sleeps;
 };
 bool plan_emission(EmissionArgs &a, size_t &lds);
 // emission_u_kernel's plan: row chunking and LDS; false when the shape needs the
