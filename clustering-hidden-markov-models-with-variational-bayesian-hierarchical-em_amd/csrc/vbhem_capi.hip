@@ -626,7 +626,6 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
   if (c.split.ok) {
     vbhem::EmissionArgs ea = c.em;
     ea.i_begin = i_begin; ea.i_end = i_end; ea.i_buf0 = i_buf0; ea.E = Ebuf; ea.e_ld = e_ld;
-    ea.prep_jobs = ea.fold_prep && i_begin == 0;  // the side jobs once, before the first pass
     size_t em_lds = c.em_lds;
     hipEvent_t em0 = !k1 && timing_on(st) ? timing_event(st) : nullptr;
     if (c.use_u) {
@@ -984,14 +983,6 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     ctx.em.W = w.W; ctx.em.bias = w.bias; ctx.em.shift = w.shift;
     ctx.bwd2_prep = true;
     ctx.fpre = w.fpre;
-  } else if (gated && ctx.use_u && ctx.em.zfix && vbhem::emission_folds_prep(ctx.em)) {
-    // emission_prep_kernel's work inside emission_u_kernel (one-chunk W', C4): every block
-    // builds W' / bias' in LDS, the first group's block 0 zeroes the counters and writes A'
-    vbhem::EmissionArgs &e = ctx.em;
-    e.W = w.W; e.bias = w.bias; e.shift = w.shift;
-    e.zero_ints = w.fpre; e.n_zero = vbhem::kFlagPre + vbhem::kFlagHead;
-    e.Atg = w.Atg; e.logA = clus->logA;
-    e.fold_prep = 1;
   } else {
     rc = run_emission_prep(ctx, w.W, w.bias, w.shift, st, w.fpre, vbhem::kFlagPre + vbhem::kFlagHead,
                            gated ? w.Atg : nullptr, clus->logA);

@@ -597,71 +597,7 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  if constexpr (PF) {
-    if (p.fold_prep) {
-      // emission_prep_kernel's work for the whole (one-chunk) W' in this block: rows r =
-      // (j, s) of K S, k-rows e of kdp, written in the A-operand lane order of Wl; the
-      // arithmetic is the prep kernel's (em_* in vbhem_internal.h), so the bits are too
-      const int d = p.d, KSr = p.ksp, KD = p.KD;
-      const bool full = p.covmode == kCovFull;
-      const int NPF = full ? d * (d + 1) / 2 : d;
-      const double *zs = p.zfix;  // the prepared operand's shift
-      auto widx = [&](int e, int r) { return ((e >> 2) * RC + (r >> 4)) * 64 + (e & 3) * 16 + (r & 15); };
-      for (int r = tid; r < KSr; r += NT) {  // per row: the P m' entries and bias'
-        double q = 0.0;
-        if (r < KS) {
-          const double *mr = p.m + (size_t)r * d;
-          if (full) {
-            const double *P = p.P + (size_t)r * d * d;
-            for (int a = 0; a < d; ++a) {
-              const double v = em_pm_full(P, mr, zs, a, d);
-              Wl[widx(NPF + a, r)] = v;
-              q = fma(mr[a] - zs[a], v, q);
-            }
-          } else {
-            const double *P = p.P + (size_t)r * d;
-            for (int a = 0; a < d; ++a) {
-              const double ma = mr[a] - zs[a];
-              Wl[widx(a, r)] = -0.5 * P[a];
-              Wl[widx(d + a, r)] = P[a] * ma;
-              q = fma(P[a] * ma, ma, q);
-            }
-          }
-          bl[r] = em_bias(d, p.c[r], q);
-        } else {
-          bl[r] = 0.0;
-        }
-      }
-      // the packed second-moment entries (full), and zeros past K S rows / KD k-rows
-      for (int x = tid; x < kq * 4 * KSr; x += NT) {
-        const int e = x / KSr, r = x - e * KSr;
-        if (r >= KS || e >= KD) {
-          Wl[widx(e, r)] = 0.0;
-        } else if (full && e < NPF) {
-          int a, b;
-          packed_ab(e, d, a, b);
-          Wl[widx(e, r)] = em_w_full(p.P + (size_t)r * d * d, a, b, d);
-        }
-      }
-      if (p.prep_jobs && blockIdx.x == 0) {  // the prep kernel's side jobs
-        for (int x = tid; x < p.n_zero; x += NT) p.zero_ints[x] = 0;
-        if (p.Atg)
-          for (int x = tid; x < KS * p.S; x += NT) {
-            const int r = x / p.S, k = x - r * p.S;
-            const double *la = p.logA + (size_t)r * p.S;
-            double mx = la[0];
-            for (int s2 = 1; s2 < p.S; ++s2) mx = fmax(mx, la[s2]);
-            p.Atg[x] = exp_nonpos(la[k] - mx);
-          }
-        for (int a = tid; a < d; a += NT) p.shift[a] = zs[a];
-      }
-      __syncthreads();
-    } else {
-      stage(0);
-    }
-  } else if (nchunk == 1) {
-    stage(0);
-  }
+  if (nchunk == 1) stage(0);
   if constexpr (PF) {  // NTW == 1, W' in one chunk (the launcher checks)
     {
       // W' resident for the whole kernel: the next round's tile of U is loaded while
@@ -924,12 +860,6 @@ static hipError_t launch_raw_kq(const EmissionArgs &a, size_t lds, hipStream_t s
                         : launch_emission_fn(&emission_raw_kernel<KQ, true, false>, a, lds, st);
   return sm ? launch_emission_fn(&emission_raw_kernel<KQ, false, true>, a, lds, st)
             : launch_emission_fn(&emission_raw_kernel<KQ, false, false>, a, lds, st);
-}
-
-// the launch takes the one-chunk path, so it can build W' / bias' itself (fold_prep)
-bool emission_folds_prep(const EmissionArgs &a) {
-  return a.urc && a.ksp / 16 == a.urc && (a.ukqb == 4 || a.ukqb == 12) && !std::getenv("VBHEM_NO_UPF") &&
-         !std::getenv("VBHEM_NO_EMPREP_FOLD");
 }
 
 // the one-chunk GEMM in half-tiles when the tiles fill fewer than 4 rounds of the

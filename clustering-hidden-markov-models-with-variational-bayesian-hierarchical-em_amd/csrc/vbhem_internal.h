@@ -191,16 +191,8 @@ struct EmissionArgs {
   double *Atg;               // [K][S][S] A' = exp(logA - rowmax), or null
   int *zero_ints;            // fallback counters zeroed by block 0, or null
   int n_zero;
-  // emission_u_kernel's one-chunk path (W' whole in LDS): every block builds W' / bias'
-  // in LDS from the cluster constants itself (no emission_prep_kernel launch, nothing
-  // staged from W / bias); prep_jobs: block 0 also does the prep kernel's side jobs
-  // (zero_ints, Atg, shift) -- the first base group's launch only
-  int fold_prep, prep_jobs;
 };
 bool plan_emission(EmissionArgs &a, size_t &lds);
-// emission_u_kernel will take its one-chunk path for a (prepared operand): it can do
-// emission_prep_kernel's work itself (EmissionArgs::fold_prep)
-bool emission_folds_prep(const EmissionArgs &a);
 // emission_u_kernel's plan: row chunking and LDS; false when the shape needs the
 // raw / generic kernels (k-steps > kUMaxKq).  launch_emission takes it when a.U is set.
 bool plan_emission_u(EmissionArgs &a, size_t &lds);
