@@ -578,6 +578,13 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
   const size_t ldE = (size_t)p.e_ld;
   const double sm = p.smooth;
   const bool vhem = __builtin_amdgcn_readfirstlane((int)(sm != 1.0)) != 0;
+  // E entry of row ub + kl at the lane's byte offset bofs (< 4 GB within a base group):
+  // a wave-uniform row base plus a 32-bit lane offset (chunked path: fewer VALU address
+  // operations per store than a 64-bit row x stride product)
+  auto e_at = [&](int ub, unsigned bofs) -> double & {
+    const char *rb = reinterpret_cast<const char *>(p.E) + (size_t)ub * ldE * sizeof(double);
+    return *reinterpret_cast<double *>(const_cast<char *>(rb) + bofs);
+  };
   typedef __attribute__((address_space(3))) void *lds_ptr;
   typedef __attribute__((address_space(1))) void *glb_ptr;
   auto stage = [&](int ch) {
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
   for (long long r = 0; r < rounds; ++r) {
     // NTW column tiles per wave: each staged W' chunk feeds NTW * RC MFMAs per k-step
     double u[NTW][KQB];
-    double *Ec[NTW];
+    unsigned lofs[NTW];  // 32-bit lane byte offsets of the stores (e_at)
     bool cv[NTW];
 #pragma unroll
     for (int n = 0; n < NTW; ++n) {
@@ -688,7 +695,7 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
       }
       const long long col = p.u_col0 + tile * 16 + cl;
       cv[n] = tv && col >= c_begin && col < c_end;
-      Ec[n] = p.E + (cv[n] ? col - (long long)p.i_buf0 * SB : 0);
+      lofs[n] = ((unsigned)(cv[n] ? col - (long long)p.i_buf0 * SB : 0) + (unsigned)kl * (unsigned)ldE) * 8u;
     }
     for (int ch = 0; ch < nchunk; ++ch) {
       if (nchunk > 1) stage(ch);
@@ -721,16 +728,16 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
           for (int q = 0; q < RC; ++q)
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              const int row = (ch * RC + q) * 16 + kl + 4 * v;
-              if (row < KS) Ec[n][(size_t)row * ldE] = acc[n][q][v] / sm;
+              const int ub = (ch * RC + q) * 16 + 4 * v;
+              if (ub + kl < KS) e_at(ub, lofs[n]) = acc[n][q][v] / sm;
             }
         } else {
 #pragma unroll
           for (int q = 0; q < RC; ++q)
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              const int row = (ch * RC + q) * 16 + kl + 4 * v;
-              if (row < KS) Ec[n][(size_t)row * ldE] = acc[n][q][v];
+              const int ub = (ch * RC + q) * 16 + 4 * v;
+              if (ub + kl < KS) e_at(ub, lofs[n]) = acc[n][q][v];
             }
         }
       }
