@@ -337,7 +337,7 @@ def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
 def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch, S):
     """The adversarial cluster at S = Sb = 8 (12), T = 10: its pairs underflow in the
     MFMA backward pass (fb_bwd4_kernel / fb_bwd12_kernel) and, being gated, again in
-    the gate-list pass (fb_list4_kernel / fb_split_kernel); both passes' flags reach
+    the gate-list pass (fb_list4_kernel / fb_list12_kernel); both passes' flags reach
     the exact fallback (folded into the consumers, or two fb_exact_kernel launches)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
