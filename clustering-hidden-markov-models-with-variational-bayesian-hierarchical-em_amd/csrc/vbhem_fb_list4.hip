@@ -37,11 +37,6 @@
 #ifndef VBHEM_LIST4_R4
 #define VBHEM_LIST4_R4 0
 #endif
-// VBHEM_LIST4_DIRECTG: the forward's g in the sigma-first layout from two more MFMA
-// products instead of a transpose of g^T (A/B switch)
-#ifndef VBHEM_LIST4_DIRECTG
-#define VBHEM_LIST4_DIRECTG 0
-#endif
 
 namespace vbhem {
 
@@ -339,26 +334,7 @@ void fb_list4_kernel(const SplitArgs p) {
 #pragma unroll
         for (int i3 = 0; i3 < 2; ++i3) H[i2][i3] = mfma4(gT[1][i2], Gt[1][i3], mfma4(gT[0][i2], Gt[0][i3], H[i2][i3]));
       double g[2][2];
-#if VBHEM_LIST4_DIRECTG
-      {
-        // g = f / Z in the sigma-first layout straight from the matrix cores (f = nu Ab,
-        // Z = A' G), instead of the per-pair transpose of g^T: 16 more MFMAs, no LDS-crossbar
-        // round trip on the step's dependency chain
-        double zf[4], rz[4], ff[4];
-#pragma unroll
-        for (int i2 = 0; i2 < 2; ++i2)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            ff[2 * i2 + jj] = mfma4(nuT[1][i2], AbF[1][jj], mfma4(nuT[0][i2], AbF[0][jj], 0.0));
-            zf[2 * i2 + jj] = mfma4(AT[1][i2], lat[t][1][jj], mfma4(AT[0][i2], lat[t][0][jj], 0.0));
-          }
-        rcp_pos_n<4>(rz, zf);
-#pragma unroll
-        for (int x = 0; x < 4; ++x) g[x / 2][x % 2] = ff[x] * rz[x];
-      }
-#else
       transpose8(gT, g, taddr);
-#endif
       // Qm^T block (J, I') = sum_I g(I, J)^T A'(I, I'); nu^T = G^T o Qm^T
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
