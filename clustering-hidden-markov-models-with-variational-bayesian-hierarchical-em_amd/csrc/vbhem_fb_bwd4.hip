@@ -82,15 +82,6 @@
 #ifndef VBHEM_BWD4_SB
 #define VBHEM_BWD4_SB 0
 #endif
-//   VBHEM_BWD4_EXPH     the exp table as pairs {t, t/2} (one fp64 operation less per exp:
-//                       m = t + r (t + (t/2) r)) and the log table at 4096 intervals
-//                       (64 KB, so both fit: 112 KB with the termination's exp table)
-#ifndef VBHEM_BWD4_EXPH
-#define VBHEM_BWD4_EXPH 0
-#endif
-#if VBHEM_BWD4_EXPH && !(VBHEM_BWD4_BIGLOG && VBHEM_BWD4_DECOUPLE && !VBHEM_BWD4_SKEW)
-#error "VBHEM_BWD4_EXPH needs BIGLOG and DECOUPLE"
-#endif
 //   VBHEM_BWD4_PRIO     static priority 1 for the second half of the block's waves
 //                       (MI355X_MICROARCH.md, two waves per SIMD, item 4) (A/B)
 #ifndef VBHEM_BWD4_PRIO
@@ -126,14 +117,7 @@ using namespace m4;
 __global__ __launch_bounds__(64 * kNWB) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void fb_bwd4_kernel(const SplitArgs p) {
   constexpr int S = 8;
-#if VBHEM_BWD4_EXPH
-  // the hot tables first (their LDS offsets fit ds_read's 16-bit offset field), the
-  // termination's exp table last
-  __shared__ __attribute__((aligned(16))) double tabs[2 * 2048 + 2 * 4096 + 2048];
-  double *const etab2 = tabs;                // {2^(i/2048 - 1010), half of it}
-  double *const ltab4 = tabs + 2 * 2048;     // {1/c, -log(1/c)}, 4096 intervals
-  double *const etab = tabs + 2 * 2048 + 2 * 4096;  // 2^(i/2048 - 1010)
-#elif VBHEM_BWD4_BIGLOG
+#if VBHEM_BWD4_BIGLOG
   // one array, the exp table first: both tables' LDS offsets then fit the 16-bit
   // offset field of ds_read (no address add per lookup)
   __shared__ __attribute__((aligned(16))) double tabs[2048 + 2 * 8192];
@@ -145,15 +129,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #endif
   __shared__ double amax[S], lpi[S];
   const int tid = threadIdx.x;
-#if VBHEM_BWD4_EXPH
-  for (int x = tid; x < 2048; x += 64 * kNWB) {
-    const double t = kExpTab4[x] * 0x1p-1010;
-    etab[x] = t;
-    etab2[2 * x] = t;
-    etab2[2 * x + 1] = 0.5 * t;
-  }
-  stage_log4k(ltab4, tid, 64 * kNWB);
-#elif VBHEM_BWD4_BIGLOG
+#if VBHEM_BWD4_BIGLOG
   for (int x = tid; x < 2048; x += 64 * kNWB) etab[x] = kExpTab4[x] * 0x1p-1010;
   stage_log8k(ltab8, tid, 64 * kNWB);
 #else
@@ -325,11 +301,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       double G[kQPW][2][2];
 #if VBHEM_BWD4_DECOUPLE
       // table values first (they do not need the maxima), then the maxima chain
-#if VBHEM_BWD4_EXPH
-      double2 tv[NE];
-#else
       double tv[NE];
-#endif
       unsigned wph[kQPW][2];
 #pragma unroll
       for (int q = 0; q < kQPW; ++q)
@@ -337,14 +309,9 @@ void fb_bwd4_kernel(const SplitArgs p) {
         for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) s[q][i2][jj] = red_s(V[q][i2][jj]);
-#if VBHEM_BWD4_EXPH
-#pragma unroll
-      for (int x = 0; x < NE; ++x) tv[x] = etab2_at(etab2, s[x / 4][(x / 2) % 2][x % 2]);
-#else
 #pragma unroll
       for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, s[x / 4][(x / 2) % 2][x % 2]);
-#endif
-#if defined(VBHEM_ABL_NOETAB) && !VBHEM_BWD4_EXPH  // ablation (timing only, wrong results)
+#ifdef VBHEM_ABL_NOETAB  // ablation (timing only, wrong results): no exp table read
 #pragma unroll
       for (int x = 0; x < NE; ++x) tv[x] = 1.0;
 #endif
@@ -371,11 +338,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
           sf[x] = s[x / 4][(x / 2) % 2][x % 2];
           wpf[x] = wph[x / 4][x % 2];
         }
-#if VBHEM_BWD4_EXPH
-        exp_dh_n<NE>(gg, vv, sf, tv, wpf);
-#else
         exp_d_n<NE>(gg, vv, sf, tv, wpf);
-#endif
 #pragma unroll
         for (int x = 0; x < NE; ++x) G[x / 4][(x / 2) % 2][x % 2] = gg[x];
       }
@@ -437,9 +400,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
             zmin[q] = min(zmin[q], min(min(__double2hiint(zf[4 * q]), __double2hiint(zf[4 * q + 1])),
                                        min(__double2hiint(zf[4 * q + 2]), __double2hiint(zf[4 * q + 3]))));
         }
-#if VBHEM_BWD4_EXPH
-        log_q4_n<NE, true>(yf, zf, wqf, ltab4);
-#elif VBHEM_BWD4_BIGLOG
+#if VBHEM_BWD4_BIGLOG
         log_q_n<NE, VBHEM_BWD4_DECOUPLE != 0>(yf, zf, wqf, ltab8);
 #elif VBHEM_BWD4_DECOUPLE
         log_d_n<NE>(yf, zf, wqf, ltab);
@@ -497,9 +458,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       {
         const double zsf[1] = {zs};
         const int wqf[1] = {(int)(w + kWq0)};
-#if VBHEM_BWD4_EXPH
-        log_q4_n<1, false>(lse1, zsf, wqf, ltab4);
-#elif VBHEM_BWD4_BIGLOG
+#if VBHEM_BWD4_BIGLOG
         log_q_n<1, false>(lse1, zsf, wqf, ltab8);
 #else
         log_m_n<1>(lse1, zsf, wqf, ltab);

@@ -261,61 +261,6 @@ __device__ __forceinline__ void exp_d_n(double (&g)[N], const double (&v)[N], co
     g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
   }
 }
-// the 4096-interval log table {1/c, -log(1/c)} (64 KB), for kernels that also keep the
-// exp table as pairs {t, t/2} (exp_dh_n): log1p(r) = r - r^2/2 with |r| <= 2^-13 (the
-// dropped r^3/3 <= 6.1e-13 absolute, the size of the exp's dropped r^3/6 relative term)
-__device__ __forceinline__ void stage_log4k(double *ltab, int tid, int nt) {
-  for (int k = tid; k < 4096; k += nt) {
-    const double c = 1.0 + ((double)k + 0.5) * (1.0 / 4096.0);
-    const double ic = 1.0 / c;
-    ltab[2 * k] = ic;
-    ltab[2 * k + 1] = -log(ic);
-  }
-}
-template <int N, bool DEC>
-__device__ __forceinline__ void log_q4_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
-                                         const double *ltab) {
-  double zz[N], ic[N], w[N];
-  unsigned one_hi = 0x3ff00000u;
-  asm("" : "+v"(one_hi));
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const unsigned hi = (unsigned)__double2hiint(z[x]);
-    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
-    unsigned ex = hi >> 20;
-    asm("" : "+v"(ex));
-    const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
-    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
-    const double2 e = *reinterpret_cast<const double2 *>(
-        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 4) & 0xfff0u), 16));
-    ic[x] = e.x;
-    w[x] = fma((double)kk, DEC ? 0x1.62e42fefa39efp-1 : kLn2N, e.y);
-  }
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const double r = fma(zz[x], ic[x], -1.0);
-    const double h = fma(r, -0.5, 1.0);
-    y[x] = fma(r, h, w[x]);
-  }
-}
-// exp_d_n with the table as pairs {t, t/2} (2^(i/2048 - 1010) and its half): exp(r) t =
-// t + r (t + (t/2) r), two fmas where exp_d_n takes a multiply and two fmas
-template <int N>
-__device__ __forceinline__ void exp_dh_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
-                                         const double2 (&t)[N], const unsigned (&wph)[N]) {
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
-    const double m = fma(r, fma(t[x].y, r, t[x].x), t[x].x);
-    unsigned e = __builtin_elementwise_sub_sat(lo_u(s[x]) >> 11, wph[x]);
-    asm("" : "+v"(e));
-    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
-  }
-}
-__device__ __forceinline__ double2 etab2_at(const double *etab2, double s) {
-  return *reinterpret_cast<const double2 *>(
-      __builtin_assume_aligned(reinterpret_cast<const char *>(etab2) + ((lo_u(s) << 4) & 0x7ff0u), 16));
-}
 __device__ __forceinline__ double etab_at(const double *etab, double s) {
   return *reinterpret_cast<const double *>(
       __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & 0x3ff8u), 8));
