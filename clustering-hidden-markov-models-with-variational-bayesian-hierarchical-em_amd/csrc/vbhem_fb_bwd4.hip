@@ -191,11 +191,6 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #if VBHEM_BWD4_PRIO
   if (wave >= kNWB / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-#ifdef VBHEM_BWD4_STAGGER
-  // A/B: half of each SIMD's waves start their tile loop VBHEM_BWD4_STAGGER x 64 cycles
-  // late, so the co-resident waves' step phases (LDS waits, MFMA runs) do not coincide
-  if ((wave >> 2) & 1) __builtin_amdgcn_s_sleep(VBHEM_BWD4_STAGGER);
-#endif
   // the tile loop, versioned on the underflow test (ZS: the cluster's A' makes it
   // unnecessary, VBHEM_BWD4_ZSAFE)
   auto tiles = [&](auto zs_tag) {
