@@ -105,18 +105,15 @@ void fb_list12_kernel(const SplitArgs p) {
     // the cluster's constants, per item (cache hits): A'^T as the B operand of Z^T
     // (block (K, I'): A'[4I' + c][4K + r]), A' in P (A'[4I + r][4I' + c]), amax (rows
     // 4I + c), lpi (rows 4I + r)
-    double AT[NB][NB], Ap[NB][NB], amQ[NB], lpP[NB];
+    double AT[NB][NB], amQ[NB], lpP[NB];
     bool cl_nf;
+    const double *At = p.Atg + (size_t)j * S * S;
     {
-      const double *At = p.Atg + (size_t)j * S * S;
       bool nf = false;
 #pragma unroll
       for (int x = 0; x < NB; ++x)
 #pragma unroll
-        for (int y = 0; y < NB; ++y) {
-          AT[x][y] = At[(4 * y + c) * S + 4 * x + r];
-          Ap[x][y] = At[(4 * x + r) * S + 4 * y + c];
-        }
+        for (int y = 0; y < NB; ++y) AT[x][y] = At[(4 * y + c) * S + 4 * x + r];
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2) {
         const double *la = p.logA + ((size_t)j * S + 4 * i2 + c) * S;
@@ -322,6 +319,12 @@ void fb_list12_kernel(const SplitArgs p) {
         const double a = p.A[((size_t)i * SB + (bp < SB ? bp : SB - 1)) * SB + (be < SB ? be : SB - 1)];
         AbF[j2][jj] = (be < SB && bp < SB) ? a : 0.0;
       }
+    // A' in P (A'[4I + r][4I' + c]), loaded only now: not live across the backward sweep
+    double Ap[NB][NB];
+#pragma unroll
+    for (int x = 0; x < NB; ++x)
+#pragma unroll
+      for (int y = 0; y < NB; ++y) Ap[x][y] = At[(4 * x + r) * S + 4 * y + c];
     double nuT[NB][NB], tnT[NB][NB], H[NB][NB];
     transpose12(nu, nuT, taddr);
 #pragma unroll
