@@ -533,7 +533,8 @@ __global__ __launch_bounds__(kUThreads) void us_build_kernel(UPrepArgs p, double
   const long long n = (long long)p.N * SBP * NUP;
   for (long long x = (long long)blockIdx.x * kUThreads + tid; x < n; x += (long long)gridDim.x * kUThreads) {
     const long long i = x / (SBP * NUP);
-    const int r = (int)(x - i * (SBP * NUP)), b = r / NUP, f = r - b * NUP;
+    const int r = (int)(x - i * (SBP * NUP)), ft = r / (SBP * 16), q = r - ft * SBP * 16;
+    const int b = q >> 4, f = 16 * ft + (q & 15);
     double u = 0.0;
     if (b < SB && f < NU) {
       const long long col = i * SB + b;

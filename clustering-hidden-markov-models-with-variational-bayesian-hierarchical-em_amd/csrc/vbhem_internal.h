@@ -220,12 +220,15 @@ struct UPrepArgs {
 };
 hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st);
 // The statistics copy of the base-set operand (vbhem_prepare_base, right after U in
-// the same buffer): per base i an [SBP][NUP] block (SBP = SB rounded up to 4, NUP =
-// NU rounded up to 16) of the statistic features f of every base state b:
+// the same buffer): per base i an [NUP / 16][SBP][16] block (SBP = SB rounded up to 4,
+// NUP = NU rounded up to 16; feature tile, base state, feature within the tile) of the
+// statistic features f of every base state b:
 // 1 | mu'_a (d) | packed Sigma + mu' mu'^T (as U, off-diagonals Sigma_ab + Sigma_ba +
 // 2 mu'_a mu'_b), mu' = mu - z, zero past SB and NU.  stats_list_m_kernel's MFMA B
-// operand: 16 features of one state are one 128-byte segment, a base's block is
-// contiguous (the tile order of U splits it over two 16-column tiles' half lines).
+// operand: a 16-feature tile of four consecutive states is one contiguous 512-byte
+// segment (one load per k-slice; with [SBP][NUP] rows it was four 128-byte segments
+// in four rows), a base's block is contiguous (the tile order of U splits it over two
+// 16-column tiles' half lines).
 __host__ __device__ inline int us_sbp(int SB) { return (SB + 3) / 4 * 4; }
 __host__ __device__ inline int us_nup(int NU) { return (NU + 15) / 16 * 16; }
 __host__ __device__ inline int us_nu(int d, int covmode) { return 1 + d + (covmode == kCovFull ? d * (d + 1) / 2 : d); }

@@ -1163,9 +1163,10 @@ __global__ __launch_bounds__(64 * kSuWaves) void stats_list_u_kernel(const Stats
 //               (Z tnu)(s, b) * Us(i, b, f)
 // i.e. one (16 x 4) x (4 x 16) v_mfma_f64_16x16x4f64 per k-slice of four base states
 // and 16-feature tile: A = Z tnu (lane: state s = lane & 15, base state 4 kk + lane / 16;
-// zero past S / SB), B = 16 consecutive features of one base state's row of Us (one
-// 128-byte segment per lane quarter).  Block (c, j) = part c of cluster j's list, as
-// stats_list_u_kernel.  Its 4 waves are G pair groups x 4 / G tile groups: wave w takes
+// zero past S / SB; KSM = SBP / 4 k-slices), B = 16 consecutive features of four base
+// states (one contiguous 512-byte segment of Us's tile-major block per load).  Block
+// (c, j) = part c of cluster j's list, as stats_list_u_kernel.  Its 4 waves are G pair
+// groups x 4 / G tile groups: wave w takes
 // the part's pairs w % G, + G, ... and the feature tiles w / G + (4 / G) t, t < NTW,
 // plus the sum_nu_1 | sum_xi entries lane + 64 (w / G + (4 / G) r).  The next PD - 1
 // pairs' operands are in flight while a pair's MFMAs run (a register ring; the kernel is
@@ -1181,10 +1182,12 @@ template <int NTW, int G, int KSM, int NXR, int PD>
 __global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const StatsArgs p) {
   extern __shared__ double lds[];
   constexpr int TG = kSmWaves / G;  // tile groups; NXR: sum_nu_1 | sum_xi chunks of 64 per wave
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index in an SGPR: the tile / pair-group tests below are scalar branches and
+  // the loads' tile offsets scalar adds to the pair's base
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pg = wave % G, tg = wave / G;
   const int K = p.K, S = p.S, SB = p.SB, d = p.d, NU = p.NU;
-  const int SBP = us_sbp(SB), NUP = us_nup(NU), ntile = NUP / 16, KSL = SBP / 4;
+  const int SBP = us_sbp(SB), NUP = us_nup(NU), ntile = NUP / 16;  // SBP = 4 KSM (launch)
   const int OT = S * SB, NX = S + S * S;
   // block -> (cluster j, part c of its list, parts nch): the gated pairs of all clusters
   // in parts of about P = total / (blocks - K) pairs, at most p.nzero (the slab count)
@@ -1247,69 +1250,73 @@ __global__ __launch_bounds__(64 * kSmWaves) void stats_list_m_kernel(const Stats
   struct Ops {
     double ta[KSM], ub[NTW][KSM], xv[NXR], z;
   };
+  bool ta_ok[KSM];  // this lane's A entry (state cl, base state 4 kk + kl) exists
+#pragma unroll
+  for (int kk = 0; kk < KSM; ++kk) ta_ok[kk] = cl < S && 4 * kk + kl < SB;
   Ops buf[PD];
   auto load = [&](int i, Ops &o) {
     // wave-uniform bases (SGPRs), 32-bit lane offsets: saddr loads, no 64-bit address
     // arithmetic per lane
     const size_t lp = (size_t)(i - p.i_buf0) * K + j;
-    o.z = p.Z[lp];
+    // Z by a vector load (an address in VGPRs), in order with the pair's other loads: a
+    // scalar load would be waited for (lgkmcnt(0)) at the start of the next pair
+    unsigned zo = (unsigned)lp;  // (a 32-bit offset: the laundered pointer would be flat)
+    asm("" : "+v"(zo));
+    o.z = p.Z[zo];
     const double *us = p.Us + (size_t)i * SBP * NUP;
     const double *tp = p.tnu + lp * OT, *n1p = p.nu1 + lp * S, *xp = p.xi + lp * S * S;
-    // lane-varying bounds by clamped (always valid) loads and a select, not branches
+    // lane-varying bounds by clamped (always valid) loads, not branches; the select that
+    // zeroes the clamped lanes waits for compute (a select here would wait for the load,
+    // and with it for every load issued before it: no prefetch at all)
 #pragma unroll
     for (int kk = 0; kk < KSM; ++kk) {
-      if (kk < KSL) {  // wave-uniform
-        const int b = 4 * kk + kl;
-        const bool ok = cl < S && b < SB;
-        const double v = tp[ok ? (unsigned)(cl * SB + b) : 0u];
-        o.ta[kk] = ok ? v : 0.0;
+      const int b = 4 * kk + kl;
+      o.ta[kk] = tp[ta_ok[kk] ? (unsigned)(cl * SB + b) : 0u];
 #pragma unroll
-        for (int t = 0; t < NTW; ++t) {
-          const int ft = tg + TG * t;
-          if (ft < ntile) o.ub[t][kk] = us[(unsigned)(b * NUP + 16 * ft + cl)];  // b < SBP: in the block
-        }
+      for (int t = 0; t < NTW; ++t) {
+        const int ft = min(tg + TG * t, ntile - 1);  // past ntile: a repeat, never used
+        o.ub[t][kk] = us[(unsigned)((ft * SBP + b) * 16 + cl)];  // b < SBP: in the block
       }
     }
+    // one load from a lane-selected address (lanes past NX read xi[0]: their sums are
+    // never stored)
 #pragma unroll
     for (int r = 0; r < NXR; ++r) {
       const int x = lane + 64 * (tg + TG * r);
-      const double v1 = n1p[x < S ? (unsigned)x : 0u];
-      const double v2 = xp[x >= S && x < NX ? (unsigned)(x - S) : 0u];
-      o.xv[r] = x < S ? v1 : x < NX ? v2 : 0.0;
+      o.xv[r] = *(x < S ? n1p + x : xp + (x < NX ? x - S : 0));
     }
   };
   auto compute = [&](const Ops &o) {
 #pragma unroll
     for (int kk = 0; kk < KSM; ++kk) {
-      if (kk < KSL) {
-        const double av = o.z * o.ta[kk];
+      const double av = o.z * (ta_ok[kk] ? o.ta[kk] : 0.0);
 #pragma unroll
-        for (int t = 0; t < NTW; ++t)
-          if (tg + TG * t < ntile) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, o.ub[t][kk], acc[t], 0, 0, 0);
-      }
+      for (int t = 0; t < NTW; ++t)
+        if (tg + TG * t < ntile) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, o.ub[t][kk], acc[t], 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < NXR; ++r) ax[r] = fma(o.z, o.xv[r], ax[r]);
   };
-  // this wave's pairs: n0 + pg + G k, k < cnt; their bases fetched 64 at a time, one
-  // per lane, for the load cursor
+  // this wave's pairs: n0 + pg + G k, k < cnt.  The loop body is branch-free around the
+  // loads (every slot loaded, the cursor clamped to the last pair; the list entries by
+  // scalar loads one pair ahead), so the compiler's wait before a pair's MFMAs counts
+  // exactly the PD - 1 later pairs' loads instead of draining them at a join.
   const int nf = n0 + pg;
   const int cnt = nf < n1 ? (n1 - nf + G - 1) / G : 0;
-  int il = 0;
-  auto base_of = [&](int k) -> int {  // k: the load cursor (ascending)
-    if ((k & 63) == 0) il = k + lane < cnt ? lst[nf + G * (k + lane)] : 0;
-    return __builtin_amdgcn_readlane(il, k & 63);
-  };
+  if (cnt > 0) {  // wave-uniform
+    const int kmax = cnt - 1;
+    const int *lw = lst + nf;
 #pragma unroll
-  for (int u = 0; u < PD - 1; ++u)
-    if (u < cnt) load(base_of(u), buf[u]);
-  for (int k0 = 0; k0 < cnt; k0 += PD) {
+    for (int u = 0; u < PD - 1; ++u) load(lw[G * min(u, kmax)], buf[u]);
+    int inext = lw[G * min(PD - 1, kmax)];
+    for (int k0 = 0; k0 < cnt; k0 += PD) {
 #pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      const int k = k0 + u;
-      if (k < cnt) {  // wave-uniform
-        if (k + PD - 1 < cnt) load(base_of(k + PD - 1), buf[(u + PD - 1) % PD]);
-        compute(buf[u]);
+      for (int u = 0; u < PD; ++u) {
+        const int k = k0 + u;
+        const int il = inext;
+        inext = lw[G * min(k + PD, kmax)];
+        load(il, buf[(u + PD - 1) % PD]);  // pair min(k + PD - 1, cnt - 1)
+        if (k < cnt) compute(buf[u]);      // wave-uniform
       }
     }
   }
@@ -1534,18 +1541,12 @@ static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t
   return hipGetLastError();
 }
 
-#ifndef VBHEM_SM_PDD
-#define VBHEM_SM_PDD 2   // the ring depth (build switch for A/B)
-#endif
 // ring depth 2 (C4: 0.177 ms of statistics per step against 0.191 with depth 4 and
-// its 768 resident blocks); VBHEM_SM_PD=3 (A/B) for the one-pair-group variant
+// its 768 resident blocks; C5: depth 3 drops the residency from 3 to 2 blocks per CU,
+// 7.7 vs 5.8 ms of statistics per step)
 template <int NTW, int G, int KSM, int NXR>
 static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
-  if (G == 1) {
-    if (const char *ev = std::getenv("VBHEM_SM_PD"))
-      if (std::atoi(ev) == 3) return launch_sm_pd<NTW, G, KSM, NXR, 3>(a, grid, st);
-  }
-  return launch_sm_pd<NTW, G, KSM, NXR, VBHEM_SM_PDD>(a, grid, st);
+  return launch_sm_pd<NTW, G, KSM, NXR, 2>(a, grid, st);
 }
 
 // the sum_nu_1 | sum_xi chunks per wave: ceil(ceil((S + S^2) / 64) / tile groups)
@@ -1561,14 +1562,10 @@ static hipError_t launch_sm_x(const StatsArgs &a, const dim3 &grid, hipStream_t 
 
 // stats_list_m_kernel's variant: 4 pair groups (every wave all feature tiles) up to 4
 // tiles (NU <= 64), 2 groups up to 8 tiles, else one group of 4 tile groups
+// (C4: 1 or 2 pair groups measured 0.41 / 0.25 ms of statistics per step against 0.21)
 template <int KSM>
 static hipError_t launch_sm_k(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
   const int nt = us_nup(a.NU) / 16;
-  if (const char *eg = std::getenv("VBHEM_SM_G")) {  // A/B: fewer pair groups up to 4 tiles
-    const int g = std::atoi(eg);
-    if (nt <= 4 && g == 1) return launch_sm_x<1, 1, KSM>(a, grid, st);
-    if (nt <= 4 && g == 2) return launch_sm_x<2, 2, KSM>(a, grid, st);
-  }
   switch (nt) {
     case 1: return launch_sm_x<1, 4, KSM>(a, grid, st);
     case 2: return launch_sm_x<2, 4, KSM>(a, grid, st);
@@ -1660,7 +1657,12 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
     if (a.nzero_m > 0) b.nzero = std::min(a.nzero_m, nchunk);
     if (stats_slabs) *stats_slabs = b.nzero;
     const dim3 g1((unsigned)std::min<long long>((long long)nchunk * a.K, 1ll << 30));
-    return us_sbp(a.SB) <= 8 ? launch_sm_k<2>(b, g1, st) : launch_sm_k<4>(b, g1, st);
+    switch (us_sbp(a.SB) / 4) {  // the k-slices of four base states, exact
+      case 1: return launch_sm_k<1>(b, g1, st);
+      case 2: return launch_sm_k<2>(b, g1, st);
+      case 3: return launch_sm_k<3>(b, g1, st);
+      default: return launch_sm_k<4>(b, g1, st);
+    }
   }
   // on the prepared operand's tile layout when the call has one (S <= 16: the split
   // kernel's range) (NU > 64, e.g. d = 16 full at C5: the covariance gather of
