@@ -19,7 +19,8 @@
 // reduction.  The exp / log are fb_bwd4_kernel's round-4 ones: maxima
 // rounded to a multiple of ln 2 (the exp table index independent of the maximum), the
 // 8192-interval log table with a second-order log1p; the tables take 144 KB of LDS,
-// one block per CU.  Underflow / range / non-finite handling as fb_bwd4_kernel: a pair
+// one block per CU, two waves per SIMD, each with its next tile's inputs in flight
+// (as fb_bwd4_kernel).  Underflow / range / non-finite handling as fb_bwd4_kernel: a pair
 // whose inputs could leave the integer range of the maxima, or whose Z underflowed,
 // is flagged to the exact fallback; the per-step underflow test runs only for a
 // cluster with an A' entry below 2^-600.
@@ -34,7 +35,11 @@
 #include "vbhem_mfma4.h"
 
 #ifndef VBHEM_BWD12_WAVES
-#define VBHEM_BWD12_WAVES 3   // waves per SIMD (the register budget)
+// waves per SIMD (the register budget): 2, with the next tile's inputs in flight in
+// 239 VGPRs.  C5, backward pass per 71 k-base group (profiles/r05u_ab_c5_bwd12_prefetch.txt):
+// 3 waves without the prefetch 5.10-5.13 ms (84 bytes of scratch), 3 with it 5.72
+// (284 bytes), 2 without it 5.37-5.40, 2 with it 4.93-4.96
+#define VBHEM_BWD12_WAVES 2
 #endif
 
 namespace vbhem {
@@ -132,10 +137,44 @@ void fb_bwd12_kernel(const SplitArgs p) {
 
   auto tiles = [&](auto zs_tag) {
     constexpr bool ZS = decltype(zs_tag)::value;
-    for (int tile = wave * NBk + t0; tile < ntile; tile += NBk * kNWB12) {
+    const int tstride = NBk * kNWB12;
+    // a tile's global inputs, loaded one tile ahead (as fb_bwd4_kernel): clamped
+    // addresses, the selects on the values only when the tile is processed
+    struct TileIn {
+      double a[NB][NB], e[NB][NB], pr[NB];
+    };
+    auto load_tile = [&](int tile, TileIn &in) {
+      const int i = p.i_begin + tile * 4 + b;
+      const int ic = i < p.i_end ? i : p.i_end - 1;
+#pragma unroll
+      for (int j2 = 0; j2 < NB; ++j2)
+#pragma unroll
+        for (int jj = 0; jj < NB; ++jj) {
+          const int be = 4 * jj + c, bp = 4 * j2 + r;
+          in.a[j2][jj] = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
+        }
+#pragma unroll
+      for (int i2 = 0; i2 < NB; ++i2)
+#pragma unroll
+        for (int jj = 0; jj < NB; ++jj) {
+          const int be = 4 * jj + c;
+          in.e[i2][jj] = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
+                             (be < SB ? be : SB - 1)];
+        }
+#pragma unroll
+      for (int jj = 0; jj < NB; ++jj) {
+        const int be = 4 * jj + c;
+        in.pr[jj] = p.prior[(size_t)ic * SB + (be < SB ? be : SB - 1)];
+      }
+    };
+    TileIn cur;
+    if (wave * NBk + t0 < ntile) load_tile(wave * NBk + t0, cur);
+    for (int tile = wave * NBk + t0; tile < ntile; tile += tstride) {
       const int i0 = p.i_begin + tile * 4;
       const int i = i0 + b;
       const int ic = i < p.i_end ? i : p.i_end - 1;
+      TileIn nxt;
+      load_tile(min(tile + tstride, ntile - 1), nxt);  // (past the last tile: a repeat)
       double Ef[NB][NB], V[NB][NB], AbT[NB][NB];
       // B operand of V = sv Ab^T + Ef, block (J', J): Ab[4J + c][4J' + r] (zero past SB)
 #pragma unroll
@@ -143,8 +182,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
-          const double a = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
-          AbT[j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+          AbT[j2][jj] = (be < SB && bp < SB) ? cur.a[j2][jj] : 0.0;
         }
       double mabs = 0.0;
       bool nf = false;
@@ -152,9 +190,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
       for (int i2 = 0; i2 < NB; ++i2)
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj) {
-          const int be = 4 * jj + c;
-          const double e = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
-                               (be < SB ? be : SB - 1)];
+          const double e = cur.e[i2][jj];
           V[i2][jj] = e;
           // Ef = E + amax[sigma] sum_b' Ab[beta][b'] on the matrix cores
           const double am = amax[4 * i2 + c];
@@ -298,7 +334,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
           const int wqf[1] = {(int)(wc[jj] + kWq0)};
           log_q_n<1, false>(lse1, zsf, wqf, ltab8);
           const int be = 4 * jj + c;
-          const double pr = be < SB ? p.prior[(size_t)ic * SB + be] : 0.0;
+          const double pr = be < SB ? cur.pr[jj] : 0.0;
           y += pr * lse1[0];
         }
         const bool bad = zmin < kZMinHi || !isfinite(y) || rbad;
@@ -319,6 +355,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
           }
         }
       }
+      cur = nxt;
     }
   };
   if (zsafe) tiles(std::true_type{});

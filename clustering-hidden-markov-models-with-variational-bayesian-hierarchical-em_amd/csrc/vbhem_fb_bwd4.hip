@@ -20,7 +20,9 @@
 //                    C = Ef, D = V in P.
 // Per element and step the VALU keeps the exp and the log (7 + 8 fp64 operations,
 // table-driven with LDS tables) and a share of the column maxima; the 16 fmas of
-// the two contractions go to the matrix cores (4 MFMAs per 64 elements).
+// the two contractions go to the matrix cores (4 MFMAs per 64 elements).  A wave's
+// next tile inputs (A, E, the prior) are loaded while it runs the current tile's
+// recursion (C4: 1.51 -> 1.41 ms per launch on one box, profiles/r05u_ab_c4_*).
 //
 // Column maxima without fp64 work.  The exp's range reduction s = V * 2048/ln2 +
 // (1.5 2^52 + 2^31) leaves n + 2^31 (n = round(V 2048/ln2)) in the low word of s as
@@ -196,23 +198,57 @@ void fb_bwd4_kernel(const SplitArgs p) {
   auto tiles = [&](auto zs_tag) {
   constexpr bool ZS = decltype(zs_tag)::value;
   const int ntile = (p.i_end - p.i_begin + kPPW - 1) / kPPW;
-  for (int tile = wave * NB + t0; tile < ntile; tile += NB * kNWB) {
+  const int tstride = NB * kNWB;
+  // a tile's global inputs (A, E, the prior), loaded one tile ahead: the next tile's
+  // loads are in flight during this tile's recursion instead of each tile starting
+  // with a full memory latency (clamped addresses, no selects on the loaded values
+  // until the tile is processed)
+  struct TileIn {
+    double a[kQPW][2][2], e[kQPW][2][2], pr[kQPW];
+  };
+  auto load_tile = [&](int tile, TileIn &in) {
     const int i0 = p.i_begin + tile * kPPW;
+#pragma unroll
+    for (int q = 0; q < kQPW; ++q) {
+      const int i = i0 + 4 * q + b;
+      const int ic = i < p.i_end ? i : p.i_end - 1;
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int be = 4 * jj + c, bp = 4 * j2 + r;
+          in.a[q][j2][jj] = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
+        }
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int be = 4 * jj + c;
+          in.e[q][i2][jj] = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
+                                (be < SB ? be : SB - 1)];
+        }
+      const int be = 4 * (r & 1) + c;
+      in.pr[q] = p.prior[(size_t)ic * SB + (be < SB ? be : SB - 1)];
+    }
+  };
+  TileIn cur;
+  if (wave * NB + t0 < ntile) load_tile(wave * NB + t0, cur);
+  for (int tile = wave * NB + t0; tile < ntile; tile += tstride) {
+    const int i0 = p.i_begin + tile * kPPW;
+    TileIn nxt;
+    load_tile(min(tile + tstride, ntile - 1), nxt);  // (past the last tile: a repeat)
     double Ef[kQPW][2][2], V[kQPW][2][2], AbT[kQPW][2][2];
     bool rbad[kQPW], nfb[kQPW];
     int zmin[kQPW];
 #pragma unroll
     for (int q = 0; q < kQPW; ++q) {
-      const int i = i0 + 4 * q + b;
-      const int ic = i < p.i_end ? i : p.i_end - 1;
       // B operand of V = sv Ab^T + Ef, block (J', J): Ab[4J + c][4J' + r] (zero past SB)
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
-          const double a = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
-          AbT[q][j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+          AbT[q][j2][jj] = (be < SB && bp < SB) ? cur.a[q][j2][jj] : 0.0;
         }
       double mabs = 0.0, rs = 0.0;
       bool nf = false;
@@ -220,9 +256,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
-          const int be = 4 * jj + c;
-          const double e = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
-                               (be < SB ? be : SB - 1)];
+          const double e = cur.e[q][i2][jj];
           V[q][i2][jj] = e;
           // Ef = E + amax[sigma] sum_b' Ab[beta][b'] on the matrix cores
           const double am = amax[4 * i2 + c];
@@ -466,7 +500,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       }
       const double lse = lse1[0];
       const int be = 4 * (r & 1) + c;
-      const double pr = be < SB ? p.prior[(size_t)ic * SB + be] : 0.0;
+      const double pr = be < SB ? cur.pr[q] : 0.0;
       double y = r < 2 ? pr * lse : 0.0;
       const bool bad = zmin[q] < kZMinHi || !isfinite(y) || rbad[q];
       y += shfl_xor_d(y, 1);
@@ -487,6 +521,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
         }
       }
     }
+    cur = nxt;
   }
   };
   if (zsafe) tiles(std::true_type{});

@@ -19,6 +19,8 @@
 //             -- 32 MFMAs per quad and step, two per-pair transposes (G -> G^T,
 //             g^T -> g) through ds_bpermute, and a reciprocal;
 //   outputs   sum_nu_1 [S], sum_t_nu [S][SB], sum_xi = A' o H [S][S] per pair.
+// An item's inputs are loaded during the previous item's forward sweep (C4 list pass
+// 0.240 -> 0.206 ms, profiles/r05v_ab_c4_list4_prefetch.txt).
 // The fallback flags are fb_bwd4_kernel's (underflow of Z, |V| range, non-finite
 // inputs); a flagged pair is recomputed by the exact kernel (or the statistics
 // kernel that folds it), as for fb_split_kernel's list mode.
@@ -59,6 +61,7 @@ void fb_list4_kernel(const SplitArgs p) {
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];
 #endif
   __shared__ int pre[kList4MaxK + 1];  // first quad item of every cluster
+  __shared__ int tots[kList4MaxK];     // the gate lists' lengths
   const int tid = threadIdx.x;
 #if VBHEM_LIST4_R4
   for (int x = tid; x < 2048; x += 64 * kL4NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
@@ -70,8 +73,10 @@ void fb_list4_kernel(const SplitArgs p) {
   if (tid == 0) {
     int s = 0;
     for (int jj = 0; jj < K; ++jj) {
+      const int t = p.list_tot[jj];
       pre[jj] = s;
-      s += (p.list_tot[jj] + 3) / 4;
+      tots[jj] = t;
+      s += (t + 3) / 4;
     }
     pre[K] = s;
   }
@@ -80,7 +85,55 @@ void fb_list4_kernel(const SplitArgs p) {
   const double vlim = kVMax / (double)T - 3.0;
   const int gw = (int)blockIdx.x * kL4NWB + (tid >> 6), nw = (int)gridDim.x * kL4NWB;
 
-  int js = 0;
+  // An item's global inputs (A in both layouts, E, the prior) are loaded during the
+  // previous item's forward sweep, once its first lattice slices are dead (no extra
+  // registers), and the item's gate-list entries at the previous item's start: an
+  // item starts with its inputs in registers instead of two dependent memory
+  // latencies (list entry, then inputs).  Clamped addresses; the selects on the loaded
+  // values only where the item uses them.
+  struct ItemIn {
+    double ab[2][2], e[2][2], pr[2], af[2][2];
+  };
+  auto load_in = [&](int i, int jj, int r_, int c_, ItemIn &in) {
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+      for (int j3 = 0; j3 < 2; ++j3) {
+        const int be = 4 * j3 + c_, bp = 4 * j2 + r_;
+        const int bec = be < SB ? be : SB - 1, bpc = bp < SB ? bp : SB - 1;
+        in.ab[j2][j3] = p.A[((size_t)i * SB + bec) * SB + bpc];
+        in.af[j2][j3] = p.A[((size_t)i * SB + bpc) * SB + bec];
+      }
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j3 = 0; j3 < 2; ++j3) {
+        const int be = 4 * j3 + c_;
+        in.e[i2][j3] = p.E[((size_t)jj * S + 4 * i2 + r_) * p.e_ld + (size_t)(i - p.i_buf0) * SB +
+                           (be < SB ? be : SB - 1)];
+      }
+#pragma unroll
+    for (int j3 = 0; j3 < 2; ++j3) {
+      const int be = 4 * j3 + c_;
+      in.pr[j3] = p.prior[(size_t)i * SB + (be < SB ? be : SB - 1)];
+    }
+  };
+  // the base of pair b of item it (cluster jj; past the list's end: the quad's first)
+  auto base_of = [&](int it, int jj, int b_) -> int {
+    const int n0 = (it - pre[jj]) * 4;
+    const int tot = tots[jj];
+    return p.list[(size_t)jj * p.list_cap + (n0 + b_ < tot ? n0 + b_ : n0)];
+  };
+  int js = 0, jsn = 0;
+  ItemIn cur;
+  int icur = 0;
+  if (gw < nitem) {
+    const int lane = tid & 63;
+    while (pre[js + 1] <= gw) ++js;
+    jsn = js;
+    icur = base_of(gw, __builtin_amdgcn_readfirstlane(js), (lane >> 2) & 3);
+    load_in(icur, __builtin_amdgcn_readfirstlane(js), lane >> 4, lane & 3, cur);
+  }
   for (int it = gw; it < nitem; it += nw) {
     // lane geometry recomputed per item from an opaque copy of the thread id, so that
     // no lane-invariant address is hoisted out of the item loop (such live ranges
@@ -92,8 +145,12 @@ void fb_list4_kernel(const SplitArgs p) {
     const int qsrc0 = (4 * b + r) << 2, qsrc1 = (16 + 4 * b + r) << 2;
     const int taddr = (16 * c + 4 * b + r) << 2;
     const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
-    while (pre[js + 1] <= it) ++js;  // items ascend within a wave: continue the search
-    const int j = __builtin_amdgcn_readfirstlane(js);
+    const int j = __builtin_amdgcn_readfirstlane(js);  // (js: advanced to it)
+    // the next item (a repeat of this one past the end): its cluster and list entry now
+    const int itn = min(it + nw, nitem - 1);
+    while (pre[jsn + 1] <= itn) ++jsn;
+    const int jn = __builtin_amdgcn_readfirstlane(jsn);
+    const int inext = base_of(itn, jn, b);
     // the cluster's constants, loaded per item (cache hits; holding them across items
     // spilled 17 values to scratch): A'^T as the B operand of Z^T (block (K, I'):
     // A'[4I' + c][4K + r]), A' in P (A'[4I + r][4I' + c]), amax (rows 4I + c), lpi
@@ -122,9 +179,9 @@ void fb_list4_kernel(const SplitArgs p) {
       cl_nf = __ballot(nf) != 0;
     }
     const int n0 = (it - pre[j]) * 4;
-    const int tot = p.list_tot[j];
+    const int tot = tots[j];
     const bool act = n0 + b < tot;
-    const int i = p.list[(size_t)j * p.list_cap + (act ? n0 + b : n0)];
+    const int i = icur;
     const size_t lp = (size_t)(i - p.i_buf0) * K + j;
 
     // ---- per-pair inputs: Ab^T as the backward's B operand, E, Ef ----
@@ -134,8 +191,7 @@ void fb_list4_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int be = 4 * jj + c, bp = 4 * j2 + r;
-        const double a = p.A[((size_t)i * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
-        AbT[j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+        AbT[j2][jj] = (be < SB && bp < SB) ? cur.ab[j2][jj] : 0.0;
       }
     double mabs = 0.0, rs = 0.0;
     bool nfp = false;
@@ -143,9 +199,7 @@ void fb_list4_kernel(const SplitArgs p) {
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
-        const int be = 4 * jj + c;
-        const double e = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(i - p.i_buf0) * SB +
-                             (be < SB ? be : SB - 1)];
+        const double e = cur.e[i2][jj];
         V[i2][jj] = e;
         Ef[i2][jj] = mfma4(amQ[i2], AbT[1][jj], mfma4(amQ[i2], AbT[0][jj], e));
         mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[i2][jj])));
@@ -273,8 +327,7 @@ void fb_list4_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int be = 4 * jj + c;
-        const double pr = p.prior[(size_t)i * SB + (be < SB ? be : SB - 1)];
-        const double pb = be < SB ? pr : 0.0;
+        const double pb = be < SB ? cur.pr[jj] : 0.0;
         nu[0][jj] = pb * ef[jj];
         nu[1][jj] = pb * ef[2 + jj];
       }
@@ -295,9 +348,9 @@ void fb_list4_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int bp = 4 * j2 + r, be = 4 * jj + c;
-        const double a = p.A[((size_t)i * SB + (bp < SB ? bp : SB - 1)) * SB + (be < SB ? be : SB - 1)];
-        AbF[j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+        AbF[j2][jj] = (be < SB && bp < SB) ? cur.af[j2][jj] : 0.0;
       }
+    ItemIn nxt;
     double nuT[2][2], tnT[2][2], H[2][2];
     transpose8(nu, nuT, taddr);
 #pragma unroll
@@ -309,6 +362,8 @@ void fb_list4_kernel(const SplitArgs p) {
       }
 #pragma unroll
     for (int t = 1; t < T; ++t) {
+      // the next item's inputs, into the registers of the lattice slices 1 .. T/2 - 1
+      if (t == T / 2) load_in(inext, jn, r, c, nxt);
       double Gt[2][2];
       transpose8(lat[t], Gt, taddr);
       // f^T block (J, I) = sum_J' Ab(J', J)^T nu^T(J', I); Z^T block (J, I') as the backward's
@@ -371,6 +426,9 @@ void fb_list4_kernel(const SplitArgs p) {
         p.flag_list[slot] = (int)((size_t)i * K + j);
       }
     }
+    cur = nxt;
+    icur = inext;
+    js = jsn;
   }
 }
 
