@@ -74,6 +74,7 @@ void fb_list12_kernel(const SplitArgs p) {
   double *const etab = tabs;           // 2^(i/2048 - 1010)
   double *const ltab8 = tabs + 2048;   // {1/c, -log(1/c)}
   __shared__ int pre[kList4MaxK + 1];  // first quad item of every cluster
+  __shared__ int tots[kList4MaxK];     // the gate lists' lengths
   const int tid = threadIdx.x;
   for (int x = tid; x < 2048; x += 64 * kL12NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
   stage_log8k(ltab8, tid, 64 * kL12NWB);
@@ -81,8 +82,10 @@ void fb_list12_kernel(const SplitArgs p) {
   if (tid == 0) {
     int s = 0;
     for (int jj = 0; jj < K; ++jj) {
+      const int t = p.list_tot[jj];
       pre[jj] = s;
-      s += (p.list_tot[jj] + 3) / 4;
+      tots[jj] = t;
+      s += (t + 3) / 4;
     }
     pre[K] = s;
   }
@@ -98,10 +101,61 @@ void fb_list12_kernel(const SplitArgs p) {
   const int taddr = (16 * c + 4 * b + r) << 2;
   const unsigned long long pmask = 0x000F000F000F000Full << (4 * b);
 
-  int js = 0;
+  // An item's global inputs (A in both layouts, E, the prior) are loaded during the
+  // previous item's forward sweep, into the registers of lattice slices that are dead
+  // by then, and its gate-list entries at the previous item's start (as
+  // fb_list4_kernel): with one wave per SIMD nothing else hides an item's start-up
+  // latency (C5: 0.588 -> 0.523 ms per group, profiles/r05w_ab_c5_list12_prefetch.txt).
+  // Clamped addresses; the selects on the values where the item uses them.
+  struct ItemIn {
+    double ab[NB][NB], af[NB][NB], e[NB][NB], pr[NB];
+  };
+  auto load_in = [&](int i, int jj, ItemIn &in) {
+#pragma unroll
+    for (int j2 = 0; j2 < NB; ++j2)
+#pragma unroll
+      for (int j3 = 0; j3 < NB; ++j3) {
+        const int be = 4 * j3 + c, bp = 4 * j2 + r;
+        const int bec = be < SB ? be : SB - 1, bpc = bp < SB ? bp : SB - 1;
+        in.ab[j2][j3] = p.A[((size_t)i * SB + bec) * SB + bpc];
+        in.af[j2][j3] = p.A[((size_t)i * SB + bpc) * SB + bec];
+      }
+#pragma unroll
+    for (int i2 = 0; i2 < NB; ++i2)
+#pragma unroll
+      for (int j3 = 0; j3 < NB; ++j3) {
+        const int be = 4 * j3 + c;
+        in.e[i2][j3] = p.E[((size_t)jj * S + 4 * i2 + r) * p.e_ld + (size_t)(i - p.i_buf0) * SB +
+                           (be < SB ? be : SB - 1)];
+      }
+#pragma unroll
+    for (int j3 = 0; j3 < NB; ++j3) {
+      const int be = 4 * j3 + c;
+      in.pr[j3] = p.prior[(size_t)i * SB + (be < SB ? be : SB - 1)];
+    }
+  };
+  // the base of pair b of item it (cluster jj; past the list's end: the quad's first)
+  auto base_of = [&](int it, int jj) -> int {
+    const int n0 = (it - pre[jj]) * 4;
+    const int tot = tots[jj];
+    return p.list[(size_t)jj * p.list_cap + (n0 + b < tot ? n0 + b : n0)];
+  };
+  int js = 0, jsn = 0;
+  ItemIn cur;
+  int icur = 0;
+  if (gw < nitem) {
+    while (pre[js + 1] <= gw) ++js;
+    jsn = js;
+    icur = base_of(gw, __builtin_amdgcn_readfirstlane(js));
+    load_in(icur, __builtin_amdgcn_readfirstlane(js), cur);
+  }
   for (int it = gw; it < nitem; it += nw) {
-    while (pre[js + 1] <= it) ++js;  // items ascend within a wave: continue the search
-    const int j = __builtin_amdgcn_readfirstlane(js);
+    const int j = __builtin_amdgcn_readfirstlane(js);  // (js: advanced to it)
+    // the next item (a repeat of this one past the end): its cluster and list entry now
+    const int itn = min(it + nw, nitem - 1);
+    while (pre[jsn + 1] <= itn) ++jsn;
+    const int jn = __builtin_amdgcn_readfirstlane(jsn);
+    const int inext = base_of(itn, jn);
     // the cluster's constants, per item (cache hits): A'^T as the B operand of Z^T
     // (block (K, I'): A'[4I' + c][4K + r]), A' in P (A'[4I + r][4I' + c]), amax (rows
     // 4I + c), lpi (rows 4I + r)
@@ -127,9 +181,9 @@ void fb_list12_kernel(const SplitArgs p) {
       cl_nf = __ballot(nf) != 0;
     }
     const int n0 = (it - pre[j]) * 4;
-    const int tot = p.list_tot[j];
+    const int tot = tots[j];
     const bool act = n0 + b < tot;
-    const int i = p.list[(size_t)j * p.list_cap + (act ? n0 + b : n0)];
+    const int i = icur;
     const size_t lp = (size_t)(i - p.i_buf0) * K + j;
 
     // ---- per-pair inputs: Ab^T as the backward's B operand, E, Ef ----
@@ -139,8 +193,7 @@ void fb_list12_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj) {
         const int be = 4 * jj + c, bp = 4 * j2 + r;
-        const double a = p.A[((size_t)i * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
-        AbT[j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+        AbT[j2][jj] = (be < SB && bp < SB) ? cur.ab[j2][jj] : 0.0;
       }
     double mabs = 0.0, rs = 0.0;
     bool nfp = false;
@@ -148,9 +201,7 @@ void fb_list12_kernel(const SplitArgs p) {
     for (int i2 = 0; i2 < NB; ++i2)
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj) {
-        const int be = 4 * jj + c;
-        const double e = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(i - p.i_buf0) * SB +
-                             (be < SB ? be : SB - 1)];
+        const double e = cur.e[i2][jj];
         V[i2][jj] = e;
         double ef = e;
 #pragma unroll
@@ -294,8 +345,7 @@ void fb_list12_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj) {
         const int be = 4 * jj + c;
-        const double pr = p.prior[(size_t)i * SB + (be < SB ? be : SB - 1)];
-        const double pb = be < SB ? pr : 0.0;
+        const double pb = be < SB ? cur.pr[jj] : 0.0;
 #pragma unroll
         for (int i2 = 0; i2 < NB; ++i2) nu[i2][jj] = pb * e2[i2 * NB + jj];
       }
@@ -316,9 +366,9 @@ void fb_list12_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj) {
         const int bp = 4 * j2 + r, be = 4 * jj + c;
-        const double a = p.A[((size_t)i * SB + (bp < SB ? bp : SB - 1)) * SB + (be < SB ? be : SB - 1)];
-        AbF[j2][jj] = (be < SB && bp < SB) ? a : 0.0;
+        AbF[j2][jj] = (be < SB && bp < SB) ? cur.af[j2][jj] : 0.0;
       }
+    ItemIn nxt;
     // A' in P (A'[4I + r][4I' + c]), loaded only now: not live across the backward sweep
     double Ap[NB][NB];
 #pragma unroll
@@ -336,6 +386,8 @@ void fb_list12_kernel(const SplitArgs p) {
       }
 #pragma unroll
     for (int t = 1; t < T; ++t) {
+      // the next item's inputs, into the registers of the lattice slices 1 .. T/2 - 1
+      if (t == T / 2) load_in(inext, jn, nxt);
       double Gt[NB][NB];
       transpose12(lat[t], Gt, taddr);
       // f^T block (J, I) = sum_J' Ab(J', J)^T nu^T(J', I); Z^T block (J, I') as the backward's
@@ -419,6 +471,9 @@ void fb_list12_kernel(const SplitArgs p) {
         p.flag_list[slot] = (int)((size_t)i * K + j);
       }
     }
+    cur = nxt;
+    icur = inext;
+    js = jsn;
   }
 }
 
