@@ -93,14 +93,20 @@ __device__ __forceinline__ double group_sum(double v, int G) {
 #ifndef VBHEM_RESP_WPE
 #define VBHEM_RESP_WPE 4
 #endif
+typedef unsigned int resp_u2 __attribute__((ext_vector_type(2)));
+
+// KP: K when it is a power of two <= 64 (every lane of a base group holds a cluster:
+// the group reductions unroll and the stores need no lane mask), else 0
+template <int KP>
 __global__ __launch_bounds__(kRespThreads) __attribute__((amdgpu_waves_per_eu(VBHEM_RESP_WPE))) void resp_kernel(
     const StatsArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = kRespThreads / 64;
-  const int K = p.K;
-  int G = 1;
-  while (G < K && G < 64) G <<= 1;
+  const int K = KP ? KP : p.K;
+  int G = KP ? KP : 1;
+  if (!KP)
+    while (G < K && G < 64) G <<= 1;
   const int BPW = 64 / G;            // bases per wave step
   const int sub = lane / G, gl = lane - sub * G;
   double *accNj = lds;               // [NW*BPW][K]
@@ -133,7 +139,58 @@ __global__ __launch_bounds__(kRespThreads) __attribute__((amdgpu_waves_per_eu(VB
   for (int x = tid; x < K; x += kRespThreads) gcnt[x] = 0;
   __syncthreads();
   double l1 = 0.0, l7 = 0.0;
-  if (K <= G) {
+  if constexpr (KP > 0) {
+    // K = G: a lane per cluster, 64 / K bases per wave step.  Two bases' loads in
+    // flight behind the one being computed (two named buffers, no register copies), and
+    // the hat_Z / Z stores are buffer stores whose lanes past the chunk carry an
+    // out-of-range offset (dropped by the hardware) instead of a branch: the compiler
+    // then waits for a buffer's loads without also waiting for the stores issued after
+    // them (a join after branched stores drains every store of the step)
+    constexpr int BP = 64 / KP;
+    const int stride = NW * BP;
+    const double lo = p.logOmega[gl];
+    const int nb = b1 - b0;
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+        p.hatZ + (size_t)b0 * KP, (short)0, nb * KP * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        p.Z + (size_t)(b0 - p.i_buf0) * KP, (short)0, nb * KP * 8, 0x00020000);
+    auto step = [&](int ib, double tnb, double llb) {
+#pragma clang fp contract(off)
+      const bool iv = ib < b1;
+      const double lz = tnb * (lo + llb);  // rounded before the shift (see below)
+      double mx = lz;
+#pragma unroll
+      for (int off = KP >> 1; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+      double sm = exp(lz - mx);
+#pragma unroll
+      for (int off = KP >> 1; off >= 1; off >>= 1) sm += __shfl_xor(sm, off, 64);
+      const double lse = mx + log(sm);
+      const double hz = exp(lz - lse) + 1e-50;
+      const double Z = hz * tnb;
+      const int off = iv ? ((ib - b0) * KP + gl) * 8 : 0x7ffffff0;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(resp_u2, hz), rh, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(resp_u2, Z), rz, off, 0, 0);
+      // (no branch in the step: the lanes past the chunk add zeros)
+      accNj[(wave * BP + sub) * KP + gl] += iv ? Z : 0.0;
+      atomicAdd(&gcnt[gl], (iv && Z > kGateZ) ? 1 : 0);
+      l1 += iv ? Z * llb : 0.0;
+      l7 += iv ? hz * log(hz) : 0.0;
+    };
+    auto ld = [&](int ib, double &tnb, double &llb) {
+      const int ii = ib < b1 ? ib : b0;
+      tnb = p.tildeN[ii];
+      llb = p.LL[(size_t)ii * KP + gl];
+    };
+    int i = b0 + wave * BP + sub;
+    double tA, lA, tB, lB;
+    ld(i, tA, lA);
+    for (; i - sub < b1; i += 2 * stride) {
+      ld(i + stride, tB, lB);
+      step(i, tA, lA);
+      ld(i + 2 * stride, tA, lA);
+      step(i + stride, tB, lB);  // (past the chunk: every lane adds zeros, stores dropped)
+    }
+  } else if (K <= G) {
     // one cluster per lane: the next base's tilde_N and L_elbo are loaded while
     // this base's ẑ is computed (a C4 wave walks 6 bases of its chunk in turn)
     const int stride = NW * BPW;
@@ -921,6 +978,14 @@ size_t resp_lds(int K, int KT) {
                   (size_t)(kRespThreads + 1) * sizeof(int));
 }
 
+template <int KP>
+static hipError_t launch_resp_k(const StatsArgs &a, int nchunk, size_t lds, hipStream_t st) {
+  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&resp_kernel<KP>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(resp_kernel<KP>, dim3(nchunk), dim3(kRespThreads), lds, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
   // per-wave Nj accumulators of all K clusters in LDS (past 64 KB at K ~ 960: the
   // launch sets the dynamic-LDS attribute; the caller rejects K past a CU's LDS)
@@ -934,10 +999,14 @@ hipError_t launch_resp(const StatsArgs &a, int nchunk, hipStream_t st) {
     hipLaunchKernelGGL(resp_trials_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
     return hipGetLastError();
   }
-  hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(&resp_kernel), lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(resp_kernel, dim3(nchunk), dim3(kRespThreads), lds, st, a);
-  return hipGetLastError();
+  switch (std::getenv("VBHEM_RESP_GENERIC") ? 0 : a.K) {  // (A/B: the generic kernel)
+    case 4: return launch_resp_k<4>(a, nchunk, lds, st);
+    case 8: return launch_resp_k<8>(a, nchunk, lds, st);
+    case 16: return launch_resp_k<16>(a, nchunk, lds, st);
+    case 32: return launch_resp_k<32>(a, nchunk, lds, st);
+    case 64: return launch_resp_k<64>(a, nchunk, lds, st);
+    default: return launch_resp_k<0>(a, nchunk, lds, st);
+  }
 }
 
 hipError_t launch_stats(const StatsArgs &a, int nchunk, int ngroups, size_t lds, hipStream_t st) {
