@@ -561,7 +561,13 @@ __global__ __launch_bounds__(kUThreads) void us_build_kernel(UPrepArgs p, double
 #ifndef UNWAVE_MAXT
 #define UNWAVE_MAXT 512  // launch bound of emission_u_kernel (threads per block)
 #endif
-template <int KQB, int RC, int NTW, bool EXACT, bool PF = false, int SPL = 1>
+typedef unsigned int em_u2 __attribute__((ext_vector_type(2)));
+
+// BST (the PF path): E stores as buffer stores, a lane outside the tile carrying an
+// out-of-range offset instead of a branch, and the next round's U loads branch-free
+// (clamped), so the wait for those loads counts the stores issued after them exactly
+// instead of draining every store of the round at a join (E < 4 GB: the launcher)
+template <int KQB, int RC, int NTW, bool EXACT, bool PF = false, int SPL = 1, bool BST = false>
 __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p) {
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -621,9 +627,18 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
         const long long it = item_at(r);
         const long long tile = t_first + (it < nitem ? it / SPL : 0);
         const double *Ut = p.U + kUHead + (size_t)tile * kq * 64 + lane;
+        if constexpr (BST) {
+          // (t past kq: a repeat of the last slice, never used)
 #pragma unroll
-        for (int t = 0; t < KQB; ++t) u[t] = t < kq ? Ut[(size_t)t * 64] : 0.0;
+          for (int t = 0; t < KQB; ++t) u[t] = Ut[(size_t)min(t, kq - 1) * 64];
+        } else {
+#pragma unroll
+          for (int t = 0; t < KQB; ++t) u[t] = t < kq ? Ut[(size_t)t * 64] : 0.0;
+        }
       };
+      __amdgpu_buffer_rsrc_t re;
+      if constexpr (BST)
+        re = __builtin_amdgcn_make_buffer_rsrc(p.E, (short)0, (int)(unsigned)((size_t)KS * ldE * 8), 0x00020000);
       double u[KQB], un[KQB];
       if (rounds_i > 0) load_u(0, u);
 #pragma unroll 1
@@ -634,7 +649,8 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
         const long long col = p.u_col0 + tile * 16 + cl;
         const bool cv = it < nitem && col >= c_begin && col < c_end;
         double *Ec = p.E + (cv ? col - (long long)p.i_buf0 * SB : 0);
-        if (r + 1 < rounds_i) load_u(r + 1, un);
+        if constexpr (BST) load_u(r + 1, un);  // (past the last round: a repeat, unused)
+        else if (r + 1 < rounds_i) load_u(r + 1, un);
         // W' is loop-invariant: an opaque offset keeps its LDS reads in the loop
         // (hoisted, 88 values would take 176 VGPRs)
         int woff = lane + q0 * 64, boff = kl + q0 * 16;
@@ -653,7 +669,25 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
                                                             0, 0, 0);
           }
         }
-        if (cv) {
+        if constexpr (BST) {
+          const unsigned cofs = (unsigned)(cv ? col - (long long)p.i_buf0 * SB : 0) * 8u;
+          auto put = [&](int row, double x) {
+            const unsigned off = (cv && row < KS) ? cofs + (unsigned)row * (unsigned)ldE * 8u : 0xfffffff8u;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(em_u2, x), re, (int)off, 0, 0);
+          };
+          // the VHEM division behind a uniform branch (both sides: the same stores)
+          if (vhem) {
+#pragma unroll
+            for (int q = 0; q < RCI; ++q)
+#pragma unroll
+              for (int v = 0; v < 4; ++v) put((q0 + q) * 16 + kl + 4 * v, acc[q][v] / sm);
+          } else {
+#pragma unroll
+            for (int q = 0; q < RCI; ++q)
+#pragma unroll
+              for (int v = 0; v < 4; ++v) put((q0 + q) * 16 + kl + 4 * v, acc[q][v]);
+          }
+        } else if (cv) {
           // the VHEM division (hem_hmm_bwd_fwd_mex.c:848-860) behind a uniform branch:
           // written as a select, the full fp64 division ran for every stored value
           if (vhem) {
@@ -780,6 +814,12 @@ hipError_t launch_us_build(const UPrepArgs &a, double *Us, hipStream_t st) {
 #ifndef UNWAVE_SINGLE
 #define UNWAVE_SINGLE 4  // 133 VGPRs at kq <= 12: 3 waves per SIMD, 4-wave blocks use them all
 #endif
+// the buffer-store path addresses E with 32-bit byte offsets (the fused E-step's base
+// groups keep E below 4 GB; a caller's own buffer may not)
+static bool em_bst_ok(const EmissionArgs &a) {
+  return (unsigned long long)a.K * a.S * (unsigned long long)a.e_ld * 8ull < 0xfffffff0ull;
+}
+
 bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   const int kq = a.kdp / 4;
   if (kq > kUMaxKq) {
@@ -795,12 +835,16 @@ bool plan_emission_u(EmissionArgs &a, size_t &lds) {
   return true;
 }
 
-template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false, int SPL = 1>
+template <int KQB, int RC, int NTW, bool EXACT = false, bool PF = false, int SPL = 1, bool BST = false>
 static hipError_t launch_u_fn(const EmissionArgs &a, size_t lds, hipStream_t st) {
   if (EXACT && a.kdp / 4 != KQB) return hipErrorInvalidValue;
   if (PF && (NTW != 1 || a.ksp / 16 != RC)) return hipErrorInvalidValue;
   if (SPL != 1 && !PF) return hipErrorInvalidValue;
-  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF, SPL>;
+  if (BST && !PF) return hipErrorInvalidValue;
+  if constexpr (PF && !BST)
+    if (em_bst_ok(a) && !std::getenv("VBHEM_EM_NOBST"))  // (A/B switch)
+      return launch_u_fn<KQB, RC, NTW, EXACT, PF, SPL, true>(a, lds, st);
+  auto *fn = &emission_u_kernel<KQB, RC, NTW, EXACT, PF, SPL, BST>;
   hipError_t e = set_dyn_lds(reinterpret_cast<const void *>(fn), lds);
   if (e != hipSuccess) return e;
   const int cus = device_cus();
