@@ -447,6 +447,7 @@ void fb_list12_kernel(const SplitArgs p) {
         }
     }
 
+    wait_vm_prefetch();  // (the next item's inputs: before this item's stores)
     // ---- outputs and fallback flags ----
     const bool pbad = (__ballot(bad) & pmask) != 0;
     const bool pnf = cl_nf || (__ballot(nfp) & pmask) != 0;

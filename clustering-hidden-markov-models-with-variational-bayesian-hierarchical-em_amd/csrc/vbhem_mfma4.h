@@ -34,6 +34,16 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
+// s_waitcnt vmcnt(0) alone (expcnt 7, lgkmcnt 15 on gfx9), issued where the only vector
+// memory operations in flight are a prefetch that has had most of an item to land: the
+// compiler's own wait before the prefetched registers are copied would otherwise come
+// after the item's output stores and wait for those as well (they count in vmcnt, and
+// the stores sit behind lane branches, so the compiler cannot count past them).
+// fb_list12_kernel (one wave per SIMD): 0.522 -> 0.512 ms per C5 group; in
+// fb_list4_kernel it measured 0.206 -> 0.215 ms and in the backward kernels no change
+// (profiles/r05z_ab_*), so only there
+__device__ __forceinline__ void wait_vm_prefetch() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // s = V 2048/ln2 + 1.5 2^52 + 2^31: n + 2^31 in the low word (exact for |V| < 7.3e5)
 __device__ __forceinline__ double red_s(double v) { return fma(v, kInvLn2N, kShiftU); }
 __device__ __forceinline__ unsigned lo_u(double x) { return (unsigned)__double2loint(x); }
