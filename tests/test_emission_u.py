@@ -154,9 +154,9 @@ def test_stats_on_prepared_operand(vb, name, prepare, monkeypatch):
     for env in ({"VBHEM_NO_STATS_U": "1"}, {"VBHEM_STATS_U": "1", **no_m},
                 {"VBHEM_STATS_U": "1", "VBHEM_SU_BLOCKS": str(K), **no_m},
                 {"VBHEM_STATS_U": "1", "VBHEM_NO_STATS_G": "1", **no_m},
-                {}, {"VBHEM_SU_BLOCKS": str(K + 1)}, {"VBHEM_SM_G": "1"}):
+                {}, {"VBHEM_SU_BLOCKS": str(K + 1)}):
         for k in ("VBHEM_NO_STATS_U", "VBHEM_SU_BLOCKS", "VBHEM_STATS_U", "VBHEM_NO_STATS_G",
-                  "VBHEM_NO_STATS_M", "VBHEM_SM_G"):
+                  "VBHEM_NO_STATS_M"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -183,6 +183,35 @@ def test_row_split_bit_identical(vb, monkeypatch, N):
     outs = []
     for split in ("0", "1"):
         monkeypatch.setenv("VBHEM_EM_SPLIT", split)
+        eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
+        eng.set_clusters(consts)
+        eng.set_log_omega(host.log_omega_tilde(P.alpha))
+        tN = (100.0 * N) * eng.base.omega
+        outs.append((eng.fused(tN).clone(), eng.LL.clone(), eng.hatZ.clone()))
+        del eng
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,N", [("C4", 12500), ("C3", 4000)])
+@pytest.mark.parametrize("switch", ["VBHEM_EM_NOBST", "VBHEM_RESP_GENERIC"])
+def test_store_paths_bit_identical(vb, monkeypatch, cfg, N, switch):
+    """The one-chunk emission GEMM's buffer stores (lanes outside the tile dropped by an
+    out-of-range offset) and resp_kernel's K-templated path (unrolled group reductions,
+    buffer stores of hat_Z / Z) write exactly what the branched paths write: the fused
+    E-step's outputs are bit-identical with VBHEM_EM_NOBST / VBHEM_RESP_GENERIC set and
+    unset (both read at launch), C4's shape (K = 16) and C3's (K = 8)."""
+    from vbhem_amd import host
+    from vbhem_amd.estep import EStepEngine
+    base, P, opt = vb.synth_workload(cfg, N=N, device=DEV)
+    consts = host.cluster_constants(P, base.covmode)
+    outs = []
+    for on in (False, True):
+        if on:
+            monkeypatch.setenv(switch, "1")
+        else:
+            monkeypatch.delenv(switch, raising=False)
         eng = EStepEngine(base, P.K, P.S, opt["tau"], device=DEV)
         eng.set_clusters(consts)
         eng.set_log_omega(host.log_omega_tilde(P.alpha))
