@@ -1610,12 +1610,16 @@ static hipError_t launch_sm_pd(const StatsArgs &a, const dim3 &grid, hipStream_t
   return hipGetLastError();
 }
 
-// ring depth 2 (C4: 0.177 ms of statistics per step against 0.191 with depth 4 and
-// its 768 resident blocks; C5: depth 3 drops the residency from 3 to 2 blocks per CU,
-// 7.7 vs 5.8 ms of statistics per step)
+// ring depth 3 since the load phase is branch-free (profiles/r05ad_ab_stats_ring_depth.txt:
+// statistics per step C4 0.160 -> 0.155 ms, C5 4.7-4.9 -> 4.5-4.7 ms, shard and C3 equal;
+// depth 4 in between).  Before that fix depth 3 lost: the ring never filled and its
+// registers cost residency (C5 7.7 vs 5.8 ms)
+#ifndef VBHEM_SM_PDD
+#define VBHEM_SM_PDD 3   // the ring depth (build switch for A/B)
+#endif
 template <int NTW, int G, int KSM, int NXR>
 static hipError_t launch_sm(const StatsArgs &a, const dim3 &grid, hipStream_t st) {
-  return launch_sm_pd<NTW, G, KSM, NXR, 2>(a, grid, st);
+  return launch_sm_pd<NTW, G, KSM, NXR, VBHEM_SM_PDD>(a, grid, st);
 }
 
 // the sum_nu_1 | sum_xi chunks per wave: ceil(ceil((S + S^2) / 64) / tile groups)
