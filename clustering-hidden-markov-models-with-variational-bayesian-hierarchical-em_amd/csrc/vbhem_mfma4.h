@@ -28,6 +28,7 @@ constexpr double kVMax = 7.0e5;                       // |V| limit of the intege
 namespace {  // one copy per translation unit
 alignas(16) __device__ const double kExpTab4[2048] = VBHEM_EXP2048_TABLE_INIT;
 alignas(16) __device__ const double kLogTab4[2 * 1024] = VBHEM_LOG12_TABLE_INIT;
+alignas(16) __device__ const double kLogTab8k[2 * 8192] = VBHEM_LOG8K_TABLE_INIT;
 }  // namespace
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
@@ -183,15 +184,17 @@ __device__ __forceinline__ void stage_tables(double *etab, double *ltab, int tid
 // ---- the round-4 step helpers (fb_bwd4_kernel, fb_bwd12_kernel) ----
 // the 8192-interval log table, {1/c, -log(1/c)} with c the centre of [1 + k/8192,
 // 1 + (k+1)/8192) and 1/c rounded to a double (the table need not hold 1/c exactly:
-// log zz = -log(ic) + log1p(zz ic - 1) for any ic), staged per block with the
-// device's correctly rounded division and libm-accurate log
+// log zz = -log(ic) + log1p(zz ic - 1) for any ic), generated with correctly rounded
+// logs (scripts/gen_log_table.py) and copied into each block's LDS: 16-byte loads from
+// L2 instead of a division and a libm log per entry (computing it took ~6 us of every
+// fb_bwd4_kernel launch, profiles/r05ah_ab_shard_cheap_stage.txt)
 __device__ __forceinline__ void stage_log8k(double *ltab, int tid, int nt) {
-  for (int k = tid; k < 8192; k += nt) {
-    const double c = 1.0 + ((double)k + 0.5) * (1.0 / 8192.0);
-    const double ic = 1.0 / c;
-    ltab[2 * k] = ic;
-    ltab[2 * k + 1] = -log(ic);
-  }
+  const double2 *src = reinterpret_cast<const double2 *>(kLogTab8k);
+  double2 *dst = reinterpret_cast<double2 *>(ltab);
+  // (unrolled: a 4-wave block's 32 copies per thread go out in two batches, not one
+  // memory latency after another)
+#pragma unroll 16
+  for (int k = tid; k < 8192; k += nt) dst[k] = src[k];
 }
 
 // log(Z) + M, 8192-interval table, log1p(r) = r - r^2/2 (|r| <= 2^-14): kk = the
