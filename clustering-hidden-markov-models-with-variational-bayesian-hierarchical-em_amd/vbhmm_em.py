@@ -9,7 +9,13 @@ work, restated here from:
 
 * vbhmm_em.m:112-414  the EM loop (E-step :133-246, bound :251-275, convergence
   and NaN handling :277-349, M-step :352-408) and the output model :426-491;
-* vbhmm_em_lb.m:74-257  the lower bound (no hyperparameter derivatives);
+* vbhmm_em_lb.m:74-257  the lower bound, :260-400 its derivatives with respect to
+  the (transformed) hyperparameters;
+* vbhmm_em_hyp.m + get_hypinfo.m  hyperparameter learning (``learn_hyps``): the
+  bound maximised over the transformed hyperparameters with minimize_new.m's BFGS
+  (:func:`hyp.minimize`), every evaluation an EM run from the trial's HMM
+  ('inithmm', vbhmm_init.m:154-161) with the derivatives at its last E-step;
+  vbhmm_learn.m:482-552 runs it on each unique random trial (uniqueLL.m);
 * vbhmm_init.m:122-204  the initial posterior from a GMM; :27-43 the K = 1 and
   N <= K special cases of the 'random' mode;
 * vbhmm_clip_hyps.m:20-85, vbhmm_learn.m:252-310 (defaults), :440-480 (random
@@ -44,7 +50,8 @@ def vbhmm_default_options(dim: int, **over) -> dict:
     defmu = {2: [256.0, 192.0], 3: [256.0, 192.0, 150.0]}.get(dim, [0.0] * dim)
     opt = dict(alpha0=0.1, mu0=defmu, W0=0.005, beta0=1.0, v0=5.0, epsilon0=0.1,
                initmode="random", numtrials=50, maxIter=100, minDiff=1e-5, seed=None,
-               fix_clusters=0, fix_cov=None, verbose=0)
+               fix_clusters=0, fix_cov=None, verbose=0, learn_hyps=0, calc_LLderiv=0,
+               minimizer="minimize-bfgs", hyp_length=100)
     opt["hyps_max"] = dict(alpha0=1.0686e13, epsilon0=1.0686e13, v0=1e4, beta0=1.0686e13,
                            W0=1.0686e13)
     opt["hyps_min"] = dict(alpha0=1.0686e-13, epsilon0=1.0686e-13, v0=2.0612e-09 + dim - 1,
@@ -136,7 +143,7 @@ def random_gmm(data: Sequence[np.ndarray], K: int, rng: np.random.Generator) -> 
 
 def vbhmm_init(data: Sequence[np.ndarray], K: int, opt: dict, gmm: dict) -> dict:
     """vbhmm_init.m:122-204: the initial variational posterior from a GMM
-    (prior [K], mean [K][dim], cov [K][dim][dim])."""
+    (prior [K], mean [K][dim], cov [K][dim][dim]), or ('inithmm') an HMM's own."""
     X = np.concatenate([np.asarray(a, dtype=np.float64) for a in data], axis=0)
     N, dim = X.shape
     if len(opt["mu0"]) != dim:
@@ -145,6 +152,13 @@ def vbhmm_init(data: Sequence[np.ndarray], K: int, opt: dict, gmm: dict) -> dict
     W0m = float(W0) * np.eye(dim) if W0.size == 1 else np.diag(W0.reshape(-1))
     W0inv = np.linalg.inv(W0m)
     beta0, v0, m0 = float(opt["beta0"]), float(opt["v0"]), opt["mu0"]
+    W0mode = "iid" if W0.size == 1 else "diag"
+    if opt.get("initmode") == "inithmm":  # vbhmm_init.m:154-161: the HMM's own posterior
+        vp = opt["inithmm"]["varpar"]
+        return dict(alpha=np.array(vp["alpha"], float), epsilon=np.array(vp["epsilon"], float),
+                    beta=np.array(vp["beta"], float), v=np.array(vp["v"], float),
+                    m=np.array(vp["m"], float), W=np.array(vp["W"], float), W0inv=W0inv,
+                    W0mode=W0mode)
     Nk = N * np.asarray(gmm["prior"], dtype=np.float64).reshape(-1)
     Nk2 = np.full(K, N / K)
     xbar = np.asarray(gmm["mean"], dtype=np.float64).reshape(K, dim)
@@ -160,14 +174,20 @@ def vbhmm_init(data: Sequence[np.ndarray], K: int, opt: dict, gmm: dict) -> dict
         diff3 = xbar[k] - m0
         W[k] = np.linalg.inv(W0inv + Nk[k] * S[k] + mult1 * np.outer(diff3, diff3))
     return dict(alpha=alpha, epsilon=epsilon, beta=beta, v=v, m=m, W=W, W0inv=W0inv,
-                W0mode="iid" if W0.size == 1 else "diag")
+                W0mode=W0mode)
 
 
 # ----------------------------------------------------------------------------
-# lower bound (vbhmm_em_lb.m, no derivatives)
+# lower bound (vbhmm_em_lb.m) and its hyperparameter derivatives
 # ----------------------------------------------------------------------------
-def vbhmm_em_lb(st: dict, opt: dict, vp: dict, fb: dict) -> float:
-    """vbhmm_em_lb.m:74-257 (usegroups = 0)."""
+def vbhmm_em_lb(st: dict, opt: dict, vp: dict, fb: dict, do_deriv: bool = False,
+                clipped: Optional[dict] = None):
+    """vbhmm_em_lb.m:74-257 (usegroups = 0); with ``do_deriv`` also :260-400, the
+    bound's derivatives with respect to the hyperparameters at this posterior
+    (returns (LB, dLB), dLB keyed as the reference's d_LB: d_logalpha0,
+    d_logepsilon0, d_logv0D1, d_sqrtv0D1, d_logbeta0, d_sqrtbeta0, d_sqrtW0inv,
+    d_logW0, d_m0), a derivative set to 0 where its hyperparameter is clipped and
+    moving past the limit would raise the bound."""
     dim, K = st["dim"], st["K"]
     alpha0, epsilon0, beta0, v0 = opt["alpha0"], opt["epsilon0"], opt["beta0"], opt["v0"]
     m0, W0inv = opt["mu0"], st["W0inv"]
@@ -213,7 +233,42 @@ def vbhmm_em_lb(st: dict, opt: dict, vp: dict, fb: dict) -> float:
     Lt6 = Lt2a + Lt2b + Lt63 - Lt64
     Lt7 = ((alpha - 1) * lPi).sum() + logCalpha + (((eps - 1) * lA).sum(1) + logCeps).sum()
     Lt8 = 0.5 * (lLT + dim * np.log(beta / (2 * np.pi))).sum() - 0.5 * dim * K - H
-    return float(Lt1 + Lt2 + Lt3 + Lt4 + Lt5 - Lt6 - Lt7 - Lt8)
+    LB = float(Lt1 + Lt2 + Lt3 + Lt4 + Lt5 - Lt6 - Lt7 - Lt8)
+    if not do_deriv:
+        return LB
+    # vbhmm_em_lb.m:263-320: the partial derivatives of Lt3 (alpha0), Lt4 (epsilon0)
+    # and Lt5 (v0, beta0, W0, m0) -- the only terms holding hyperparameters
+    d = {}
+    d["alpha0"] = np.atleast_1d(K * digamma(K * alpha0) - K * digamma(alpha0) + lPi.sum())
+    d["epsilon0"] = np.atleast_1d(K * (K * digamma(K * epsilon0) - K * digamma(epsilon0)) + lA.sum())
+    dlogB0_dv0 = 0.5 * logdetW0inv - (dim / 2) * np.log(2) - 0.5 * digamma(0.5 * (v0 + 1 - q)).sum()
+    d["v0"] = np.atleast_1d(K * dlogB0_dv0 + 0.5 * lLT.sum())
+    d["beta0"] = np.atleast_1d(0.5 * (dim / beta0 - dim / beta - v * mWm).sum())
+    trW = np.array([np.trace(W[k]) for k in range(K)])
+    if st["W0mode"] == "iid":
+        myW0inv = W0inv[0, 0]
+        d_trW0invW = -(myW0inv ** 2) * trW                                  # [K]
+        d["W0"] = np.atleast_1d(K * (-0.5 * v0 * dim * myW0inv) - 0.5 * (v * d_trW0invW).sum())
+    else:
+        myW0inv = np.diag(W0inv).copy()
+        d_trW0invW = -(myW0inv[:, None] ** 2) * np.stack([np.diag(W[k]) for k in range(K)], 1)  # [dim][K]
+        d["W0"] = K * (-0.5 * v0 * myW0inv) - 0.5 * (v[None, :] * d_trW0invW).sum(1)
+    myW0 = 1.0 / myW0inv
+    d["m0"] = sum(beta0 * v[k] * (W[k] @ (m[k] - m0)) for k in range(K))
+    # :326-341: a clipped hyperparameter's derivative is zeroed where moving further
+    # past its limit would raise the bound
+    for name, flags in (clipped or {}).items():
+        g = d[name]
+        for j, fl in enumerate(np.atleast_1d(flags)):
+            if (fl == +1 and g[j] > 0) or (fl == -1 and g[j] < 0):
+                g[j] = 0.0
+    # :387-398: derivatives of the transformed hyperparameters
+    dLB = dict(d_logalpha0=d["alpha0"] * alpha0, d_logepsilon0=d["epsilon0"] * epsilon0,
+               d_logv0D1=d["v0"] * (v0 - dim + 1), d_sqrtv0D1=d["v0"] * 2 * np.sqrt(v0 - dim + 1),
+               d_logbeta0=d["beta0"] * beta0, d_sqrtbeta0=d["beta0"] * 2 * np.sqrt(beta0),
+               d_sqrtW0inv=d["W0"] * (myW0 ** 1.5) * (-2), d_logW0=d["W0"] * myW0,
+               d_m0=np.asarray(d["m0"], dtype=np.float64))
+    return LB, dLB
 
 
 # ----------------------------------------------------------------------------
@@ -222,13 +277,14 @@ def vbhmm_em_lb(st: dict, opt: dict, vp: dict, fb: dict) -> float:
 def vbhmm_em(data: Sequence[np.ndarray], K: int, opt: dict, gmm: Optional[dict] = None,
              rng: Optional[np.random.Generator] = None, device="cuda",
              batch: Optional["vbhmm.SequenceBatch"] = None) -> dict:
-    """vbhmm_em.m:1-491 (usegroups = 0, no derivatives): EM from the posterior
-    vbhmm_init builds out of ``gmm`` (or a 'random' GMM drawn with ``rng``).
-    Returns the output HMM (prior, trans, pdf, LL, gamma, M, N1, N, varpar)
-    plus the bound trajectory ``LLs``."""
+    """vbhmm_em.m:1-491 (usegroups = 0): EM from the posterior vbhmm_init builds
+    out of ``gmm`` (or a 'random' GMM drawn with ``rng``; or opt['inithmm'] when
+    opt['initmode'] == 'inithmm').  Returns the output HMM (prior, trans, pdf, LL,
+    gamma, M, N1, N, varpar) plus the bound trajectory ``LLs``, and with
+    opt['calc_LLderiv'] the bound's hyperparameter derivatives ``dLL``."""
     data = [np.asarray(a, dtype=np.float64).reshape(-1, len(opt["mu0"])) for a in data]
     opt, clipped = vbhmm_clip_hyps(opt)
-    if gmm is None:
+    if gmm is None and opt.get("initmode") != "inithmm":
         gmm = random_gmm(data, K, rng if rng is not None else np.random.default_rng(0))
     mix = vbhmm_init(data, K, opt, gmm)
     dim = len(opt["mu0"])
@@ -243,6 +299,7 @@ def vbhmm_em(data: Sequence[np.ndarray], K: int, opt: dict, gmm: Optional[dict] 
     W0inv = mix["W0inv"]
     L = lastL = -np.finfo(float).max
     LLs: List[float] = []
+    dLL = None
     C = np.zeros((K, dim, dim))
     unstable = False
     for it in range(1, int(opt["maxIter"]) + 1):
@@ -271,6 +328,12 @@ def vbhmm_em(data: Sequence[np.ndarray], K: int, opt: dict, gmm: Optional[dict] 
         if np.isnan(L):  # vbhmm_em.m:314-330
             do_break, unstable, L = True, True, -np.inf
         LLs.append(L)
+        if do_break and opt.get("calc_LLderiv", 0):
+            # vbhmm_em.m:332-343: the derivatives at the last E-step, before its M-step
+            # (NaN when the run went unstable)
+            _, dLL = vbhmm_em_lb(st, opt, vp, fb, do_deriv=True, clipped=clipped)
+            if unstable:
+                dLL = {k: np.full_like(np.asarray(g, dtype=float), np.nan) for k, g in dLL.items()}
         if do_break and unstable:
             break
         # M-step (vbhmm_em.m:352-408)
@@ -301,15 +364,108 @@ def vbhmm_em(data: Sequence[np.ndarray], K: int, opt: dict, gmm: Optional[dict] 
                 LL=float(L), LLs=np.array(LLs), iters=it, unstable=unstable,
                 gamma=[g_all[:, n, :lens[n]].copy() for n in range(N)], M=M, N1=Nk1, N=Nk,
                 varpar=dict(epsilon=eps, alpha=alpha, beta=beta, v=v, m=m, W=W.copy()),
-                clipped=clipped)
+                clipped=clipped, dLL=dLL)
+
+
+# ----------------------------------------------------------------------------
+# hyperparameter learning (vbhmm_em_hyp.m, get_hypinfo.m, uniqueLL.m)
+# ----------------------------------------------------------------------------
+VBHMM_HYPS = ("alpha0", "epsilon0", "v0", "beta0", "W0", "mu0")
+
+
+def vbhmm_hypinfo(learn_hyps, opt: dict) -> list:
+    """get_hypinfo.m:13-79: per learnable hyperparameter its optimiser-space
+    transform, inverse, derivative key and size ('W0' = the sqrt(W0inv) transform)."""
+    from .hyp import HypInfo
+    dim = len(opt["mu0"])
+    names = VBHMM_HYPS if (learn_hyps is True or (np.isscalar(learn_hyps) and learn_hyps == 1)) \
+        else tuple(learn_hyps)
+    out = []
+    for h in names:
+        if h in ("alpha0", "epsilon0", "beta0"):
+            out.append(HypInfo(h, "d_log" + h, np.exp, np.log, 1))
+        elif h == "v0":
+            out.append(HypInfo("v0", "d_logv0D1", lambda x: np.exp(x) + dim - 1,
+                               lambda x: np.log(x - dim + 1), 1))
+        elif h in ("W0", "W0isqrt"):
+            out.append(HypInfo("W0", "d_sqrtW0inv", lambda x: x ** (-2.0),
+                               lambda x: 1.0 / np.sqrt(x), int(np.size(opt["W0"]))))
+        elif h == "W0log":
+            out.append(HypInfo("W0", "d_logW0", np.exp, np.log, int(np.size(opt["W0"]))))
+        elif h == "mu0":
+            out.append(HypInfo("mu0", "d_m0", lambda x: x, lambda x: x, dim))
+        else:
+            raise ValueError("bad value of learn_hyp")
+    return out
+
+
+def _set_hyps(X: np.ndarray, opt: dict, info: list) -> dict:
+    """vbhmm_em_hyp.m set_vbopt: optimiser vector -> options."""
+    o = dict(opt)
+    i = 0
+    for h in info:
+        val = np.asarray(h.trans(X[i:i + h.dims]), dtype=np.float64)
+        o[h.optname] = float(val[0]) if (h.dims == 1 and np.ndim(opt[h.optname]) == 0) else val
+        i += h.dims
+    o["mu0"] = np.asarray(o["mu0"], dtype=np.float64).reshape(-1)
+    return o
+
+
+def unique_ll(LLall: np.ndarray, diffthresh: float) -> List[int]:
+    """uniqueLL.m:40-66: the trials whose bound differs from every earlier unique
+    one by more than ``diffthresh`` relative."""
+    inds: List[int] = []
+    for it, ll in enumerate(np.asarray(LLall, dtype=np.float64)):
+        if it == 0 or np.all(np.abs((np.asarray([LLall[j] for j in inds]) - ll) / ll) > diffthresh):
+            inds.append(it)
+    return inds
+
+
+def vbhmm_em_hyp(data: Sequence[np.ndarray], K: int, opt: dict, inithmm: dict, device="cuda",
+                 batch: Optional["vbhmm.SequenceBatch"] = None) -> dict:
+    """vbhmm_em_hyp.m:15-126: maximise the bound over the transformed
+    hyperparameters (minimize_new.m, p.length = opt['hyp_length'], BFGS by default),
+    every evaluation an EM run from ``inithmm`` with its derivatives (vbhmm_grad,
+    :172-190), then one EM run at the optimum; the result carries ``learn_hyps``
+    (hypinfo names, opt_transhyp, opt_L, the optimised hyperparameters)."""
+    from . import hyp
+    dim = len(opt["mu0"])
+    data = [np.asarray(a, dtype=np.float64).reshape(-1, dim) for a in data]
+    sb = batch if batch is not None else vbhmm.SequenceBatch(data, dim, device)
+    info = vbhmm_hypinfo(opt.get("learn_hyps", 1) or 1, opt)
+    base = dict(opt, initmode="inithmm", inithmm=inithmm)
+    n_eval = [0]
+
+    def grad(X):
+        o = _set_hyps(X, base, info)
+        o["calc_LLderiv"] = 1
+        h = vbhmm_em(data, K, o, batch=sb)
+        n_eval[0] += 1
+        return -h["LL"], np.concatenate([-np.atleast_1d(h["dLL"][i.derivname]).reshape(-1) for i in info])
+
+    methods = {"minimize-bfgs": "BFGS", "minimize-lbfgs": "LBFGS", "minimize-cg": "CG"}
+    name = opt.get("minimizer", "minimize-bfgs")
+    if name not in methods:  # 'fminunc' needs MATLAB's Optimization Toolbox
+        raise ValueError("bad minimizer specified")
+    X0 = hyp.init_x(opt, info)
+    Xopt, fX, nls = hyp.minimize(X0, grad, length=int(opt.get("hyp_length", 100)), method=methods[name])
+    o2 = _set_hyps(Xopt, base, info)
+    o2["calc_LLderiv"] = 0
+    h = vbhmm_em(data, K, o2, batch=sb)
+    h["learn_hyps"] = dict(hypinfo=[i.optname for i in info], opt_transhyp=Xopt, opt_L=-fX[-1],
+                           fX=fX, line_searches=nls, evaluations=n_eval[0],
+                           vbopt={i.optname: o2[i.optname] for i in info})
+    return h
 
 
 def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
                 gmms: Optional[dict] = None) -> dict:
-    """vbhmm_learn.m (initmode 'random', learn_hyps = 0): for each K, numtrials EM
-    runs from random GMMs (seeded by opt['seed'], vbhmm_learn.m:443-451; K = 1
-    needs one), keep the best bound; over several K, select by LL + gammaln(K+1)
-    (:367-405).  ``gmms[K]`` = list of GMMs to inject instead of random draws."""
+    """vbhmm_learn.m (initmode 'random'): for each K, numtrials EM runs from random
+    GMMs (seeded by opt['seed'], vbhmm_learn.m:443-451; K = 1 needs one); with
+    opt['learn_hyps'] every unique trial (uniqueLL, 2 minDiff 10 apart) is re-run
+    through :func:`vbhmm_em_hyp` (:482-552); keep the best bound; over several K,
+    select by LL + gammaln(K+1) (:367-405).  ``gmms[K]`` = list of GMMs to inject
+    instead of random draws."""
     Ks = [int(k) for k in np.atleast_1d(Ks)]
     dim = len(opt["mu0"])
     data = [np.asarray(a, dtype=np.float64).reshape(-1, dim) for a in data]
@@ -324,8 +480,19 @@ def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
             inits = [random_gmm(data, K, rng) for _ in range(numits)]
         trials = [vbhmm_em(data, K, opt, gmm=g, batch=sb) for g in inits]
         LLall = np.array([h["LL"] for h in trials])
-        best = trials[int(np.argmax(LLall))]
+        LLall_random, trials_random = LLall.copy(), list(trials)
+        if opt.get("learn_hyps", 0):
+            uniq = unique_ll(LLall, 2 * opt["minDiff"] * 10)
+            LLall = np.full(len(trials), np.nan)
+            for it in uniq:
+                trials[it] = vbhmm_em_hyp(data, K, opt, trials_random[it], batch=sb)
+                LLall[it] = trials[it]["LL"]
+        best = trials[int(np.nanargmax(LLall))]
         best["trials_LL"] = LLall
+        if opt.get("learn_hyps", 0):
+            best["trials_LL_random"] = LLall_random
+            if opt.get("keep_best_random_trial", 0):  # vbhmm_learn.m:587-596
+                best["learn_hyps"]["hmm_best_random_trial"] = trials_random[int(np.argmax(LLall_random))]
         out_all.append(best)
     if len(Ks) == 1:
         return out_all[0]
