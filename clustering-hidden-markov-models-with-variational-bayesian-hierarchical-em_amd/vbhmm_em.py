@@ -404,21 +404,12 @@ def _set_hyps(X: np.ndarray, opt: dict, info: list) -> dict:
     o = dict(opt)
     i = 0
     for h in info:
-        val = np.asarray(h.trans(X[i:i + h.dims]), dtype=np.float64)
+        with np.errstate(over="ignore"):  # a line-search probe may overflow; clipped later
+            val = np.asarray(h.trans(X[i:i + h.dims]), dtype=np.float64)
         o[h.optname] = float(val[0]) if (h.dims == 1 and np.ndim(opt[h.optname]) == 0) else val
         i += h.dims
     o["mu0"] = np.asarray(o["mu0"], dtype=np.float64).reshape(-1)
     return o
-
-
-def unique_ll(LLall: np.ndarray, diffthresh: float) -> List[int]:
-    """uniqueLL.m:40-66: the trials whose bound differs from every earlier unique
-    one by more than ``diffthresh`` relative."""
-    inds: List[int] = []
-    for it, ll in enumerate(np.asarray(LLall, dtype=np.float64)):
-        if it == 0 or np.all(np.abs((np.asarray([LLall[j] for j in inds]) - ll) / ll) > diffthresh):
-            inds.append(it)
-    return inds
 
 
 def vbhmm_em_hyp(data: Sequence[np.ndarray], K: int, opt: dict, inithmm: dict, device="cuda",
@@ -481,15 +472,20 @@ def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
         trials = [vbhmm_em(data, K, opt, gmm=g, batch=sb) for g in inits]
         LLall = np.array([h["LL"] for h in trials])
         LLall_random, trials_random = LLall.copy(), list(trials)
-        if opt.get("learn_hyps", 0):
+        learn = _do_learn_hyps(opt.get("learn_hyps", 0))
+        if learn or opt.get("keep_suboptimal_hmms", 0):
+            from .cluster import unique_ll   # uniqueLL.m
             uniq = unique_ll(LLall, 2 * opt["minDiff"] * 10)
+        if learn:
             LLall = np.full(len(trials), np.nan)
             for it in uniq:
                 trials[it] = vbhmm_em_hyp(data, K, opt, trials_random[it], batch=sb)
                 LLall[it] = trials[it]["LL"]
         best = trials[int(np.nanargmax(LLall))]
         best["trials_LL"] = LLall
-        if opt.get("learn_hyps", 0):
+        if opt.get("keep_suboptimal_hmms", 0):  # vbhmm_learn.m:600-602 (the random trials)
+            best["suboptimal_hmms"] = [trials_random[it] for it in uniq]
+        if learn:
             best["trials_LL_random"] = LLall_random
             if opt.get("keep_best_random_trial", 0):  # vbhmm_learn.m:587-596
                 best["learn_hyps"]["hmm_best_random_trial"] = trials_random[int(np.argmax(LLall_random))]
@@ -500,14 +496,72 @@ def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
     ind = int(np.argmax(LLk))
     h = dict(out_all[ind])
     h.update(model_LL=LLk, model_k=Ks, model_bestK=Ks[ind], model_all=out_all, LL=float(LLk[ind]))
+    if opt.get("keep_suboptimal_hmms", 0):  # :417-424: every K's unique trials
+        h["suboptimal_hmms"] = [q for o in out_all for q in o["suboptimal_hmms"]]
     return h
+
+
+def _do_learn_hyps(v) -> bool:
+    """vbhmm_learn.m:357-361: a list of names, or 1."""
+    return isinstance(v, (list, tuple)) or (np.isscalar(v) and v == 1)
 
 
 def vbhmm_learn_batch(datas: Sequence[Sequence[np.ndarray]], Ks, opt: dict, device="cuda",
                       gmms: Optional[list] = None):
-    """vbhmm_learn_batch.m: one vbhmm_learn per subject; returns (hmms, LLs)."""
-    hmms = [vbhmm_learn(d, Ks, opt, device, gmms[i] if gmms is not None else None)
-            for i, d in enumerate(datas)]
+    """vbhmm_learn_batch.m: one vbhmm_learn per subject; returns (hmms, LLs).  With
+    opt['learn_hyps_batch'] (:84-189) one set of hyperparameters shared by every
+    subject: each subject's unique random trials (keep_suboptimal_hmms) seed EM runs,
+    and BFGS (minimize_new.m, length 100) minimises the mean over subjects of the
+    best -(LL + gammaln(K+1)) among that subject's runs (vbhmm_grad_batch_parfor,
+    :347-457); the returned HMMs are the final run's, each with its ``vbopt``."""
+    lhb = opt.get("learn_hyps_batch", 0)
+    if not (isinstance(lhb, (list, tuple)) or lhb):
+        hmms = [vbhmm_learn(d, Ks, opt, device, gmms[i] if gmms is not None else None)
+                for i, d in enumerate(datas)]
+        return hmms, np.array([h["LL"] for h in hmms])
+    from . import hyp
+    if not isinstance(lhb, (list, tuple)):
+        if lhb != 1:
+            raise ValueError("learn_hyps_batch not set properly")
+        lhb = list(VBHMM_HYPS)
+    opt = dict(opt, learn_hyps=0)            # :97-101: individual learning is switched off
+    info = vbhmm_hypinfo(list(lhb), opt)
+    dim = len(opt["mu0"])
+    datas = [[np.asarray(a, dtype=np.float64).reshape(-1, dim) for a in d] for d in datas]
+    batches = [vbhmm.SequenceBatch(d, dim, device) for d in datas]
+    iopt = dict(opt, keep_suboptimal_hmms=1)
+    inithmms = [vbhmm_learn(d, Ks, iopt, device, gmms[i] if gmms is not None else None)
+                for i, d in enumerate(datas)]
+
+    def grad_batch(X, keep=False):
+        nL, dnL, out = 0.0, 0.0, []
+        for n, d in enumerate(datas):
+            o = _set_hyps(X, dict(opt, initmode="inithmm", calc_LLderiv=1), info)
+            best = None
+            for q in inithmms[n]["suboptimal_hmms"]:
+                K = len(q["pdf"])
+                qh = vbhmm_em(d, K, dict(o, inithmm=q), batch=batches[n])
+                qnL = -qh["LL"] - gammaln(K + 1)
+                if best is None or qnL < best[0]:   # MATLAB min: the first of equal values
+                    best = (qnL, qh)
+            nL += best[0]
+            dnL = dnL - np.concatenate([np.atleast_1d(best[1]["dLL"][i.derivname]).reshape(-1) for i in info])
+            if keep:
+                best[1]["vbopt"] = {i.optname: o[i.optname] for i in info}
+                out.append(best[1])
+        N = len(datas)
+        return (nL / N, dnL / N, out) if keep else (nL / N, dnL / N)
+
+    methods = {"minimize-bfgs": "BFGS", "minimize-lbfgs": "LBFGS", "minimize-cg": "CG"}
+    name = opt.get("minimizer", "minimize-bfgs")
+    if name not in methods:
+        raise ValueError("bad minimizer specified")
+    X0 = hyp.init_x(opt, info)
+    Xopt, fX, nls = hyp.minimize(X0, grad_batch, length=100, method=methods[name])
+    _, _, hmms = grad_batch(Xopt, keep=True)
+    for h in hmms:
+        h["learn_hyps_batch"] = dict(hypinfo=[i.optname for i in info], opt_transhyp=Xopt,
+                                     opt_L=-fX[-1], fX=fX, line_searches=nls)
     return hmms, np.array([h["LL"] for h in hmms])
 
 

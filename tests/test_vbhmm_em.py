@@ -113,10 +113,11 @@ def test_vbhmm_em_matches_oracle(vb, K):
 @pytest.mark.gpu
 def test_c1_demo_end_to_end(vb, vo):
     """vbdemo_face.m: 10 subjects -> vbhmm_learn_batch(K = 1:3) -> vbhem_h3m_cluster(K = 1:5,
-    S = 1:3).  The HMM stage runs without learn_hyps (vbhmm_em_hyp is outside the
-    scope table) and the clustering with the 'baseem' initialiser and 8 trials
-    per (K, S) instead of 'wtkmeans' x 50 (Statistics Toolbox); everything else
-    follows the demo's options."""
+    S = 1:3), both stages without learn_hyps so that every bound can be re-run by
+    the oracles (test_vbhmm_hyp.test_c1_demo_with_learn_hyps runs the demo with
+    it); the clustering with the 'baseem' initialiser and 8 trials per (K, S)
+    instead of 'wtkmeans' x 50 (Statistics Toolbox); everything else follows the
+    demo's options."""
     from cases import post_dict
     from vbhem_amd import cluster
     from vbhem_amd.vbhmm_em import vbhmm_learn_batch, vbhmm_remove_empty

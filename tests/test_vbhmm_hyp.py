@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 import vbhem_oracle as vo
-from test_vbhmm_em import DEMO_VBOPT, demo_subjects
+from test_vbhmm_em import DEMO_VBHEMOPT, DEMO_VBOPT, demo_subjects
 
 
 def _opts(dim=2, **over):
@@ -92,7 +92,7 @@ def test_clipped_derivative_zeroed(vb):
 
 
 def test_unique_ll(vb):
-    from vbhem_amd.vbhmm_em import unique_ll
+    from vbhem_amd.cluster import unique_ll
     LL = np.array([-1000.0, -1000.0001, -1010.0, -999.99999, -1010.00001, -1200.0])
     assert unique_ll(LL, 2e-4) == [0, 2, 5]
     assert unique_ll(LL, 0.0) == [0, 1, 2, 3, 4, 5]
@@ -157,3 +157,58 @@ def test_em_hyp_gpu_matches_cpu_fb(vb, monkeypatch):
     np.testing.assert_allclose(h_g["LL"], h_c["LL"], rtol=1e-6)
     np.testing.assert_allclose(h_g["learn_hyps"]["opt_transhyp"], h_c["learn_hyps"]["opt_transhyp"],
                                rtol=1e-3, atol=1e-3)
+
+
+def test_learn_hyps_batch_cpu(cpu_fb):
+    """vbhmm_learn_batch.m learn_hyps_batch: one hyperparameter set for all subjects."""
+    from scipy.special import gammaln
+    subs = demo_subjects()
+    datas = [subs[1], subs[4]]
+    opt = _opts(learn_hyps_batch=["alpha0", "epsilon0", "mu0"], numtrials=2, maxIter=40)
+    hmms, Ls = cpu_fb.vbhmm_learn_batch(datas, [1, 2], opt)
+    lh = hmms[0]["learn_hyps_batch"]
+    assert lh["hypinfo"] == ["alpha0", "epsilon0", "mu0"] and lh["opt_transhyp"].size == 4
+    assert lh["fX"][-1] < lh["fX"][0]                     # the shared bound went up
+    np.testing.assert_allclose(hmms[0]["vbopt"]["mu0"], hmms[1]["vbopt"]["mu0"])
+    # the optimiser's value is the mean over subjects of -(LL + gammaln(K+1))
+    nL = np.mean([-(h["LL"] + gammaln(len(h["pdf"]) + 1)) for h in hmms])
+    np.testing.assert_allclose(nL, lh["fX"][-1], rtol=1e-12)
+    np.testing.assert_allclose(Ls, [h["LL"] for h in hmms])
+    # without the shared learning the same subjects give the per-subject path
+    hmms0, _ = cpu_fb.vbhmm_learn_batch(datas, [1, 2], dict(opt, learn_hyps_batch=0))
+    assert "learn_hyps_batch" not in hmms0[0]
+
+
+@pytest.mark.gpu
+def test_c1_demo_with_learn_hyps(vb, monkeypatch):
+    """vbdemo_face.m as written (vbopt.learn_hyps = 1, K = 1:3; vbhemopt with its
+    default learn_hyps = 1, K = 1:5, S = 1:3), except 3 injected random GMMs per K
+    instead of 50 trials and 'baseem' x 8 instead of 'wtkmeans' x 50: the GPU HMM
+    stage agrees with the same run on the C forward-backward, every K's optimised
+    bound is >= its best random trial, and the learned HMMs cluster."""
+    from vbhem_amd import cluster
+    from vbhem_amd import vbhmm_em as vme
+    subjects = demo_subjects()
+    opt = _opts(learn_hyps=1, numtrials=3)
+    gmms = []
+    for i, d in enumerate(subjects):
+        rng = np.random.default_rng(1000 + i)
+        gmms.append({K: [vme.random_gmm(d, K, np.random.default_rng(int(rng.integers(1 << 30))))
+                         for _ in range(1 if K == 1 else 3)] for K in (1, 2, 3)})
+    hmms, Ls = vme.vbhmm_learn_batch(subjects, [1, 2, 3], opt, device="cuda:0", gmms=gmms)
+    assert len(hmms) == 10 and np.isfinite(Ls).all()
+    for h in hmms:
+        for o in h["model_all"]:
+            assert np.nanmax(o["trials_LL"]) >= o["trials_LL_random"].max() - 1e-9 * abs(o["LL"])
+            assert "learn_hyps" in o
+    with monkeypatch.context() as m:
+        m.setattr(vme.vbhmm, "vbhmm_fb", _cpu_fb)
+        m.setattr(vme.vbhmm, "SequenceBatch", lambda data, dim, device: None)
+        _, Ls_c = vme.vbhmm_learn_batch(subjects, [1, 2, 3], opt, gmms=gmms)
+    np.testing.assert_allclose(Ls, Ls_c, rtol=1e-6)
+    # the clustering stage as the demo writes it leaves vbhemopt.learn_hyps at its default, 1
+    hopt = dict(DEMO_VBHEMOPT, trials=8, max_iter=200, minDiff=1e-5, learn_hyps=1)
+    res = cluster.vbhem_h3m_cluster(hmms, [1, 2, 3, 4, 5], [1, 2, 3], hopt, device="cuda:0")
+    assert 1 <= res["model_bestK"] <= 5 and 1 <= res["model_bestS"] <= 3
+    assert np.isfinite(res["model_LL"]).all() and sum(res["group_size"]) == 10
+    assert res["hyp"] is not None
