@@ -415,7 +415,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.gate_cnt = cv.take<int>((size_t)w.nslab * K);
   w.list = cv.take<int>(g * K);
   w.list_tot = cv.take<int>((size_t)K);
-  w.Atg = cv.take<double>((size_t)K * S * S);
+  // A' [K][S][S], then [K][S] the row maxima of logA (fb_bwd4_kernel writes them)
+  w.Atg = cv.take<double>((size_t)K * S * S + (size_t)K * S);
   // the exact fallback's scratch last: its size does not move the hot buffers
   w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   return cv.off + 256;

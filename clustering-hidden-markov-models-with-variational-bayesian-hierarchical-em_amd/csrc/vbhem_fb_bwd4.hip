@@ -89,6 +89,19 @@
 #ifndef VBHEM_BWD4_PRIO
 #define VBHEM_BWD4_PRIO 0
 #endif
+//   VBHEM_BWD4_ETAB2    the exp table as {t, t/2} pairs (vbhem_mfma4.h exp_d2_n: one fp64
+//                       operation less per element and step); its 32 KB and the log
+//                       table's 128 KB fill the CU's 160 KB, so the cluster's row maxima of
+//                       logA (stored past A') and log pi are read from global memory.
+//                       Measured no faster (C4 1.43-1.49 vs 1.42-1.44 ms per launch, shard
+//                       0.189 vs 0.184-0.187 ms; profiles/r05am_ab_bwd4_etab2.txt): the
+//                       16-byte table reads cost what the fp64 operation saved.  A/B switch
+#ifndef VBHEM_BWD4_ETAB2
+#define VBHEM_BWD4_ETAB2 0
+#endif
+#if VBHEM_BWD4_ETAB2 && (VBHEM_BWD4_SKEW || !VBHEM_BWD4_BIGLOG || !VBHEM_BWD4_DECOUPLE)
+#error "VBHEM_BWD4_ETAB2 needs BIGLOG and DECOUPLE, without SKEW"
+#endif
 #if VBHEM_BWD4_SKEW && !(VBHEM_BWD4_QPW == 2 && VBHEM_BWD4_BIGLOG && VBHEM_BWD4_DECOUPLE)
 #error "VBHEM_BWD4_SKEW needs VBHEM_BWD4_QPW=2 with BIGLOG and DECOUPLE"
 #endif
@@ -119,7 +132,12 @@ using namespace m4;
 __global__ __launch_bounds__(64 * kNWB) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void fb_bwd4_kernel(const SplitArgs p) {
   constexpr int S = 8;
-#if VBHEM_BWD4_BIGLOG
+#if VBHEM_BWD4_ETAB2
+  // 163,840 B: all of the CU's LDS (one block per CU)
+  __shared__ __attribute__((aligned(16))) double tabs[2 * 2048 + 2 * 8192];
+  double *const etab = tabs;                 // {2^(i/2048 - 1010), half of it}
+  double *const ltab8 = tabs + 2 * 2048;     // {1/c, -log(1/c)}
+#elif VBHEM_BWD4_BIGLOG
   // one array, the exp table first: both tables' LDS offsets then fit the 16-bit
   // offset field of ds_read (no address add per lookup)
   __shared__ __attribute__((aligned(16))) double tabs[2048 + 2 * 8192];
@@ -129,9 +147,14 @@ void fb_bwd4_kernel(const SplitArgs p) {
   __shared__ __attribute__((aligned(16))) double etab[2048];      // 2^(i/2048 - 1010)
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];  // {1/(2c), -log(1/c)}
 #endif
+#if !VBHEM_BWD4_ETAB2
   __shared__ double amax[S], lpi[S];
+#endif
   const int tid = threadIdx.x;
-#if VBHEM_BWD4_BIGLOG
+#if VBHEM_BWD4_ETAB2
+  stage_etab2(etab, tid, 64 * kNWB);
+  stage_log8k(ltab8, tid, 64 * kNWB);
+#elif VBHEM_BWD4_BIGLOG
   for (int x = tid; x < 2048; x += 64 * kNWB) etab[x] = kExpTab4[x] * 0x1p-1010;
   stage_log8k(ltab8, tid, 64 * kNWB);
 #else
@@ -150,6 +173,20 @@ void fb_bwd4_kernel(const SplitArgs p) {
     t0 = bk / K;
   }
   j = __builtin_amdgcn_readfirstlane(j);
+#if VBHEM_BWD4_ETAB2
+  // the row maxima of logA in global memory past A' ([K][S] after the [K][S][S] block,
+  // every block of the cluster writing the same values), read once per tile with log pi
+  // where they are used (L1 hits; kept in registers they would spill)
+  double *const amax = const_cast<double *>(p.Atg) + (size_t)K * S * S + (size_t)j * S;
+  const double *const lpi = p.logPi + (size_t)j * S;
+  if (tid < S) {
+    const double *la = p.logA + ((size_t)j * S + tid) * S;
+    double mx = la[0];
+    for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
+    amax[tid] = mx;
+  }
+  __syncthreads();
+#else
   if (tid < S) {
     const double *la = p.logA + ((size_t)j * S + tid) * S;
     double mx = la[0];
@@ -158,6 +195,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
     lpi[tid] = p.logPi[(size_t)j * S + tid];
   }
   __syncthreads();
+#endif
 
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane >> 4, b = (lane >> 2) & 3, c = lane & 3;
@@ -335,7 +373,11 @@ void fb_bwd4_kernel(const SplitArgs p) {
       double G[kQPW][2][2];
 #if VBHEM_BWD4_DECOUPLE
       // table values first (they do not need the maxima), then the maxima chain
+#if VBHEM_BWD4_ETAB2
+      double2 tv[NE];
+#else
       double tv[NE];
+#endif
       unsigned wph[kQPW][2];
 #pragma unroll
       for (int q = 0; q < kQPW; ++q)
@@ -344,10 +386,14 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) s[q][i2][jj] = red_s(V[q][i2][jj]);
 #pragma unroll
+#if VBHEM_BWD4_ETAB2
+      for (int x = 0; x < NE; ++x) tv[x] = etab2_at(etab, s[x / 4][(x / 2) % 2][x % 2]);
+#else
       for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, s[x / 4][(x / 2) % 2][x % 2]);
+#endif
 #ifdef VBHEM_ABL_NOETAB  // ablation (timing only, wrong results): no exp table read
 #pragma unroll
-      for (int x = 0; x < NE; ++x) tv[x] = 1.0;
+      for (int x = 0; x < NE; ++x) tv[x] = {};
 #endif
 #if VBHEM_BWD4_SB
       // A/B: every exp table read issued before anything after it (no interleaving that
@@ -372,7 +418,11 @@ void fb_bwd4_kernel(const SplitArgs p) {
           sf[x] = s[x / 4][(x / 2) % 2][x % 2];
           wpf[x] = wph[x / 4][x % 2];
         }
+#if VBHEM_BWD4_ETAB2
+        exp_d2_n<NE>(gg, vv, sf, tv, wpf);
+#else
         exp_d_n<NE>(gg, vv, sf, tv, wpf);
+#endif
 #pragma unroll
         for (int x = 0; x < NE; ++x) G[x / 4][(x / 2) % 2][x % 2] = gg[x];
       }
@@ -483,7 +533,11 @@ void fb_bwd4_kernel(const SplitArgs p) {
         const double sf[4] = {s[0][0], s[0][1], s[1][0], s[1][1]};
         const unsigned wpf[4] = {wp[0], wp[1], wp[0], wp[1]};
         double ef[4];
+#if VBHEM_BWD4_ETAB2
+        exp_m2_n<4>(ef, wf, sf, wpf, etab);
+#else
         exp_m_n<4>(ef, wf, sf, wpf, etab);
+#endif
         ev[0][0] = ef[0]; ev[0][1] = ef[1]; ev[1][0] = ef[2]; ev[1][1] = ef[3];
       }
       // row r: column 4 (r & 1) + c, the layout of w

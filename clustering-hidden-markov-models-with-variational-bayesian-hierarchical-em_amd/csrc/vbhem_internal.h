@@ -262,7 +262,8 @@ struct SplitArgs {
   int *flag_count, *flag_list;
   const int *list, *list_tot;  // kFbList: gated bases per cluster (gate_list_kernel)
   int list_cap;
-  const double *Atg;           // kFbBackward, LPC 1: [K][S][S] A' (emission_prep_kernel)
+  const double *Atg;           // kFbBackward, LPC 1: [K][S][S] A' (emission_prep_kernel),
+                               // then [K][S] room for fb_bwd4_kernel's logA row maxima
   // K1 inside the recursion kernel (eU set; fb_bwd2_kernel and fb_split_kernel's list
   // mode, for a short GEMM inner dimension, kdp <= kK1InKernelMaxKdp): E = bias' + W'^T u
   // per entry from the prepared operand U (u_prep layout, tile 0 at column e_col0,

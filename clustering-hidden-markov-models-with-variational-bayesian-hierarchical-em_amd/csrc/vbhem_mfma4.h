@@ -279,5 +279,58 @@ __device__ __forceinline__ double etab_at(const double *etab, double s) {
       __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & 0x3ff8u), 8));
 }
 
+// ---- the paired exp table {t, t/2} (t = 2^(i/2048 - 1010)): exp(r) t to second order
+// as t + r (t + (t/2) r), two fp64 operations after the range reduction instead of three
+// (0.5 r, r + r^2/2, t + t (r + r^2/2)); one 16-byte LDS read per element, as the log's
+__device__ __forceinline__ double2 etab2_at(const double *etab2, double s) {
+  return *reinterpret_cast<const double2 *>(
+      __builtin_assume_aligned(reinterpret_cast<const char *>(etab2) + ((lo_u(s) << 4) & 0x7ff0u), 16));
+}
+template <int N>
+__device__ __forceinline__ void exp_d2_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
+                                         const double2 (&t)[N], const unsigned (&wph)[N]) {
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
+    const double m = fma(fma(t[x].y, r, t[x].x), r, t[x].x);
+    unsigned e = __builtin_elementwise_sub_sat(lo_u(s[x]) >> 11, wph[x]);
+    asm("" : "+v"(e));
+    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
+  }
+}
+// exp_m_n on the paired table (the termination's exps)
+template <int N>
+__device__ __forceinline__ void exp_m2_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
+                                         const unsigned (&wp)[N], const double *etab2) {
+  double2 t[N];
+  unsigned d[N];
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    d[x] = __builtin_elementwise_sub_sat(lo_u(s[x]), wp[x]);
+    t[x] = *reinterpret_cast<const double2 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(etab2) + ((d[x] << 4) & 0x7ff0u), 16));
+  }
+#pragma unroll
+  for (int x = 0; x < N; ++x) {
+    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
+    const double m = fma(fma(t[x].y, r, t[x].x), r, t[x].x);
+    unsigned e = d[x] >> 11;
+    asm("" : "+v"(e));
+    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
+  }
+}
+__device__ __forceinline__ void stage_etab2(double *etab2, int tid, int nt) {
+  for (int x = tid; x < 2048; x += nt) {
+    const double t = kExpTab4[x] * 0x1p-1010;
+    etab2[2 * x] = t;
+    etab2[2 * x + 1] = 0.5 * t;
+  }
+}
+// a wave-uniform double from lane l (an SGPR pair)
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+
 }  // namespace m4
 }  // namespace vbhem
