@@ -13,11 +13,13 @@
 * :func:`unique_ll` -- src/util/uniqueLL.m; :func:`form_groups` --
   form_outputH3M.m:50-60 (label, groups, group_size).
 
-Initialisation: the reference's default init modes are 'baseem', 'gmmNew'
-and 'wtkmeans' (auto mode); 'gmmNew'/'wtkmeans' need the Statistics Toolbox
-(out of scope).  Every trial here is the 'baseem' restatement
-(vbhemhmm_init.m:58-100) with its draws from a numpy generator seeded by
-seed + trial (vbhem_h3m_c.m:32-38 seeds MATLAB's twister the same way).
+Initialisation (opt['initmode']): 'baseem' (the default here; vbhemhmm_init.m:58-100)
+with its draws from a numpy generator seeded by seed + trial (vbhem_h3m_c.m:32-38
+seeds MATLAB's twister the same way), 'wtkmeans' (vbhemhmm_init.m:294-425:
+weighted k-means of the base states' means, h3m.wtkmeans_init; MATLAB's kmeans
+replaced by a k-means++ stand-in), or 'auto' (vbhem_h3m_cluster.m:359-395: each of
+them, the best bound wins).  'gmmNew' needs the Statistics Toolbox's gmdistribution
+(out of scope).
 """
 from __future__ import annotations
 
@@ -30,7 +32,7 @@ from scipy.special import gammaln
 from . import em
 from .estep import EStepEngine
 from .h3m import (COV_FULL, BaseSet, baseem_draws, baseem_init, default_options, hmms_to_h3m_hem,
-                  hmms_to_h3m_hem_device)
+                  hmms_to_h3m_hem_device, wtkmeans_init, wtkmeans_points)
 
 
 def unique_ll(LLall: Sequence[float], diffthresh: float) -> List[int]:
@@ -72,9 +74,17 @@ def vbhem_h3m_c(base: BaseSet, opt: dict, device="cuda", engine_factory=None,
     K, S, R = int(opt["K"]), int(opt["S"]), int(opt.get("trials", 100))
     make = engine_factory or _device_engine(device)
     posts = []
+    initmode = opt.get("initmode", "baseem")
+    if initmode not in ("baseem", "wtkmeans"):
+        raise ValueError(f"initmode {initmode!r}: 'baseem' or 'wtkmeans' ('gmmNew' needs the "
+                         "Statistics Toolbox)")
+    pts = wtkmeans_points(base, opt.get("initopt_mode", "r0")) if initmode == "wtkmeans" else None
     for it in range(1, R + 1):
-        rb, rg, om = baseem_draws(base, K, S, seed=int(opt["seed"]) + it)
-        posts.append(baseem_init(base, opt, rb, rg, om))
+        if initmode == "wtkmeans":  # vbhem_h3m_c.m:52-54: wtseed = seed + trial
+            posts.append(wtkmeans_init(base, opt, int(opt["seed"]) + it, pts))
+        else:
+            rb, rg, om = baseem_draws(base, K, S, seed=int(opt["seed"]) + it)
+            posts.append(baseem_init(base, opt, rb, rg, om))
     results, LLs = [], []
     if S <= 16 and base.SB <= S:
         per = max(1, 256 // K)
@@ -155,4 +165,13 @@ def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda
         return h
     o = default_options(Ks[0], Ss[0], base.d, **{k: v for k, v in opt.items()
                                                   if k not in ("K", "S")})
+    if o.get("initmode") == "auto":
+        # vbhem_h3m_cluster.m:359-395: every initialisation in turn, the best bound wins
+        # ('gmmNew' of the reference's list needs the Statistics Toolbox: out of scope)
+        modes = list(o.get("initmodes", ["baseem", "wtkmeans"]))
+        runs = [vbhem_h3m_c(base, dict(o, initmode=m), device, engine_factory) for m in modes]
+        ind = int(np.argmax([r["LL"] for r in runs]))
+        out = dict(runs[ind])
+        out.update(initmode=modes[ind], init_trials_LL=[r["LL"] for r in runs])
+        return out
     return vbhem_h3m_c(base, o, device, engine_factory)

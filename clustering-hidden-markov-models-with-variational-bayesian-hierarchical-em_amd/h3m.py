@@ -290,6 +290,206 @@ def baseem_draws(base: BaseSet, K: int, S: int, seed: int):
 
 
 # ----------------------------------------------------------------------------
+# 'wtkmeans' initialisation (vbhemhmm_init.m:294-425, my_weighted_kmeans.m)
+# ----------------------------------------------------------------------------
+def make_gmm_weights(p: np.ndarray, A: np.ndarray, mode: str) -> np.ndarray:
+    """vbhemhmm_init.m makeGMMweights (:1109-1135): a base HMM's state weights."""
+    p = np.asarray(p, dtype=float).reshape(-1)
+    if "0" in mode:
+        for _ in range(50):
+            p = p @ A
+        return p
+    if "3" in mode:
+        out = p.copy()
+        for _ in range(2):
+            p = p @ A
+            out = out + p
+        return out / 3.0
+    if "x" in mode:
+        return np.full(p.size, 1.0 / p.size)
+    raise ValueError("unknown mode")
+
+
+def make_a_prior(N: int, mode: str, rng: np.random.Generator):
+    """vbhemhmm_init.m makeAprior (:1138-1150): uniform ('u') or random ('r') prior / A."""
+    if "u" in mode:
+        return np.full(N, 1.0 / N), np.full((N, N), 1.0 / N)
+    if "r" in mode:
+        prior = rng.random(N)
+        prior = prior / prior.sum()
+        A = rng.random((N, N))
+        return prior, A / A.sum(1, keepdims=True)
+    raise ValueError("unknown mode")
+
+
+def _wk_centroids(point, cluster, weight, K):
+    """my_weighted_kmeans.m gcentroids: weighted centres (zero for a weightless cluster)."""
+    cen = np.zeros((K, point.shape[1]))
+    cw = np.zeros(K)
+    for j in range(K):
+        mem = cluster == j
+        cw[j] = weight[mem].sum()
+        cen[j] = (point[mem] * weight[mem, None]).sum(0)
+        if cw[j] > 0:
+            cen[j] = cen[j] / cw[j]
+    return cen, cw
+
+
+def _wk_energy(point, weight, cen, cw, cluster):
+    """my_weighted_kmeans.m genergy: member distances scaled by cw / (cw - w)."""
+    f = np.zeros(point.shape[0])
+    energy = np.zeros(cen.shape[0])
+    with np.errstate(divide="ignore", invalid="ignore"):  # MATLAB: x/0 = Inf, 0/0 = NaN
+        for j in range(cen.shape[0]):
+            mem = cluster == j
+            fm = ((point[mem] - cen[j]) ** 2).sum(1)
+            energy[j] = (weight[mem] * fm).sum()
+            f[mem] = fm * cw[j] / (cw[j] - weight[mem])
+    return f, energy
+
+
+def _nanargmin0(fmat: np.ndarray) -> np.ndarray:
+    """MATLAB min(x, [], 1): NaN skipped, the first of equal minima; all-NaN -> 1st."""
+    x = np.where(np.isnan(fmat), np.inf, fmat)
+    return np.argmin(x, axis=0)
+
+
+def weighted_kmeans(K: int, it_max: int, point: np.ndarray, weight: np.ndarray,
+                    centres: np.ndarray):
+    """my_weighted_kmeans.m: points [n][dim] with weights [n] from initial centres
+    [K][dim]; returns (0-based cluster [n], centres [K][dim], energies)."""
+    point = np.asarray(point, dtype=float)
+    weight = np.asarray(weight, dtype=float).reshape(-1)
+    cen = np.asarray(centres, dtype=float)
+    d2 = ((point[None, :, :] - cen[:, None, :]) ** 2).sum(2)          # [K][n]
+    cluster = _nanargmin0(d2)
+    cen, cw = _wk_centroids(point, cluster, weight, K)
+    f, energy = _wk_energy(point, weight, cen, cw, cluster)
+    old = energy.sum()
+    energies = [old]
+    it = 0
+    while it < it_max:
+        fmat = np.zeros((K, point.shape[0]))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            for j in range(K):
+                mem = cluster == j
+                fmat[j, mem] = f[mem]
+                non = ~mem
+                adj = cw[j] / (cw[j] + weight[non])
+                fmat[j, non] = ((point[non] - cen[j]) ** 2).sum(1) * adj
+        cluster = _nanargmin0(fmat)
+        cen, cw = _wk_centroids(point, cluster, weight, K)
+        f, energy = _wk_energy(point, weight, cen, cw, cluster)
+        new = energy.sum()
+        if abs(new - old) < 1e-6:
+            break
+        old = new
+        it += 1
+        energies.append(new)
+    return cluster, cen, np.array(energies)
+
+
+def kmeans_pp(X: np.ndarray, k: int, rng: np.random.Generator, max_iter: int = 100) -> np.ndarray:
+    """Stand-in for MATLAB's kmeans(X, k, 'Replicates', 1) (Statistics Toolbox, absent):
+    k-means++ seeding from ``rng``, then batch (Lloyd) updates, an emptied cluster
+    re-seeded with the point farthest from its centre ('singleton').  Its draws are not
+    MATLAB's twister stream, so the centres are not the reference's: parity unpinned."""
+    X = np.asarray(X, dtype=float)
+    n = X.shape[0]
+    cen = np.empty((k, X.shape[1]))
+    cen[0] = X[rng.integers(n)]
+    d2 = ((X - cen[0]) ** 2).sum(1)
+    for c in range(1, k):
+        tot = d2.sum()
+        i = rng.choice(n, p=d2 / tot) if tot > 0 else rng.integers(n)
+        cen[c] = X[i]
+        d2 = np.minimum(d2, ((X - cen[c]) ** 2).sum(1))
+    lab = None
+    for _ in range(max_iter):
+        dist = ((X[None, :, :] - cen[:, None, :]) ** 2).sum(2)
+        new = np.argmin(dist, axis=0)
+        if lab is not None and np.array_equal(new, lab):
+            break
+        lab = new
+        for c in range(k):
+            mem = lab == c
+            if mem.any():
+                cen[c] = X[mem].mean(0)
+            else:
+                far = int(np.argmax(dist[lab, np.arange(n)]))
+                cen[c] = X[far]
+                lab[far] = c
+    return cen
+
+
+def wtkmeans_points(base: BaseSet, mode: str = "r0"):
+    """vbhemhmm_init.m:296-323: every base state's mean [n][d] and its normalised
+    weight [n] (makeGMMweights of its HMM), plus the first base state's covariance."""
+    bn = base.numpy()
+    ns = bn["nstates"]
+    pts, w = [], []
+    for i in range(base.N):
+        m = int(ns[i])
+        pts.append(bn["centres"][i, :m])
+        w.append(make_gmm_weights(bn["prior"][i, :m], bn["A"][i, :m, :m], mode))
+    wv = np.concatenate(w)
+    return np.concatenate(pts, 0), wv / wv.sum(), bn["covars"][0, 0]
+
+
+def wtkmeans_init(base: BaseSet, opt: dict, wtseed: int, points=None) -> Posterior:
+    """'wtkmeans' initialisation (vbhemhmm_init.m:294-425, initopt.mode 'r0' by default,
+    ``points`` = :func:`wtkmeans_points` computed once for all trials;
+    vbhem_h3m_cluster.m:213-221): every base state's mean, weighted by its HMM's
+    50-step state distribution (makeGMMweights), is clustered into K groups (k-means
+    seed, then my_weighted_kmeans); each group's means into S state centres (k-means, or
+    the means themselves padded with the first when there are at most S); random prior /
+    A per cluster (makeAprior 'r'); counts NJ = (Nv Kb) Kb / K as the reference computes
+    them (:386).  MATLAB's kmeans and twister draws are replaced by :func:`kmeans_pp` on
+    numpy generators seeded with wtseed and wtseed + 1 (vbhem_h3m_c.m:53 sets wtseed =
+    seed + trial): parity of the centres is unpinned, the construction around them
+    follows the reference."""
+    opt = clip_hyps(opt)
+    mode = opt.get("initopt_mode", "r0")
+    K, S = opt["K"], opt["S"]
+    Kb, d = base.N, base.d
+    mumtx, alpha_w, c11 = points if points is not None else wtkmeans_points(base, mode)
+    g1 = np.random.Generator(np.random.PCG64(wtseed))
+    init_c = kmeans_pp(mumtx, K, g1)
+    cluster, _, _ = weighted_kmeans(K, 100, mumtx, alpha_w, init_c)
+    centres = [None] * K
+    g2 = g1
+    for i in range(K):
+        mi = mumtx[cluster == i]
+        if mi.shape[0] == 0:
+            continue
+        if mi.shape[0] <= S:
+            centres[i] = np.concatenate([mi, np.repeat(mi[:1], S - mi.shape[0], 0)], 0)
+        else:
+            g2 = np.random.Generator(np.random.PCG64(wtseed + 1))
+            centres[i] = kmeans_pp(mi, S, g2)
+    first = next(i for i in range(K) if centres[i] is not None)
+    centres = [c if c is not None else centres[first] for c in centres]
+    Nv = opt["Nv"] * Kb
+    NJ = Nv * Kb / K
+    nsj = NJ / S
+    eta = np.empty((K, S))
+    eps = np.empty((K, S, S))
+    for j in range(K):
+        prior, A = make_a_prior(S, mode, g2)
+        eta[j] = prior * NJ + opt["eta0"]
+        eps[j] = A * NJ + opt["epsilon0"]
+    v = np.full((K, S), opt["v0"] + nsj + 1)
+    lam = np.full((K, S), opt["lambda0"] + nsj)
+    if base.covmode == COV_DIAG:
+        W = np.broadcast_to(1.0 / ((opt["v0"] + nsj + 1 - d - 1) * c11), (K, S, d)).copy()
+    else:
+        W = np.broadcast_to(np.linalg.inv((opt["v0"] + nsj + 1 - d - 1) * c11), (K, S, d, d)).copy()
+    alpha = opt["alpha0"] + NJ * np.ones(K)
+    return Posterior(alpha=alpha, eta=eta, epsilon=eps, lam=lam, v=v, m=np.stack(centres), W=W,
+                     W0mode="iid" if np.size(opt["W0"]) == 1 else "diag")
+
+
+# ----------------------------------------------------------------------------
 # synthetic workloads (BASELINE.md configs; SURVEY.md section 8d)
 # ----------------------------------------------------------------------------
 CONFIGS = {

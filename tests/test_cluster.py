@@ -122,3 +122,55 @@ def test_cluster_vector_k_without_opt(vb):
     with um.patch.object(cluster, "vbhem_h3m_c", fake_c):
         res = cluster.vbhem_h3m_cluster(None, [1, 2], 2, None, base=base)
     assert calls == [(1, 2), (2, 2)] and res["model_bestK"] in (1, 2)
+
+
+def test_weighted_kmeans_vs_loop_restatement(vb):
+    """h3m.weighted_kmeans against oracle/wtkmeans_oracle.py (my_weighted_kmeans.m in
+    loops): the same assignments, centres to 1e-12."""
+    import wtkmeans_oracle as wo
+    rng = np.random.default_rng(3)
+    for K, n in ((2, 30), (3, 45), (4, 60)):
+        pts = np.concatenate([rng.normal(loc, 0.7, (n // K, 2)) for loc in rng.uniform(-6, 6, (K, 2))])
+        w = rng.uniform(0.1, 1.0, pts.shape[0])
+        init = pts[rng.choice(pts.shape[0], K, replace=False)]
+        got_c, got_cen, _ = vb.weighted_kmeans(K, 100, pts, w / w.sum(), init)
+        ref_c, ref_cen = wo.weighted_kmeans(K, 100, pts.tolist(), (w / w.sum()).tolist(), init.tolist())
+        assert got_c.tolist() == ref_c
+        np.testing.assert_allclose(got_cen, np.array(ref_cen), rtol=1e-12, atol=1e-12)
+
+
+def test_wtkmeans_init_structure(vb):
+    """vbhemhmm_init.m:294-425 around the k-means centres: counts NJ = (Nv Kb) Kb / K,
+    one W for every state, prior / A rows summing to NJ plus the pseudo-counts, and
+    state centres drawn from the base means of well separated groups."""
+    base = _exprmt1(vb, N=16)
+    o = vb.default_options(2, 2, 2, **dict(OPT, initmode="wtkmeans"))
+    P = vb.wtkmeans_init(base, o, 1005)
+    Kb, NJ = base.N, o["Nv"] * base.N * base.N / 2
+    np.testing.assert_allclose(P.alpha, o["alpha0"] + NJ)
+    np.testing.assert_allclose(P.eta.sum(1), NJ + 2 * o["eta0"])
+    np.testing.assert_allclose(P.epsilon.sum(2), NJ + 2 * o["epsilon0"])
+    np.testing.assert_allclose(P.v, o["v0"] + NJ / 2 + 1)
+    np.testing.assert_allclose(P.lam, o["lambda0"] + NJ / 2)
+    W11 = np.linalg.inv((o["v0"] + NJ / 2 + 1 - 3) * base.covars[0, 0].numpy())
+    np.testing.assert_allclose(P.W, np.broadcast_to(W11, P.W.shape))
+    # exprmt1: ground-truth means {0, 3}; each cluster's centres sit near one of them
+    cm = np.sort(P.m.mean(1)[:, 0])
+    np.testing.assert_allclose(cm, [0.0, 3.0], atol=0.5)
+    # deterministic in the seed
+    np.testing.assert_array_equal(vb.wtkmeans_init(base, o, 1005).m, P.m)
+
+
+def test_cluster_wtkmeans_and_auto(vb):
+    from vbhem_amd import cluster
+    base = _exprmt1(vb, N=12)
+    o = vb.default_options(2, 2, 2, **dict(OPT, initmode="wtkmeans", trials=3, max_iter=20))
+    r = cluster.vbhem_h3m_c(base, o, engine_factory=_factory)
+    assert np.isfinite(r["LLall"]).all() and r["LL"] == max(r["LLall"])
+    d = np.diff(r["result"].LogLs)
+    assert (d >= -1e-9 * np.abs(r["result"].LogLs[1:])).all()
+    auto = cluster.vbhem_h3m_cluster(None, 2, 2, dict(OPT, initmode="auto", trials=3, max_iter=20),
+                                     base=base, engine_factory=_factory)
+    assert auto["initmode"] in ("baseem", "wtkmeans")
+    assert auto["LL"] == max(auto["init_trials_LL"])
+    np.testing.assert_allclose(auto["init_trials_LL"][1], r["LL"], rtol=1e-12)

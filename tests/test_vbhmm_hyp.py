@@ -181,11 +181,11 @@ def test_learn_hyps_batch_cpu(cpu_fb):
 
 @pytest.mark.gpu
 def test_c1_demo_with_learn_hyps(vb, monkeypatch):
-    """vbdemo_face.m as written (vbopt.learn_hyps = 1, K = 1:3; vbhemopt with its
-    default learn_hyps = 1, K = 1:5, S = 1:3), except 3 injected random GMMs per K
-    instead of 50 trials and 'baseem' x 8 instead of 'wtkmeans' x 50: the GPU HMM
-    stage agrees with the same run on the C forward-backward, every K's optimised
-    bound is >= its best random trial, and the learned HMMs cluster."""
+    """vbdemo_face.m as written (vbopt.learn_hyps = 1, K = 1:3; vbhemopt 'wtkmeans' x 50
+    with its default learn_hyps = 1, K = 1:5, S = 1:3), except 3 injected random GMMs per
+    K instead of 50 trials in the HMM stage and the k-means stand-in inside 'wtkmeans':
+    the GPU HMM stage agrees with the same run on the C forward-backward, every K's
+    optimised bound is >= its best random trial, and the learned HMMs cluster."""
     from vbhem_amd import cluster
     from vbhem_amd import vbhmm_em as vme
     subjects = demo_subjects()
@@ -206,8 +206,10 @@ def test_c1_demo_with_learn_hyps(vb, monkeypatch):
         m.setattr(vme.vbhmm, "SequenceBatch", lambda data, dim, device: None)
         _, Ls_c = vme.vbhmm_learn_batch(subjects, [1, 2, 3], opt, gmms=gmms)
     np.testing.assert_allclose(Ls, Ls_c, rtol=1e-6)
-    # the clustering stage as the demo writes it leaves vbhemopt.learn_hyps at its default, 1
-    hopt = dict(DEMO_VBHEMOPT, trials=8, max_iter=200, minDiff=1e-5, learn_hyps=1)
+    # the clustering stage as the demo writes it: 'wtkmeans' x 50 trials, vbhemopt.learn_hyps
+    # left at its default, 1
+    hopt = dict(DEMO_VBHEMOPT, initmode="wtkmeans", trials=50, max_iter=200, minDiff=1e-5,
+                learn_hyps=1)
     res = cluster.vbhem_h3m_cluster(hmms, [1, 2, 3, 4, 5], [1, 2, 3], hopt, device="cuda:0")
     assert 1 <= res["model_bestK"] <= 5 and 1 <= res["model_bestS"] <= 3
     assert np.isfinite(res["model_LL"]).all() and sum(res["group_size"]) == 10
