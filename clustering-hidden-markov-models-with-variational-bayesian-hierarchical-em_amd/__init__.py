@@ -6,7 +6,8 @@ helper ``pkgload.load()`` (registers it as ``vbhem_amd``).
 """
 from .h3m import (COV_DIAG, COV_FULL, CONFIGS, BaseSet, Posterior, baseem_draws,  # noqa: F401
                   baseem_init, clip_hyps, default_options, hmms_to_h3m_hem, synth_base_set,
-                  synth_workload, weighted_kmeans, wtkmeans_init, wtkmeans_points)
+                  synth_workload, weighted_kmeans, wtkmeans_init, wtkmeans_points,
+                  gmm_mix_hier_em, gmmnew_init)
 from . import host  # noqa: F401
 
 __version__ = "0.1.0"

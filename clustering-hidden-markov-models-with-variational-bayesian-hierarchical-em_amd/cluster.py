@@ -17,9 +17,9 @@ Initialisation (opt['initmode']): 'baseem' (the default here; vbhemhmm_init.m:58
 with its draws from a numpy generator seeded by seed + trial (vbhem_h3m_c.m:32-38
 seeds MATLAB's twister the same way), 'wtkmeans' (vbhemhmm_init.m:294-425:
 weighted k-means of the base states' means, h3m.wtkmeans_init; MATLAB's kmeans
-replaced by a k-means++ stand-in), or 'auto' (vbhem_h3m_cluster.m:359-395: each of
-them, the best bound wins).  'gmmNew' needs the Statistics Toolbox's gmdistribution
-(out of scope).
+replaced by a k-means++ stand-in), 'gmmNew' (vbhemhmm_init.m:103-293: the base
+Gaussians reduced by hierarchical EM, GMM_MixHierEM.m, h3m.gmmnew_init), or 'auto'
+(vbhem_h3m_cluster.m:359-395: each of the three, the best bound wins).
 """
 from __future__ import annotations
 
@@ -32,7 +32,7 @@ from scipy.special import gammaln
 from . import em
 from .estep import EStepEngine
 from .h3m import (COV_FULL, BaseSet, baseem_draws, baseem_init, default_options, hmms_to_h3m_hem,
-                  hmms_to_h3m_hem_device, wtkmeans_init, wtkmeans_points)
+                  hmms_to_h3m_hem_device, gmmnew_init, wtkmeans_init, wtkmeans_points)
 
 
 def unique_ll(LLall: Sequence[float], diffthresh: float) -> List[int]:
@@ -75,13 +75,19 @@ def vbhem_h3m_c(base: BaseSet, opt: dict, device="cuda", engine_factory=None,
     make = engine_factory or _device_engine(device)
     posts = []
     initmode = opt.get("initmode", "baseem")
-    if initmode not in ("baseem", "wtkmeans"):
-        raise ValueError(f"initmode {initmode!r}: 'baseem' or 'wtkmeans' ('gmmNew' needs the "
-                         "Statistics Toolbox)")
+    if initmode not in ("baseem", "wtkmeans", "gmmNew"):
+        raise ValueError(f"initmode {initmode!r}: 'baseem', 'gmmNew' or 'wtkmeans'")
     pts = wtkmeans_points(base, opt.get("initopt_mode", "r0")) if initmode == "wtkmeans" else None
+    if initmode == "gmmNew":
+        bn = base.numpy()
+        ns = bn["nstates"]
+        pts = (np.concatenate([bn["centres"][i, :int(ns[i])] for i in range(base.N)]),
+               np.concatenate([bn["covars"][i, :int(ns[i])] for i in range(base.N)]))
     for it in range(1, R + 1):
         if initmode == "wtkmeans":  # vbhem_h3m_c.m:52-54: wtseed = seed + trial
             posts.append(wtkmeans_init(base, opt, int(opt["seed"]) + it, pts))
+        elif initmode == "gmmNew":  # (the trial's stream: rng(seed + trial), :32-38)
+            posts.append(gmmnew_init(base, opt, int(opt["seed"]) + it, pts))
         else:
             rb, rg, om = baseem_draws(base, K, S, seed=int(opt["seed"]) + it)
             posts.append(baseem_init(base, opt, rb, rg, om))
@@ -167,8 +173,7 @@ def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda
                                                   if k not in ("K", "S")})
     if o.get("initmode") == "auto":
         # vbhem_h3m_cluster.m:359-395: every initialisation in turn, the best bound wins
-        # ('gmmNew' of the reference's list needs the Statistics Toolbox: out of scope)
-        modes = list(o.get("initmodes", ["baseem", "wtkmeans"]))
+        modes = list(o.get("initmodes", ["baseem", "gmmNew", "wtkmeans"]))
         runs = [vbhem_h3m_c(base, dict(o, initmode=m), device, engine_factory) for m in modes]
         ind = int(np.argmax([r["LL"] for r in runs]))
         out = dict(runs[ind])

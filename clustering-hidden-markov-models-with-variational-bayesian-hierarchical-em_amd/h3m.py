@@ -490,6 +490,112 @@ def wtkmeans_init(base: BaseSet, opt: dict, wtseed: int, points=None) -> Posteri
 
 
 # ----------------------------------------------------------------------------
+# 'gmmNew' initialisation (vbhemhmm_init.m:103-293, GMM_MixHierEM.m, naiveWordMix.m)
+# ----------------------------------------------------------------------------
+def gmm_mix_hier_em(centres: np.ndarray, covars: np.ndarray, full: bool, T: int,
+                    virtual_samples: float, iterations: int, rng: np.random.Generator,
+                    init_centres: Optional[np.ndarray] = None):
+    """GMM_MixHierEM.m: the mixture of all base Gaussians (naiveWordMix: equal priors)
+    reduced to T components by hierarchical EM with ``virtual_samples`` virtual samples;
+    returns (priors [T], centres [T][d], covars [T][d][d] | [T][d], log-posteriors
+    [T][n]).  The initial centres come from :func:`kmeans_pp` (the reference's arKmeans
+    with its anchors start): parity of the result unpinned."""
+    X = np.asarray(centres, dtype=float)
+    C = np.asarray(covars, dtype=float)
+    n, dim = X.shape
+    prior = np.full(n, 1.0 / n)
+    if T == 1:
+        # (:60-73: second moments about the origin, as the reference computes them)
+        cov = (prior[:, None, None] * (X[:, :, None] * X[:, None, :] + C)).sum(0) if full \
+            else (prior[:, None] * (X ** 2 + C)).sum(0)
+        return np.ones(1), (prior @ X)[None, :], cov[None], np.zeros((1, n))
+    rng.random((T, n))                                   # (:91 post = rand(T, n): overwritten)
+    cent = kmeans_pp(X, T, rng) if init_centres is None else np.array(init_centres, dtype=float)
+    vr = np.repeat(C.mean(0)[None], T, 0) if full else np.repeat(C.max(0)[None], T, 0)
+    mxwt = np.full(T, 1.0 / T)
+    coef = -(dim / 2.0) * np.log(2 * np.pi)
+    dpp = prior * virtual_samples
+    last = -np.finfo(float).max
+    logpost = np.zeros((T, n))
+    for _ in range(int(iterations)):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            if full:
+                ivr = np.linalg.inv(vr)
+                trc = np.einsum("tab,nab->tn", ivr, C)
+                ld = np.log(np.linalg.det(vr))
+                diff = cent[:, None, :] - X[None, :, :]
+                quad = np.einsum("tna,tab,tnb->tn", diff, ivr, diff)
+                xpt = np.log(mxwt)[:, None] + dpp[None, :] * (coef - 0.5 * (trc + quad + ld[:, None]))
+            else:
+                ivr = 1.0 / vr                                   # [T][d]
+                trc = ivr @ C.T
+                nrm = (cent * cent * ivr + np.log(vr)).sum(1)
+                xpt = np.log(mxwt)[:, None] + dpp[None, :] * (
+                    coef - 0.5 * (ivr @ (X * X).T - 2 * (cent * ivr) @ X.T + nrm[:, None] + trc))
+            mv = xpt.max(0)
+            lx = mv + np.log(np.exp(xpt - mv).sum(0))
+            logpost = xpt - lx
+            post = np.exp(logpost)
+        logp = lx.mean()
+        if not np.isfinite(logp) or logp - last < 1e-6:   # (:129-141: stop, keep the last update)
+            break
+        last = logp
+        mxwt = post.mean(1)
+        wts = post * prior[None, :]
+        wts = wts / wts.sum(1, keepdims=True)
+        cent = wts @ X
+        for c in range(T):
+            dx = X - cent[c]
+            if full:
+                vr[c] = np.einsum("n,nab->ab", wts[c], dx[:, :, None] * dx[:, None, :] + C)
+            else:
+                vr[c] = wts[c] @ (dx ** 2 + C)
+    return mxwt, cent, vr, logpost
+
+
+def gmmnew_init(base: BaseSet, opt: dict, seed: int, points=None) -> Posterior:
+    """'gmmNew' initialisation (vbhemhmm_init.m:103-293, initopt.mode 'r0' by default):
+    the base states' Gaussians reduced to S components (:func:`gmm_mix_hier_em`, Nv Kb
+    virtual samples, initopt.iter = 30 iterations) shared by every cluster's states;
+    random prior / A per cluster (makeAprior) and random cluster weights omega, counts
+    Nsj = omega Nv Kb (:262-291).  ``points`` = (centres, covars) of all base states.
+    Draws from one numpy generator seeded with ``seed`` (MATLAB's twister stream in the
+    reference): parity unpinned."""
+    opt = clip_hyps(opt)
+    mode = opt.get("initopt_mode", "r0")
+    if "m" in mode:
+        raise ValueError("initopt.mode 'm' (priors from the base HMMs) is not supported for gmmNew")
+    K, S = opt["K"], opt["S"]
+    Kb, d = base.N, base.d
+    full = base.covmode == COV_FULL
+    if points is None:
+        bn = base.numpy()
+        ns = bn["nstates"]
+        points = (np.concatenate([bn["centres"][i, :int(ns[i])] for i in range(Kb)]),
+                  np.concatenate([bn["covars"][i, :int(ns[i])] for i in range(Kb)]))
+    rng = np.random.Generator(np.random.PCG64(seed))
+    Nv = opt["Nv"] * Kb
+    _, cen, cov, _ = gmm_mix_hier_em(points[0], points[1], full, S, Nv,
+                                     int(opt.get("initopt_iter", 30)), rng)
+    rng.random((K, S))                                   # (:249-250 the emissions' priors)
+    pa = [make_a_prior(S, mode, rng) for _ in range(K)]
+    omega = rng.random(K)
+    omega = omega / omega.sum()
+    Nsj = omega * Nv
+    eta = np.stack([pa[j][0] * Nsj[j] + opt["eta0"] for j in range(K)])
+    eps = np.stack([pa[j][1] * Nsj[j] + opt["epsilon0"] for j in range(K)])
+    v = opt["v0"] + Nsj[:, None] / S + 1 + np.zeros((K, S))
+    lam = opt["lambda0"] + Nsj[:, None] / S + np.zeros((K, S))
+    m = np.repeat(cen[None], K, 0)
+    if full:
+        W = np.linalg.inv((v - d - 1)[:, :, None, None] * cov[None])
+    else:
+        W = 1.0 / ((v - d - 1)[:, :, None] * cov[None])
+    return Posterior(alpha=opt["alpha0"] + Nsj, eta=eta, epsilon=eps, lam=lam, v=v, m=m, W=W,
+                     W0mode="iid" if np.size(opt["W0"]) == 1 else "diag")
+
+
+# ----------------------------------------------------------------------------
 # synthetic workloads (BASELINE.md configs; SURVEY.md section 8d)
 # ----------------------------------------------------------------------------
 CONFIGS = {

@@ -81,3 +81,54 @@ def weighted_kmeans(K, it_max, point, weight, centres):
         old = new
         it += 1
     return cluster, cen
+
+
+def hier_em_full(X, C, T, virtual_samples, iterations, cent):
+    """GMM_MixHierEM.m:90-206 (full covariance) from given initial centres, one
+    component and one point at a time (numpy only for the d x d inverse and
+    determinant); returns (priors, centres, covars)."""
+    import numpy as np
+    X = [np.asarray(x, dtype=float) for x in X]
+    C = [np.asarray(c, dtype=float) for c in C]
+    n, dim = len(X), X[0].size
+    prior = 1.0 / n
+    cent = [np.asarray(c, dtype=float) for c in cent]
+    mean_cov = sum(C) / n
+    vr = [mean_cov.copy() for _ in range(T)]
+    mxwt = [1.0 / T] * T
+    coef = -(dim / 2.0) * math.log(2 * math.pi)
+    dpp = prior * virtual_samples
+    last = -1.7976931348623157e308
+    for _ in range(iterations):
+        xpt = [[0.0] * n for _ in range(T)]
+        for t in range(T):
+            ivr = np.linalg.inv(vr[t])
+            ld = math.log(np.linalg.det(vr[t]))
+            for k in range(n):
+                tr = float((ivr * C[k]).sum())
+                df = cent[t] - X[k]
+                xpt[t][k] = math.log(mxwt[t]) + dpp * (coef - 0.5 * (tr + float(df @ ivr @ df) + ld))
+        lx = []
+        post = [[0.0] * n for _ in range(T)]
+        for k in range(n):
+            mv = max(xpt[t][k] for t in range(T))
+            s = mv + math.log(sum(math.exp(xpt[t][k] - mv) for t in range(T)))
+            lx.append(s)
+            for t in range(T):
+                post[t][k] = math.exp(xpt[t][k] - s)
+        logp = sum(lx) / n
+        if not math.isfinite(logp) or logp - last < 1e-6:
+            break
+        last = logp
+        mxwt = [sum(post[t]) / n for t in range(T)]
+        for t in range(T):
+            w = [post[t][k] * prior for k in range(n)]
+            sw = sum(w)
+            w = [x / sw for x in w]
+            cent[t] = sum(w[k] * X[k] for k in range(n))
+            acc = np.zeros((dim, dim))
+            for k in range(n):
+                df = X[k] - cent[t]
+                acc = acc + w[k] * (np.outer(df, df) + C[k])
+            vr[t] = acc
+    return mxwt, cent, vr

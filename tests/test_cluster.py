@@ -125,9 +125,9 @@ def test_cluster_vector_k_without_opt(vb):
 
 
 def test_weighted_kmeans_vs_loop_restatement(vb):
-    """h3m.weighted_kmeans against oracle/wtkmeans_oracle.py (my_weighted_kmeans.m in
+    """h3m.weighted_kmeans against oracle/h3m_init_oracle.py (my_weighted_kmeans.m in
     loops): the same assignments, centres to 1e-12."""
-    import wtkmeans_oracle as wo
+    import h3m_init_oracle as wo
     rng = np.random.default_rng(3)
     for K, n in ((2, 30), (3, 45), (4, 60)):
         pts = np.concatenate([rng.normal(loc, 0.7, (n // K, 2)) for loc in rng.uniform(-6, 6, (K, 2))])
@@ -171,6 +171,40 @@ def test_cluster_wtkmeans_and_auto(vb):
     assert (d >= -1e-9 * np.abs(r["result"].LogLs[1:])).all()
     auto = cluster.vbhem_h3m_cluster(None, 2, 2, dict(OPT, initmode="auto", trials=3, max_iter=20),
                                      base=base, engine_factory=_factory)
-    assert auto["initmode"] in ("baseem", "wtkmeans")
+    assert auto["initmode"] in ("baseem", "gmmNew", "wtkmeans")
     assert auto["LL"] == max(auto["init_trials_LL"])
+    np.testing.assert_allclose(auto["init_trials_LL"][2], r["LL"], rtol=1e-12)
+
+
+def test_hier_em_vs_loop_restatement(vb):
+    """h3m.gmm_mix_hier_em (GMM_MixHierEM.m) against the loop restatement in
+    oracle/h3m_init_oracle.py from the same initial centres (full covariance)."""
+    import h3m_init_oracle as wo
+    rng = np.random.default_rng(5)
+    X = np.concatenate([rng.normal(loc, 0.4, (8, 2)) for loc in ([0, 0], [4, 1], [1, 5])])
+    C = np.stack([(lambda a: a @ a.T + 0.2 * np.eye(2))(rng.normal(size=(2, 2)) * 0.3) for _ in X])
+    init = X[[0, 9, 17]]
+    pri, cen, cov, _ = vb.gmm_mix_hier_em(X, C, True, 3, 100.0 * 24, 30, rng, init_centres=init)
+    rp, rc, rv = wo.hier_em_full(X, C, 3, 100.0 * 24, 30, init)
+    np.testing.assert_allclose(pri, rp, rtol=1e-10)
+    np.testing.assert_allclose(cen, np.stack(rc), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(cov, np.stack(rv), rtol=1e-10, atol=1e-12)
+    # three well separated groups: the reduced components sit on them
+    np.testing.assert_allclose(np.sort(cen[:, 0]), [0, 1, 4], atol=0.4)
+
+
+def test_gmmnew_init_and_auto(vb):
+    from vbhem_amd import cluster
+    base = _exprmt1(vb, N=12)
+    o = vb.default_options(2, 2, 2, **dict(OPT, initmode="gmmNew", trials=3, max_iter=20))
+    P = vb.gmmnew_init(base, o, 1002)
+    Nv = o["Nv"] * base.N
+    np.testing.assert_allclose(P.alpha.sum(), 2 * o["alpha0"] + Nv)
+    np.testing.assert_allclose(P.m[0], P.m[1])                 # shared reduced components
+    np.testing.assert_allclose(np.sort(P.m[0][:, 0]), [0.0, 3.0], atol=0.5)
+    r = cluster.vbhem_h3m_c(base, o, engine_factory=_factory)
+    assert np.isfinite(r["LLall"]).all()
+    auto = cluster.vbhem_h3m_cluster(None, 2, 2, dict(OPT, initmode="auto", trials=3, max_iter=20),
+                                     base=base, engine_factory=_factory)
+    assert len(auto["init_trials_LL"]) == 3 and auto["LL"] == max(auto["init_trials_LL"])
     np.testing.assert_allclose(auto["init_trials_LL"][1], r["LL"], rtol=1e-12)
