@@ -140,12 +140,13 @@ def vbhem_h3m_c(base: BaseSet, opt: dict, device="cuda", engine_factory=None,
 
 def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda",
                       base: Optional[BaseSet] = None, engine_factory=None) -> dict:
-    """vbhem_h3m_cluster.m:103-402 (initmode 'baseem', full covariance,
-    use_post = 1).  ``hmms``: list of VB-HMM dicts (vbhmm_em output) or None;
+    """vbhem_h3m_cluster.m:103-402 (full covariance, use_post = 1; initmode 'auto'
+    unless opt says otherwise, as the reference).  ``hmms``: list of VB-HMM dicts (vbhmm_em output) or None;
     ``base``: an already converted h3m_b (skips the conversion)."""
     Ks = [int(k) for k in np.atleast_1d(K)]
     Ss = [int(s) for s in np.atleast_1d(S)]
     opt = dict(opt or {})
+    opt.setdefault("initmode", "auto")  # vbhem_h3m_cluster.m:165
     if base is None:
         from .vbhmm_em import vbhmm_remove_empty
         if opt.get("remove_empty", 1):

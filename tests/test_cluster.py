@@ -24,7 +24,7 @@ OPT = dict(alpha0=1e6, eta0=1.0, epsilon0=1.0, lambda0=1.0, v0=5.0, W0=1.0, m0=[
 def test_cluster_model_selection(vb):
     from vbhem_amd import cluster, em
     base = _exprmt1(vb)
-    res = cluster.vbhem_h3m_cluster(None, [1, 2], [1, 2], dict(OPT), base=base,
+    res = cluster.vbhem_h3m_cluster(None, [1, 2], [1, 2], dict(OPT, initmode="baseem"), base=base,
                                     engine_factory=_factory)
     # per-K raw bounds (each the best S of its run) + gammaln(K+1) select K
     raw = np.array([o["LL"] for o in res["model_all"]])
@@ -121,7 +121,8 @@ def test_cluster_vector_k_without_opt(vb):
     import unittest.mock as um
     with um.patch.object(cluster, "vbhem_h3m_c", fake_c):
         res = cluster.vbhem_h3m_cluster(None, [1, 2], 2, None, base=base)
-    assert calls == [(1, 2), (2, 2)] and res["model_bestK"] in (1, 2)
+    # (the default initmode 'auto': baseem, gmmNew, wtkmeans for each K)
+    assert calls == [(1, 2)] * 3 + [(2, 2)] * 3 and res["model_bestK"] in (1, 2)
 
 
 def test_weighted_kmeans_vs_loop_restatement(vb):

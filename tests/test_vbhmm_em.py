@@ -138,7 +138,7 @@ def test_c1_demo_end_to_end(vb, vo):
         ref = vho.em(subjects[i], K, opt, gmms[i][K][best])
         assert abs(h["LL"] - (ref["LL"] + gammaln(K + 1))) <= 1e-9 * abs(ref["LL"]), i
     # clustering: K = 1:5, S = 1:3 over the learned HMMs
-    hopt = dict(DEMO_VBHEMOPT, trials=8, max_iter=200, minDiff=1e-5, learn_hyps=0)
+    hopt = dict(DEMO_VBHEMOPT, initmode="baseem", trials=8, max_iter=200, minDiff=1e-5, learn_hyps=0)
     res = cluster.vbhem_h3m_cluster(hmms, [1, 2, 3, 4, 5], [1, 2, 3], hopt, device="cuda:0")
     bestK, bestS = res["model_bestK"], res["model_bestS"]
     assert 1 <= bestK <= 5 and 1 <= bestS <= 3
