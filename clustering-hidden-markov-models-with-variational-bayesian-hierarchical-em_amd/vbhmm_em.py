@@ -51,7 +51,7 @@ def vbhmm_default_options(dim: int, **over) -> dict:
     opt = dict(alpha0=0.1, mu0=defmu, W0=0.005, beta0=1.0, v0=5.0, epsilon0=0.1,
                initmode="random", numtrials=50, maxIter=100, minDiff=1e-5, seed=None,
                fix_clusters=0, fix_cov=None, verbose=0, learn_hyps=0, calc_LLderiv=0,
-               minimizer="minimize-bfgs", hyp_length=100)
+               minimizer="minimize-bfgs", hyp_length=100, sortclusters="f")
     opt["hyps_max"] = dict(alpha0=1.0686e13, epsilon0=1.0686e13, v0=1e4, beta0=1.0686e13,
                            W0=1.0686e13)
     opt["hyps_min"] = dict(alpha0=1.0686e-13, epsilon0=1.0686e-13, v0=2.0612e-09 + dim - 1,
@@ -488,7 +488,12 @@ def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
         if learn:
             best["trials_LL_random"] = LLall_random
             if opt.get("keep_best_random_trial", 0):  # vbhmm_learn.m:587-596
-                best["learn_hyps"]["hmm_best_random_trial"] = trials_random[int(np.argmax(LLall_random))]
+                tmp = trials_random[int(np.argmax(LLall_random))]
+                if opt.get("sortclusters"):
+                    tmp = vbhmm_standardize(tmp, opt["sortclusters"])
+                best["learn_hyps"]["hmm_best_random_trial"] = tmp
+        if opt.get("sortclusters"):  # vbhmm_learn.m:635-640
+            best = vbhmm_standardize(best, opt["sortclusters"])
         out_all.append(best)
     if len(Ks) == 1:
         return out_all[0]
@@ -498,7 +503,72 @@ def vbhmm_learn(data: Sequence[np.ndarray], Ks, opt: dict, device="cuda",
     h.update(model_LL=LLk, model_k=Ks, model_bestK=Ks[ind], model_all=out_all, LL=float(LLk[ind]))
     if opt.get("keep_suboptimal_hmms", 0):  # :417-424: every K's unique trials
         h["suboptimal_hmms"] = [q for o in out_all for q in o["suboptimal_hmms"]]
+    if opt.get("sortclusters"):  # :635-640 (again; idempotent for the sub-calls' order)
+        h = vbhmm_standardize(h, opt["sortclusters"])
     return h
+
+
+def vbhmm_permute(hmm: dict, cl) -> dict:
+    """vbhmm_permute.m (usegroups = 0): the states reordered by ``cl`` (0-based)."""
+    cl = np.asarray(cl, dtype=np.int64)
+    out = dict(hmm)
+    out["prior"] = np.asarray(hmm["prior"])[cl]
+    out["trans"] = np.asarray(hmm["trans"])[np.ix_(cl, cl)]
+    for k in ("M",):
+        if k in hmm:
+            out[k] = np.asarray(hmm[k])[np.ix_(cl, cl)]
+    for k in ("N1", "N"):
+        if k in hmm:
+            out[k] = np.asarray(hmm[k])[cl]
+    out["pdf"] = [hmm["pdf"][k] for k in cl]
+    if "gamma" in hmm:
+        out["gamma"] = [np.asarray(g)[cl] for g in hmm["gamma"]]
+    if "varpar" in hmm:
+        vp = hmm["varpar"]
+        out["varpar"] = dict(vp, epsilon=np.asarray(vp["epsilon"])[np.ix_(cl, cl)],
+                             alpha=np.asarray(vp["alpha"])[cl], beta=np.asarray(vp["beta"])[cl],
+                             v=np.asarray(vp["v"])[cl], m=np.asarray(vp["m"])[cl],
+                             W=np.asarray(vp["W"])[cl])
+    return out
+
+
+def vbhmm_prob_steadystate(hmm: dict) -> np.ndarray:
+    """vbhmm_prob_steadystate.m computep: the stationary distribution (least squares
+    of [A' - I; 1] p = [0; 1]), or the prior for an identity transition matrix."""
+    A = np.asarray(hmm["trans"], dtype=float)
+    d = A.shape[0]
+    if np.all(np.abs(A - np.eye(d)) < 1e-6):
+        return np.asarray(hmm["prior"], dtype=float)
+    M = np.vstack([A.T - np.eye(d), np.ones((1, d))])
+    return np.linalg.lstsq(M, np.r_[np.zeros(d), 1.0], rcond=None)[0]
+
+
+def vbhmm_standardize(hmm: dict, mode: str) -> dict:
+    """vbhmm_standardize.m: reorder the states -- 'e' (or 'd') by size N, 's' by the
+    steady-state probability, 'p' by the prior (all descending, stable), 'f' along the
+    most likely fixation path (the prior's argmax, then each row's argmax among the
+    states not visited yet), 'l' / 'r' by the first mean coordinate ascending /
+    descending."""
+    if mode in ("d", "e"):
+        wi = np.argsort(-np.asarray(hmm["N"], dtype=float), kind="stable")
+    elif mode == "s":
+        wi = np.argsort(-vbhmm_prob_steadystate(hmm), kind="stable")
+    elif mode == "p":
+        wi = np.argsort(-np.asarray(hmm["prior"], dtype=float).reshape(-1), kind="stable")
+    elif mode == "f":
+        A = np.array(hmm["trans"], dtype=float)
+        p = np.asarray(hmm["prior"], dtype=float).reshape(-1)
+        wi = []
+        for t in range(p.size):
+            cur = int(np.argmax(p)) if t == 0 else int(np.argmax(A[cur]))
+            wi.append(cur)
+            A[:, cur] = -1.0
+    elif mode in ("l", "r"):
+        x = np.array([np.asarray(q["mean"]).reshape(-1)[0] for q in hmm["pdf"]])
+        wi = np.argsort(x if mode == "l" else -x, kind="stable")
+    else:
+        raise ValueError("unknown mode")
+    return vbhmm_permute(hmm, wi)
 
 
 def _do_learn_hyps(v) -> bool:

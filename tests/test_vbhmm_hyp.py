@@ -214,3 +214,30 @@ def test_c1_demo_with_learn_hyps(vb, monkeypatch):
     assert 1 <= res["model_bestK"] <= 5 and 1 <= res["model_bestS"] <= 3
     assert np.isfinite(res["model_LL"]).all() and sum(res["group_size"]) == 10
     assert res["hyp"] is not None
+
+
+def test_vbhmm_standardize(vb):
+    """vbhmm_standardize.m / vbhmm_permute.m on a hand-made 3-state HMM."""
+    from vbhem_amd.vbhmm_em import vbhmm_permute, vbhmm_prob_steadystate, vbhmm_standardize
+    hmm = dict(prior=np.array([0.2, 0.5, 0.3]), trans=np.array([[0.1, 0.2, 0.7], [0.6, 0.1, 0.3],
+                                                                   [0.3, 0.6, 0.1]]),
+               N=np.array([5.0, 9.0, 7.0]), N1=np.array([1.0, 2.0, 3.0]), M=np.arange(9.0).reshape(3, 3),
+               pdf=[dict(mean=np.array([x, 0.0]), cov=np.eye(2)) for x in (3.0, 1.0, 2.0)],
+               gamma=[np.array([[0.2], [0.5], [0.3]])],
+               varpar=dict(alpha=np.array([1.0, 2.0, 3.0]), epsilon=np.arange(9.0).reshape(3, 3),
+                           beta=np.ones(3), v=np.array([4.0, 5.0, 6.0]), m=np.eye(3)[:, :2],
+                           W=np.stack([np.eye(2) * k for k in (1, 2, 3)])))
+    f = vbhmm_standardize(hmm, "f")          # prior argmax 1, then row 1 -> 0, then 2
+    np.testing.assert_allclose(f["prior"], [0.5, 0.2, 0.3])
+    np.testing.assert_allclose(f["trans"], hmm["trans"][np.ix_([1, 0, 2], [1, 0, 2])])
+    assert [q["mean"][0] for q in f["pdf"]] == [1.0, 3.0, 2.0]
+    np.testing.assert_allclose(f["varpar"]["W"][:, 0, 0], [2, 1, 3])
+    np.testing.assert_allclose(f["gamma"][0][:, 0], [0.5, 0.2, 0.3])
+    np.testing.assert_allclose(vbhmm_standardize(f, "f")["prior"], f["prior"])   # idempotent
+    assert list(vbhmm_standardize(hmm, "e")["N"]) == [9.0, 7.0, 5.0]
+    assert [q["mean"][0] for q in vbhmm_standardize(hmm, "l")["pdf"]] == [1.0, 2.0, 3.0]
+    p = vbhmm_prob_steadystate(hmm)
+    np.testing.assert_allclose(p @ hmm["trans"], p, atol=1e-12)
+    np.testing.assert_allclose(p.sum(), 1.0)
+    back = vbhmm_permute(vbhmm_permute(hmm, [2, 0, 1]), [1, 2, 0])
+    np.testing.assert_allclose(back["varpar"]["epsilon"], hmm["varpar"]["epsilon"])
