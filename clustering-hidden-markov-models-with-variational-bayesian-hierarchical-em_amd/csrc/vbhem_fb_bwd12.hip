@@ -42,6 +42,11 @@
 #define VBHEM_BWD12_WAVES 2
 #endif
 
+// VBHEM_EF_VALU: Ef from the row sums by one fma per element (fb_bwd4_kernel's switch)
+#ifndef VBHEM_EF_VALU
+#define VBHEM_EF_VALU 1
+#endif
+
 namespace vbhem {
 
 namespace {
@@ -186,6 +191,33 @@ void fb_bwd12_kernel(const SplitArgs p) {
         }
       double mabs = 0.0;
       bool nf = false;
+#if VBHEM_EF_VALU
+      // row sums of Ab first (P layout: column 4J + c's sum in every lane row), then
+      // Ef = E + amax[sigma] rowsum(Ab)[beta] as one fma per element (row sigma = 4I + r)
+      // instead of NB MFMAs
+      double rsj[NB], rs = 0.0;  // (the |V| bound assumes row sums <= 1)
+#pragma unroll
+      for (int jj = 0; jj < NB; ++jj) {
+        double x = 0.0;
+#pragma unroll
+        for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
+        rsj[jj] = x;
+        rs = fmax(rs, x);
+      }
+#pragma unroll
+      for (int i2 = 0; i2 < NB; ++i2) {
+        const double amr = amax[4 * i2 + r];
+#pragma unroll
+        for (int jj = 0; jj < NB; ++jj) {
+          const double e = cur.e[i2][jj];
+          V[i2][jj] = e;
+          const double ef = fma(amr, rsj[jj], e);
+          Ef[i2][jj] = ef;
+          mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
+          nf |= !isfinite(ef);
+        }
+      }
+#else
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2)
 #pragma unroll
@@ -209,6 +241,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
         for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
         rs = fmax(rs, x);
       }
+#endif
       const bool rbad = !(mabs < vlim) || rs > 1.0 + 1e-6;
       int zmin = 0x7fffffff;
 

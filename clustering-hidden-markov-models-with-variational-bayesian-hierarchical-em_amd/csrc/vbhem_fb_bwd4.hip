@@ -96,6 +96,12 @@
 //                       Measured no faster (C4 1.43-1.49 vs 1.42-1.44 ms per launch, shard
 //                       0.189 vs 0.184-0.187 ms; profiles/r05am_ab_bwd4_etab2.txt): the
 //                       16-byte table reads cost what the fp64 operation saved.  A/B switch
+//   VBHEM_EF_VALU       Ef = E + amax rowsum(Ab) as one fma per element from the row sums
+//                       the range check computes anyway, instead of 2 MFMAs per element
+//                       (8 of a tile's 12 setup MFMAs); the same in fb_bwd12_kernel
+#ifndef VBHEM_EF_VALU
+#define VBHEM_EF_VALU 1
+#endif
 #ifndef VBHEM_BWD4_ETAB2
 #define VBHEM_BWD4_ETAB2 0
 #endif
@@ -290,6 +296,27 @@ void fb_bwd4_kernel(const SplitArgs p) {
         }
       double mabs = 0.0, rs = 0.0;
       bool nf = false;
+#if VBHEM_EF_VALU
+      // row sums of Ab (P layout: every lane row holds column 4J + c's sum), then
+      // Ef = E + amax[sigma] rowsum(Ab)[beta] as one fma per element (the P layout's row
+      // sigma = 4I + r) instead of two MFMAs
+      double rsj[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) rsj[jj] = mfma4(1.0, AbT[q][1][jj], mfma4(1.0, AbT[q][0][jj], 0.0));
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const double amr = amax[4 * i2 + r];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const double e = cur.e[q][i2][jj];
+          V[q][i2][jj] = e;
+          Ef[q][i2][jj] = fma(amr, rsj[jj], e);
+          mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[q][i2][jj])));
+          nf |= !isfinite(Ef[q][i2][jj]);
+        }
+      }
+      rs = fmax(rsj[0], rsj[1]);
+#else
 #pragma unroll
       for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -305,6 +332,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       // row sums of Ab (P layout, column 4J + c): the |V| bound assumes <= 1
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) rs = fmax(rs, mfma4(1.0, AbT[q][1][jj], mfma4(1.0, AbT[q][0][jj], 0.0)));
+#endif
       rbad[q] = !(mabs < vlim) || rs > 1.0 + 1e-6;
       nfb[q] = nf;
       zmin[q] = 0x7fffffff;

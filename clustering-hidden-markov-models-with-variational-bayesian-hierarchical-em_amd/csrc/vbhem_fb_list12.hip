@@ -29,6 +29,11 @@
 #include "vbhem_math.h"
 #include "vbhem_mfma4.h"
 
+// VBHEM_EF_VALU: Ef from the row sums by one fma per element (fb_bwd4_kernel's switch)
+#ifndef VBHEM_EF_VALU
+#define VBHEM_EF_VALU 1
+#endif
+
 namespace vbhem {
 
 namespace {
@@ -170,7 +175,11 @@ void fb_list12_kernel(const SplitArgs p) {
         for (int y = 0; y < NB; ++y) AT[x][y] = At[(4 * y + c) * S + 4 * x + r];
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2) {
+#if VBHEM_EF_VALU
+        const double *la = p.logA + ((size_t)j * S + 4 * i2 + r) * S;  // (P rows: the fma below)
+#else
         const double *la = p.logA + ((size_t)j * S + 4 * i2 + c) * S;
+#endif
         double mx = la[0];
 #pragma unroll
         for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
@@ -197,6 +206,30 @@ void fb_list12_kernel(const SplitArgs p) {
       }
     double mabs = 0.0, rs = 0.0;
     bool nfp = false;
+#if VBHEM_EF_VALU
+    // Ef = E + amax[sigma] rowsum(Ab)[beta]: one fma per element from the row sums
+    // (fb_bwd12_kernel's VBHEM_EF_VALU; amQ holds the P rows 4I + r here)
+    double rsj[NB];
+#pragma unroll
+    for (int jj = 0; jj < NB; ++jj) {
+      double x = 0.0;
+#pragma unroll
+      for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
+      rsj[jj] = x;
+      rs = fmax(rs, x);
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < NB; ++i2)
+#pragma unroll
+      for (int jj = 0; jj < NB; ++jj) {
+        const double e = cur.e[i2][jj];
+        V[i2][jj] = e;
+        const double ef = fma(amQ[i2], rsj[jj], e);
+        Ef[i2][jj] = ef;
+        mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
+        nfp |= !isfinite(ef);
+      }
+#else
 #pragma unroll
     for (int i2 = 0; i2 < NB; ++i2)
 #pragma unroll
@@ -217,6 +250,7 @@ void fb_list12_kernel(const SplitArgs p) {
       for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
       rs = fmax(rs, x);
     }
+#endif
     const bool rbad = !(mabs < vlim) || rs > 1.0 + 1e-6;
     int zmin = 0x7fffffff;
 

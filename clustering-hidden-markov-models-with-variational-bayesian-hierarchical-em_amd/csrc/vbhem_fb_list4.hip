@@ -40,6 +40,11 @@
 #define VBHEM_LIST4_R4 0
 #endif
 
+// VBHEM_EF_VALU: Ef from the row sums by one fma per element (fb_bwd4_kernel's switch)
+#ifndef VBHEM_EF_VALU
+#define VBHEM_EF_VALU 1
+#endif
+
 namespace vbhem {
 
 namespace {
@@ -168,7 +173,11 @@ void fb_list4_kernel(const SplitArgs p) {
         }
 #pragma unroll
       for (int i2 = 0; i2 < 2; ++i2) {
+#if VBHEM_EF_VALU
+        const double *la = p.logA + ((size_t)j * S + 4 * i2 + r) * S;  // (P rows: the fma below)
+#else
         const double *la = p.logA + ((size_t)j * S + 4 * i2 + c) * S;
+#endif
         double mx = la[0];
 #pragma unroll
         for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
@@ -195,6 +204,24 @@ void fb_list4_kernel(const SplitArgs p) {
       }
     double mabs = 0.0, rs = 0.0;
     bool nfp = false;
+#if VBHEM_EF_VALU
+    // Ef = E + amax[sigma] rowsum(Ab)[beta]: one fma per element from the row sums
+    // (fb_bwd4_kernel's VBHEM_EF_VALU; amQ holds the P rows 4I + r here)
+    double rsj[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) rsj[jj] = mfma4(1.0, AbT[1][jj], mfma4(1.0, AbT[0][jj], 0.0));
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const double e = cur.e[i2][jj];
+        V[i2][jj] = e;
+        Ef[i2][jj] = fma(amQ[i2], rsj[jj], e);
+        mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[i2][jj])));
+        nfp |= !isfinite(Ef[i2][jj]);
+      }
+    rs = fmax(rsj[0], rsj[1]);
+#else
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -207,6 +234,7 @@ void fb_list4_kernel(const SplitArgs p) {
       }
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) rs = fmax(rs, mfma4(1.0, AbT[1][jj], mfma4(1.0, AbT[0][jj], 0.0)));
+#endif
     const bool rbad = !(mabs < vlim) || rs > 1.0 + 1e-6;
     int zmin = 0x7fffffff;
 
