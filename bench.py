@@ -121,8 +121,12 @@ def committed_traffic(config, N, world, want):
             return full["hbm_bytes"]["traffic"], os.path.relpath(path, ROOT) + " (full-size launches)"
         if not summ.get("pmc_full_size_only"):
             continue    # PMC passes that mixed launch sizes: not this kernel's traffic
-        for name, k in summ.get("kernels", {}).items():
-            if name == want and "hbm_bytes_per_launch" in k:
+        kern = summ.get("kernels", {})
+        # the exact name, else the same kernel under another template argument (the
+        # fb_bwd4_kernel<O32> versions, or a summary from before the template)
+        for name in [want] + [n for n in kern if n.split("<")[0] == want.split("<")[0] and n != want]:
+            k = kern.get(name, {})
+            if "hbm_bytes_per_launch" in k:
                 return k["hbm_bytes_per_launch"]["traffic"], os.path.relpath(path, ROOT)
     return None, None
 

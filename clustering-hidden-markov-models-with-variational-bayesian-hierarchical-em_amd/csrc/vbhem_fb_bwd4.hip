@@ -135,6 +135,7 @@ using namespace m4;
 
 }  // namespace
 
+template <bool O32>
 __global__ __launch_bounds__(64 * kNWB) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void fb_bwd4_kernel(const SplitArgs p) {
   constexpr int S = 8;
@@ -239,8 +240,12 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #endif
   // the tile loop, versioned on the underflow test (ZS: the cluster's A' makes it
   // unnecessary, VBHEM_BWD4_ZSAFE)
-  auto tiles = [&](auto zs_tag) {
+  // and on SB == 8 (F8: every base state present, so no clamp or zero select is
+  // left in the tile's addresses and operands)
+  auto tiles = [&](auto zs_tag, auto f8_tag) {
   constexpr bool ZS = decltype(zs_tag)::value;
+  constexpr bool F8 = decltype(f8_tag)::value;
+  const int SBk = F8 ? 8 : SB;
   const int ntile = (p.i_end - p.i_begin + kPPW - 1) / kPPW;
   const int tstride = NB * kNWB;
   // a tile's global inputs (A, E, the prior), loaded one tile ahead: the next tile's
@@ -249,6 +254,17 @@ void fb_bwd4_kernel(const SplitArgs p) {
   // until the tile is processed)
   struct TileIn {
     double a[kQPW][2][2], e[kQPW][2][2], pr[kQPW];
+  };
+  // O32: 32-bit element offsets from the uniform base pointers (launch_bwd4 checks that
+  // A, the prior and E stay below 4 GB), so every load is one offset computation and a
+  // saddr load instead of 64-bit address arithmetic (with the SB == 8 versions this
+  // also took the kernel's last 12 bytes of scratch away)
+  using off_t_ = typename std::conditional<O32, unsigned, size_t>::type;
+  auto ld = [](const double *base, off_t_ x) {
+    if constexpr (O32)
+      return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + x * 8u);
+    else
+      return base[x];
   };
   auto load_tile = [&](int tile, TileIn &in) {
     const int i0 = p.i_begin + tile * kPPW;
@@ -261,18 +277,20 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
-          in.a[q][j2][jj] = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
+          const off_t_ x = ((off_t_)ic * SBk + (be < SBk ? be : SBk - 1)) * SBk + (bp < SBk ? bp : SBk - 1);
+          in.a[q][j2][jj] = ld(p.A, x);
         }
 #pragma unroll
       for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int be = 4 * jj + c;
-          in.e[q][i2][jj] = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
-                                (be < SB ? be : SB - 1)];
+          const off_t_ x = (off_t_)(j * S + 4 * i2 + r) * (off_t_)p.e_ld +
+                           (off_t_)(ic - p.i_buf0) * SBk + (be < SBk ? be : SBk - 1);
+          in.e[q][i2][jj] = ld(p.E, x);
         }
       const int be = 4 * (r & 1) + c;
-      in.pr[q] = p.prior[(size_t)ic * SB + (be < SB ? be : SB - 1)];
+      in.pr[q] = ld(p.prior, (off_t_)ic * SBk + (be < SBk ? be : SBk - 1));
     }
   };
   TileIn cur;
@@ -292,7 +310,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
-          AbT[q][j2][jj] = (be < SB && bp < SB) ? cur.a[q][j2][jj] : 0.0;
+          AbT[q][j2][jj] = (be < SBk && bp < SBk) ? cur.a[q][j2][jj] : 0.0;
         }
       double mabs = 0.0, rs = 0.0;
       bool nf = false;
@@ -582,7 +600,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       }
       const double lse = lse1[0];
       const int be = 4 * (r & 1) + c;
-      const double pr = be < SB ? cur.pr[q] : 0.0;
+      const double pr = be < SBk ? cur.pr[q] : 0.0;
       double y = r < 2 ? pr * lse : 0.0;
       const bool bad = zmin[q] < kZMinHi || !isfinite(y) || rbad[q];
       y += shfl_xor_d(y, 1);
@@ -606,8 +624,13 @@ void fb_bwd4_kernel(const SplitArgs p) {
     cur = nxt;
   }
   };
-  if (zsafe) tiles(std::true_type{});
-  else tiles(std::false_type{});
+  if (SB == 8) {
+    if (zsafe) tiles(std::true_type{}, std::true_type{});
+    else tiles(std::false_type{}, std::true_type{});
+  } else {
+    if (zsafe) tiles(std::true_type{}, std::false_type{});
+    else tiles(std::false_type{}, std::false_type{});
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -615,16 +638,23 @@ bool bwd4_supported(int S, int SB) { return S == 8 && SB >= 1 && SB <= 8; }
 int bwd4_waves() { return kNWB; }
 int bwd4_ppb() { return kNWB * kPPW; }
 int bwd4_resident_blocks() {
-  return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd4_kernel), 64 * kNWB, 0);
+  return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd4_kernel<true>), 64 * kNWB, 0);
+}
+// the O32 version when every byte offset of A, the prior and E fits 32 bits
+bool bwd4_o32(const SplitArgs &a) {
+  const unsigned long long lim = 0xffffffffull / 8;
+  return (unsigned long long)a.i_end * a.SB * a.SB < lim &&
+         (unsigned long long)a.K * a.S * (unsigned long long)a.e_ld < lim;
 }
 
 hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0,
                        hipEvent_t t1) {
   if (!bwd4_supported(a.S, a.SB) || !a.Atg) return hipErrorInvalidValue;
+  auto *fn = bwd4_o32(a) ? &fb_bwd4_kernel<true> : &fb_bwd4_kernel<false>;
   if (t0)  // timing events recorded by the dispatch itself (the bench's roofline)
-    hipExtLaunchKernelGGL(fb_bwd4_kernel, dim3(grid), dim3(64 * kNWB), 0, st, t0, t1, 0, a);
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(64 * kNWB), 0, st, t0, t1, 0, a);
   else
-    hipLaunchKernelGGL(fb_bwd4_kernel, dim3(grid), dim3(64 * kNWB), 0, st, a);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * kNWB), 0, st, a);
   return hipGetLastError();
 }
 

@@ -40,5 +40,5 @@ def test_bench_gpus2_launches_two_ranks():
     assert col["allreduce_ms"] is not None and col["allreduce_ms"] > 0
     assert len(col["allreduce_ms_per_rank"]) == 2
     assert res["value"] > 0 and res["em_iteration"]["iterations"] > 0
-    assert res["roofline"]["kernel"] == "vbhem::fb_bwd4_kernel"
+    assert res["roofline"]["kernel"] == "vbhem::fb_bwd4_kernel<true>"
     assert res["gated_forward"]["kernel"] == "vbhem::fb_list4_kernel<10>"
