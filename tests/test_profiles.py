@@ -44,11 +44,12 @@ def test_frac_from_summary_matches_bench(name, summ):
     # recomputed here from the summary's own numbers (not its stored fraction)
     frac = c["flops_per_launch"] / (c["trace_mean_ms"] * 1e-3) / 1e12 / c["peak_TFLOPs"]
     assert abs(frac - c["frac_trace_mean"]) < 1e-12
-    # 3 % for launches of a millisecond or more (C4, C5); the bench's live timing takes
-    # its two HIP events from the dispatch itself, which adds the ~5-14 us of wave launch
-    # and drain to the kernel trace's time -- 7 % of the 0.19 ms shard-size launch, 12 %
-    # of C3's 0.047 ms one -- so those are held to 15 %
-    tol = 0.03 if c["trace_mean_ms"] >= 1.0 else 0.15
+    # 4 % for launches of a millisecond or more (C4, C5); the bench's live timing takes
+    # its two HIP events from the dispatch itself, which adds the wave launch and drain
+    # to the kernel trace's time -- 5-40 us: up to 3 % of a 1.3 ms launch (r05zz3: 1.286
+    # ms traced, 1.322 ms live), 7 % of the 0.19 ms shard-size launch, 12 % of C3's
+    # 0.047 ms one -- so the short ones are held to 15 %
+    tol = 0.04 if c["trace_mean_ms"] >= 1.0 else 0.15
     assert abs(frac / c["bench_frac"] - 1.0) < tol, (name, frac, c["bench_frac"])
     k = summ["kernels"][c["kernel"]]
     assert k["trace_launches_ms"]["n"] == c["trace_launches"]
