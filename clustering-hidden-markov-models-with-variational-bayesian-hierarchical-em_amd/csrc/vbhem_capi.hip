@@ -691,7 +691,7 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
       if (nb >= 8) nb = nb / 8 * 8;
       e = vbhem::launch_bwd12(ca, (unsigned)ca.K * nb, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd12_kernel");
-      g_last_kernel[0] = "vbhem::fb_bwd12_kernel";
+      g_last_kernel[0] = vbhem::bwd12_o32(ca) ? "vbhem::fb_bwd12_kernel<true>" : "vbhem::fb_bwd12_kernel<false>";
     } else if (mode == vbhem::kFbBackward && c.bwd2_lds) {
       // fb_bwd2_kernel, persistent: NB blocks per cluster (x8 when possible)
       ca.nwb = c.bwd2_nwb;

@@ -78,6 +78,7 @@ __device__ __forceinline__ double rowsum_all(double x) {
 }
 }  // namespace
 
+template <bool O32>
 __global__ __launch_bounds__(64 * kNWB12) __attribute__((amdgpu_waves_per_eu(kWaves12)))
 void fb_bwd12_kernel(const SplitArgs p) {
   constexpr int S = 12, NB = 3;
@@ -140,8 +141,21 @@ void fb_bwd12_kernel(const SplitArgs p) {
   const double vlim = kVMax / (double)T - 3.0;
   const int ntile = (p.i_end - p.i_begin + 3) / 4;
 
-  auto tiles = [&](auto zs_tag) {
+  // versioned on SB == 12 too (F12: no clamp or zero select in the tile's addresses and
+  // operands), as fb_bwd4_kernel
+  auto tiles = [&](auto zs_tag, auto f12_tag) {
     constexpr bool ZS = decltype(zs_tag)::value;
+    constexpr bool F12 = decltype(f12_tag)::value;
+    const int SBk = F12 ? 12 : SB;
+    // O32: 32-bit element offsets from the uniform base pointers (launch_bwd12 checks
+    // that A, the prior and E stay below 4 GB), as fb_bwd4_kernel
+    using off_t_ = typename std::conditional<O32, unsigned, size_t>::type;
+    auto ld = [](const double *base, off_t_ x) {
+      if constexpr (O32)
+        return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + x * 8u);
+      else
+        return base[x];
+    };
     const int tstride = NBk * kNWB12;
     // a tile's global inputs, loaded one tile ahead (as fb_bwd4_kernel): clamped
     // addresses, the selects on the values only when the tile is processed
@@ -156,20 +170,20 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
-          in.a[j2][jj] = p.A[((size_t)ic * SB + (be < SB ? be : SB - 1)) * SB + (bp < SB ? bp : SB - 1)];
+          in.a[j2][jj] = ld(p.A, ((off_t_)ic * SBk + (be < SBk ? be : SBk - 1)) * SBk + (bp < SBk ? bp : SBk - 1));
         }
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2)
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj) {
           const int be = 4 * jj + c;
-          in.e[i2][jj] = p.E[((size_t)j * S + 4 * i2 + r) * p.e_ld + (size_t)(ic - p.i_buf0) * SB +
-                             (be < SB ? be : SB - 1)];
+          in.e[i2][jj] = ld(p.E, (off_t_)(j * S + 4 * i2 + r) * (off_t_)p.e_ld + (off_t_)(ic - p.i_buf0) * SBk +
+                                     (be < SBk ? be : SBk - 1));
         }
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj) {
         const int be = 4 * jj + c;
-        in.pr[jj] = p.prior[(size_t)ic * SB + (be < SB ? be : SB - 1)];
+        in.pr[jj] = ld(p.prior, (off_t_)ic * SBk + (be < SBk ? be : SBk - 1));
       }
     };
     TileIn cur;
@@ -187,7 +201,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
-          AbT[j2][jj] = (be < SB && bp < SB) ? cur.a[j2][jj] : 0.0;
+          AbT[j2][jj] = (be < SBk && bp < SBk) ? cur.a[j2][jj] : 0.0;
         }
       double mabs = 0.0;
       bool nf = false;
@@ -367,7 +381,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
           const int wqf[1] = {(int)(wc[jj] + kWq0)};
           log_q_n<1, false>(lse1, zsf, wqf, ltab8);
           const int be = 4 * jj + c;
-          const double pr = be < SB ? cur.pr[jj] : 0.0;
+          const double pr = be < SBk ? cur.pr[jj] : 0.0;
           y += pr * lse1[0];
         }
         const bool bad = zmin < kZMinHi || !isfinite(y) || rbad;
@@ -391,24 +405,38 @@ void fb_bwd12_kernel(const SplitArgs p) {
       cur = nxt;
     }
   };
-  if (zsafe) tiles(std::true_type{});
-  else tiles(std::false_type{});
+  if (SB == 12) {
+    if (zsafe) tiles(std::true_type{}, std::true_type{});
+    else tiles(std::false_type{}, std::true_type{});
+  } else {
+    if (zsafe) tiles(std::true_type{}, std::false_type{});
+    else tiles(std::false_type{}, std::false_type{});
+  }
 }
 
 // ---------------------------------------------------------------------------
 bool bwd12_supported(int S, int SB) { return S == 12 && SB >= 1 && SB <= 12; }
 int bwd12_ppb() { return kNWB12 * 4; }
 int bwd12_resident_blocks() {
-  return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd12_kernel), 64 * kNWB12, 0);
+  return resident_per_cu(reinterpret_cast<const void *>(&fb_bwd12_kernel<true>), 64 * kNWB12, 0);
+}
+
+// the O32 version when every byte offset of A, the prior and E fits 32 bits
+bool bwd12_o32(const SplitArgs &a) {
+  const unsigned long long lim = 0xffffffffull / 8;
+  return (unsigned long long)a.i_end * a.SB * a.SB < lim &&
+         (unsigned long long)a.K * a.S * (unsigned long long)a.e_ld < lim;
 }
 
 hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0,
                         hipEvent_t t1) {
   if (!bwd12_supported(a.S, a.SB) || !a.Atg) return hipErrorInvalidValue;
   if (t0)  // timing events recorded by the dispatch itself (the bench's roofline)
-    hipExtLaunchKernelGGL(fb_bwd12_kernel, dim3(grid), dim3(64 * kNWB12), 0, st, t0, t1, 0, a);
+    hipExtLaunchKernelGGL(bwd12_o32(a) ? &fb_bwd12_kernel<true> : &fb_bwd12_kernel<false>, dim3(grid),
+                          dim3(64 * kNWB12), 0, st, t0, t1, 0, a);
   else
-    hipLaunchKernelGGL(fb_bwd12_kernel, dim3(grid), dim3(64 * kNWB12), 0, st, a);
+    hipLaunchKernelGGL(bwd12_o32(a) ? &fb_bwd12_kernel<true> : &fb_bwd12_kernel<false>, dim3(grid),
+                       dim3(64 * kNWB12), 0, st, a);
   return hipGetLastError();
 }
 
