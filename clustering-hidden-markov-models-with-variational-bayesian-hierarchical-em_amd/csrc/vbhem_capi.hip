@@ -575,7 +575,8 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
     const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list4_resident_blocks()));
     e = vbhem::launch_list4(ca, grid, st);
     if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
-    g_last_kernel[1] = "vbhem::fb_list4_kernel<" + std::to_string(ca.T) + ">";
+    g_last_kernel[1] = "vbhem::fb_list4_kernel<" + std::to_string(ca.T) +
+                       (vbhem::list4_fast(ca) ? ", true>" : ", false>");
   } else if (c.list12) {  // S = 12, SB <= 12, T = 10: fb_list12_kernel (MFMA), one wave per quad
     ca.Atg = c.bwd.a.Atg;
     const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list12_resident_blocks()));

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "vbhem_internal.h"
 #include "vbhem_math.h"
@@ -54,7 +55,9 @@ constexpr int kL4NWB = VBHEM_LIST4_R4 ? 8 : 4;   // waves per block
 constexpr int kL4T = 10;      // the tau this kernel is built for (C3 - C5)
 }  // namespace
 
-template <int T>
+// FAST: SB == 8 (no clamp or zero select in the item's addresses and operands) and
+// 32-bit load offsets (A, the prior and E below 4 GB), as fb_bwd4_kernel<O32>
+template <int T, bool FAST>
 __global__ __launch_bounds__(64 * kL4NWB) __attribute__((amdgpu_waves_per_eu(kL4Waves)))
 void fb_list4_kernel(const SplitArgs p) {
   constexpr int S = 8;
@@ -74,7 +77,14 @@ void fb_list4_kernel(const SplitArgs p) {
 #else
   stage_tables(etab, ltab, tid, 64 * kL4NWB);
 #endif
-  const int K = p.K, SB = p.SB;
+  const int K = p.K, SB = FAST ? 8 : p.SB;
+  using off_t_ = typename std::conditional<FAST, unsigned, size_t>::type;
+  auto ld = [](const double *base, off_t_ x) {
+    if constexpr (FAST)
+      return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + x * 8u);
+    else
+      return base[x];
+  };
   if (tid == 0) {
     int s = 0;
     for (int jj = 0; jj < K; ++jj) {
@@ -106,21 +116,21 @@ void fb_list4_kernel(const SplitArgs p) {
       for (int j3 = 0; j3 < 2; ++j3) {
         const int be = 4 * j3 + c_, bp = 4 * j2 + r_;
         const int bec = be < SB ? be : SB - 1, bpc = bp < SB ? bp : SB - 1;
-        in.ab[j2][j3] = p.A[((size_t)i * SB + bec) * SB + bpc];
-        in.af[j2][j3] = p.A[((size_t)i * SB + bpc) * SB + bec];
+        in.ab[j2][j3] = ld(p.A, ((off_t_)i * SB + bec) * SB + bpc);
+        in.af[j2][j3] = ld(p.A, ((off_t_)i * SB + bpc) * SB + bec);
       }
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
       for (int j3 = 0; j3 < 2; ++j3) {
         const int be = 4 * j3 + c_;
-        in.e[i2][j3] = p.E[((size_t)jj * S + 4 * i2 + r_) * p.e_ld + (size_t)(i - p.i_buf0) * SB +
-                           (be < SB ? be : SB - 1)];
+        in.e[i2][j3] = ld(p.E, (off_t_)(jj * S + 4 * i2 + r_) * (off_t_)p.e_ld + (off_t_)(i - p.i_buf0) * SB +
+                                   (be < SB ? be : SB - 1));
       }
 #pragma unroll
     for (int j3 = 0; j3 < 2; ++j3) {
       const int be = 4 * j3 + c_;
-      in.pr[j3] = p.prior[(size_t)i * SB + (be < SB ? be : SB - 1)];
+      in.pr[j3] = ld(p.prior, (off_t_)i * SB + (be < SB ? be : SB - 1));
     }
   };
   // the base of pair b of item it (cluster jj; past the list's end: the quad's first)
@@ -464,12 +474,19 @@ void fb_list4_kernel(const SplitArgs p) {
 bool list4_supported(int S, int SB, int T, int K) {
   return S == 8 && SB >= 1 && SB <= 8 && T == kL4T && K >= 1 && K <= kList4MaxK;
 }
+bool list4_fast(const SplitArgs &a) {
+  const unsigned long long lim = 0xffffffffull / 8;
+  return a.SB == 8 && (unsigned long long)a.i_end * a.SB * a.SB < lim &&
+         (unsigned long long)a.K * a.S * (unsigned long long)a.e_ld < lim;
+}
 int list4_resident_blocks() {
-  return resident_per_cu(reinterpret_cast<const void *>(&fb_list4_kernel<kL4T>), 64 * kL4NWB, 0);
+  auto *fn = &fb_list4_kernel<kL4T, true>;
+  return resident_per_cu(reinterpret_cast<const void *>(fn), 64 * kL4NWB, 0);
 }
 hipError_t launch_list4(const SplitArgs &a, unsigned grid, hipStream_t st) {
   if (!list4_supported(a.S, a.SB, a.T, a.K) || !a.Atg || !a.list || !a.list_tot) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fb_list4_kernel<kL4T>, dim3(grid), dim3(64 * kL4NWB), 0, st, a);
+  auto *fn = list4_fast(a) ? &fb_list4_kernel<kL4T, true> : &fb_list4_kernel<kL4T, false>;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * kL4NWB), 0, st, a);
   return hipGetLastError();
 }
 

@@ -41,4 +41,4 @@ def test_bench_gpus2_launches_two_ranks():
     assert len(col["allreduce_ms_per_rank"]) == 2
     assert res["value"] > 0 and res["em_iteration"]["iterations"] > 0
     assert res["roofline"]["kernel"] == "vbhem::fb_bwd4_kernel<true>"
-    assert res["gated_forward"]["kernel"] == "vbhem::fb_list4_kernel<10>"
+    assert res["gated_forward"]["kernel"] == "vbhem::fb_list4_kernel<10, true>"
