@@ -582,7 +582,8 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
     const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list12_resident_blocks()));
     e = vbhem::launch_list12(ca, grid, st);
     if (e != hipSuccess) return hip_fail(e, "fb_list12_kernel");
-    g_last_kernel[1] = "vbhem::fb_list12_kernel<" + std::to_string(ca.T) + ">";
+    g_last_kernel[1] = "vbhem::fb_list12_kernel<" + std::to_string(ca.T) +
+                       (vbhem::list12_fast(ca) ? ", true>" : ", false>");
   } else {
     if (c.k1_in_kernel) set_k1_operands(c, i_begin, ca);
     const unsigned grid = list_grid(ca, c.split.lds_l);

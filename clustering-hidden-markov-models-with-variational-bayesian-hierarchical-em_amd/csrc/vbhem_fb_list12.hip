@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "vbhem_internal.h"
 #include "vbhem_math.h"
@@ -70,7 +71,9 @@ __device__ __forceinline__ void transpose12(const double (&x)[NB][NB], double (&
 }
 }  // namespace
 
-template <int T>
+// FAST: SB == 12 (no clamp or zero select in the item's addresses and operands) and
+// 32-bit load offsets (A, the prior and E below 4 GB), as fb_list4_kernel<T, FAST>
+template <int T, bool FAST>
 __global__ __launch_bounds__(64 * kL12NWB) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void fb_list12_kernel(const SplitArgs p) {
   constexpr int S = 12;
@@ -83,7 +86,14 @@ void fb_list12_kernel(const SplitArgs p) {
   const int tid = threadIdx.x;
   for (int x = tid; x < 2048; x += 64 * kL12NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
   stage_log8k(ltab8, tid, 64 * kL12NWB);
-  const int K = p.K, SB = p.SB;
+  const int K = p.K, SB = FAST ? 12 : p.SB;
+  using off_t_ = typename std::conditional<FAST, unsigned, size_t>::type;
+  auto ld = [](const double *base, off_t_ x) {
+    if constexpr (FAST)
+      return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + x * 8u);
+    else
+      return base[x];
+  };
   if (tid == 0) {
     int s = 0;
     for (int jj = 0; jj < K; ++jj) {
@@ -122,21 +132,21 @@ void fb_list12_kernel(const SplitArgs p) {
       for (int j3 = 0; j3 < NB; ++j3) {
         const int be = 4 * j3 + c, bp = 4 * j2 + r;
         const int bec = be < SB ? be : SB - 1, bpc = bp < SB ? bp : SB - 1;
-        in.ab[j2][j3] = p.A[((size_t)i * SB + bec) * SB + bpc];
-        in.af[j2][j3] = p.A[((size_t)i * SB + bpc) * SB + bec];
+        in.ab[j2][j3] = ld(p.A, ((off_t_)i * SB + bec) * SB + bpc);
+        in.af[j2][j3] = ld(p.A, ((off_t_)i * SB + bpc) * SB + bec);
       }
 #pragma unroll
     for (int i2 = 0; i2 < NB; ++i2)
 #pragma unroll
       for (int j3 = 0; j3 < NB; ++j3) {
         const int be = 4 * j3 + c;
-        in.e[i2][j3] = p.E[((size_t)jj * S + 4 * i2 + r) * p.e_ld + (size_t)(i - p.i_buf0) * SB +
-                           (be < SB ? be : SB - 1)];
+        in.e[i2][j3] = ld(p.E, (off_t_)(jj * S + 4 * i2 + r) * (off_t_)p.e_ld + (off_t_)(i - p.i_buf0) * SB +
+                                   (be < SB ? be : SB - 1));
       }
 #pragma unroll
     for (int j3 = 0; j3 < NB; ++j3) {
       const int be = 4 * j3 + c;
-      in.pr[j3] = p.prior[(size_t)i * SB + (be < SB ? be : SB - 1)];
+      in.pr[j3] = ld(p.prior, (off_t_)i * SB + (be < SB ? be : SB - 1));
     }
   };
   // the base of pair b of item it (cluster jj; past the list's end: the quad's first)
@@ -516,13 +526,20 @@ void fb_list12_kernel(const SplitArgs p) {
 bool list12_supported(int S, int SB, int T, int K) {
   return S == 12 && SB >= 1 && SB <= 12 && T == kL12T && K >= 1 && K <= kList4MaxK;
 }
+bool list12_fast(const SplitArgs &a) {
+  const unsigned long long lim = 0xffffffffull / 8;
+  return a.SB == 12 && (unsigned long long)a.i_end * a.SB * a.SB < lim &&
+         (unsigned long long)a.K * a.S * (unsigned long long)a.e_ld < lim;
+}
 int list12_resident_blocks() {
-  return resident_per_cu(reinterpret_cast<const void *>(&fb_list12_kernel<kL12T>), 64 * kL12NWB, 0);
+  auto *fn = &fb_list12_kernel<kL12T, true>;
+  return resident_per_cu(reinterpret_cast<const void *>(fn), 64 * kL12NWB, 0);
 }
 hipError_t launch_list12(const SplitArgs &a, unsigned grid, hipStream_t st) {
   if (!list12_supported(a.S, a.SB, a.T, a.K) || !a.Atg || !a.list || !a.list_tot)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fb_list12_kernel<kL12T>, dim3(grid), dim3(64 * kL12NWB), 0, st, a);
+  auto *fn = list12_fast(a) ? &fb_list12_kernel<kL12T, true> : &fb_list12_kernel<kL12T, false>;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * kL12NWB), 0, st, a);
   return hipGetLastError();
 }
 

@@ -373,6 +373,7 @@ int bwd4_resident_blocks();  // per CU
 bool bwd4_o32(const SplitArgs &a);  // the 32-bit-offset version applies (kernel <true>)
 bool bwd12_o32(const SplitArgs &a);  // fb_bwd12_kernel's likewise
 bool list4_fast(const SplitArgs &a);  // fb_list4_kernel<T, true>: SB == 8 and 32-bit offsets
+bool list12_fast(const SplitArgs &a);  // fb_list12_kernel<T, true>: SB == 12 and 32-bit offsets
 hipError_t launch_bwd4(const SplitArgs &a, unsigned grid, hipStream_t st, hipEvent_t t0 = nullptr,
                        hipEvent_t t1 = nullptr);
 // fb_bwd12_kernel (vbhem_fb_bwd12.hip): the same pass for S = 12, SB <= 12 (3 x 3 blocks)
