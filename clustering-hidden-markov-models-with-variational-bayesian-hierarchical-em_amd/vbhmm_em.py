@@ -632,6 +632,8 @@ def vbhmm_learn_batch(datas: Sequence[Sequence[np.ndarray]], Ks, opt: dict, devi
     for h in hmms:
         h["learn_hyps_batch"] = dict(hypinfo=[i.optname for i in info], opt_transhyp=Xopt,
                                      opt_L=-fX[-1], fX=fX, line_searches=nls)
+    if opt.get("sortclusters"):  # vbhmm_learn_batch.m:202-209
+        hmms = [vbhmm_standardize(h, opt["sortclusters"]) for h in hmms]
     return hmms, np.array([h["LL"] for h in hmms])
 
 
