@@ -241,3 +241,21 @@ def test_vbhmm_standardize(vb):
     np.testing.assert_allclose(p.sum(), 1.0)
     back = vbhmm_permute(vbhmm_permute(hmm, [2, 0, 1]), [1, 2, 0])
     np.testing.assert_allclose(back["varpar"]["epsilon"], hmm["varpar"]["epsilon"])
+
+
+@pytest.mark.gpu
+def test_learn_hyps_batch_gpu_matches_cpu_fb(vb, monkeypatch):
+    """learn_hyps_batch on the GPU forward-backward agrees with the same run on the C
+    restatement of vbhmm_fb_mex.c (bounds 1e-6, shared hyperparameters 1e-3)."""
+    from vbhem_amd import vbhmm_em as vme
+    subs = demo_subjects()
+    datas = [subs[1], subs[4]]
+    opt = _opts(learn_hyps_batch=["alpha0", "epsilon0", "mu0"], numtrials=2, maxIter=40)
+    hmms_g, Ls_g = vme.vbhmm_learn_batch(datas, [1, 2], opt, device="cuda:0")
+    with monkeypatch.context() as m:
+        m.setattr(vme.vbhmm, "vbhmm_fb", _cpu_fb)
+        m.setattr(vme.vbhmm, "SequenceBatch", lambda data, dim, device: None)
+        hmms_c, Ls_c = vme.vbhmm_learn_batch(datas, [1, 2], opt)
+    np.testing.assert_allclose(Ls_g, Ls_c, rtol=1e-6)
+    np.testing.assert_allclose(hmms_g[0]["learn_hyps_batch"]["opt_transhyp"],
+                               hmms_c[0]["learn_hyps_batch"]["opt_transhyp"], rtol=1e-3, atol=1e-3)
