@@ -697,7 +697,9 @@ def main():
                                 "the next (no overlap of the host hand-over)"},
         "pairs_per_s": N * K * args.steps / dt,
         "roofline": {
-            "bound": "valu",
+            # the compute roof (the contract's "mfma"): fp64 dense, 78.6 TF/s, the same for
+            # v_mfma_f64 and the vector ALU; see the note for which unit runs what
+            "bound": "mfma",
             "achieved": achieved,
             "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s",
@@ -712,8 +714,11 @@ def main():
             "timed_every_nth_step": time_every,
             "flops_per_pair": fpp,
             "pairs_per_launch": pairs_per_launch,
-            "note": ("fp64 VALU-bound (software exp/log + contractions on the vector ALU); "
-                     "peak = MI355X FP64 dense "
+            "note": (("fp64 issue-bound: the recursion's contractions on v_mfma_f64_4x4x4f64, the "
+                      "software exp/log on the VALU (the two do not co-issue)"
+                      if ("bwd4" in kname or "bwd12" in kname) else
+                      "fp64 VALU-bound (software exp/log + contractions on the vector ALU)") +
+                     "; peak = MI355X FP64 dense "
                      "78.6 TF/s (vector = matrix rate); achievable_peak = the sustained "
                      "v_fma_f64 rate measured on this chip by scripts/ubench_valu.hip "
                      "(4 waves/SIMD, independent chains); flops counted on the reference "
