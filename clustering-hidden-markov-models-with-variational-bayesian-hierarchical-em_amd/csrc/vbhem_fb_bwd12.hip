@@ -205,6 +205,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
         }
       double mabs = 0.0;
       bool nf = false;
+      uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
 #if VBHEM_EF_VALU
       // row sums of Ab first (P layout: column 4J + c's sum in every lane row), then
       // Ef = E + amax[sigma] rowsum(Ab)[beta] as one fma per element (row sigma = 4I + r)
@@ -216,7 +217,11 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
         for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
         rsj[jj] = x;
+#if VBHEM_RANGE_CMP
+        bigm |= gt_mask(x, 1.0 + 1e-6);
+#else
         rs = fmax(rs, x);
+#endif
       }
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2) {
@@ -227,7 +232,11 @@ void fb_bwd12_kernel(const SplitArgs p) {
           V[i2][jj] = e;
           const double ef = fma(amr, rsj[jj], e);
           Ef[i2][jj] = ef;
+#if VBHEM_RANGE_CMP
+          bigm |= ge_mask(fabs(e), vlim) | ge_mask(fabs(ef), vlim);
+#else
           mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
+#endif
           nf |= !isfinite(ef);
         }
       }
@@ -256,7 +265,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
         rs = fmax(rs, x);
       }
 #endif
-      const bool rbad = !(mabs < vlim) || rs > 1.0 + 1e-6;
+      const bool rbad = lane_in(bigm) || !(mabs < vlim) || rs > 1.0 + 1e-6;
       int zmin = 0x7fffffff;
 
       // ---- K2: backward recursion, t = T-1 .. 1 ----

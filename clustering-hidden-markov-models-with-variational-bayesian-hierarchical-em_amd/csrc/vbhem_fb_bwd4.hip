@@ -301,6 +301,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
     load_tile(min(tile + tstride, ntile - 1), nxt);  // (past the last tile: a repeat)
     double Ef[kQPW][2][2], V[kQPW][2][2], AbT[kQPW][2][2];
     bool rbad[kQPW], nfb[kQPW];
+    uint64_t rbadm[kQPW];
     int zmin[kQPW];
 #pragma unroll
     for (int q = 0; q < kQPW; ++q) {
@@ -314,6 +315,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
         }
       double mabs = 0.0, rs = 0.0;
       bool nf = false;
+      uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
 #if VBHEM_EF_VALU
       // row sums of Ab (P layout: every lane row holds column 4J + c's sum), then
       // Ef = E + amax[sigma] rowsum(Ab)[beta] as one fma per element (the P layout's row
@@ -329,11 +331,21 @@ void fb_bwd4_kernel(const SplitArgs p) {
           const double e = cur.e[q][i2][jj];
           V[q][i2][jj] = e;
           Ef[q][i2][jj] = fma(amr, rsj[jj], e);
+#if VBHEM_RANGE_CMP
+          bigm |= ge_mask(fabs(e), vlim);
+          bigm |= ge_mask(fabs(Ef[q][i2][jj]), vlim);
+#else
           mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[q][i2][jj])));
+#endif
           nf |= !isfinite(Ef[q][i2][jj]);
         }
       }
+#if VBHEM_RANGE_CMP
+      bigm |= gt_mask(rsj[0], 1.0 + 1e-6);
+      bigm |= gt_mask(rsj[1], 1.0 + 1e-6);
+#else
       rs = fmax(rsj[0], rsj[1]);
+#endif
 #else
 #pragma unroll
       for (int i2 = 0; i2 < 2; ++i2)
@@ -351,7 +363,9 @@ void fb_bwd4_kernel(const SplitArgs p) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) rs = fmax(rs, mfma4(1.0, AbT[q][1][jj], mfma4(1.0, AbT[q][0][jj], 0.0)));
 #endif
+      // bigm (VBHEM_RANGE_CMP): the same test as a wave mask, joined at the ballot
       rbad[q] = !(mabs < vlim) || rs > 1.0 + 1e-6;
+      rbadm[q] = bigm;
       nfb[q] = nf;
       zmin[q] = 0x7fffffff;
     }
@@ -606,7 +620,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       y += shfl_xor_d(y, 1);
       y += shfl_xor_d(y, 2);
       y += shfl_xor_d(y, 16);
-      const bool pbad = (__ballot(bad) & pmask) != 0;
+      const bool pbad = ((__ballot(bad) | rbadm[q]) & pmask) != 0;
       const bool pnf = cl_nf || (__ballot(nfb[q]) & pmask) != 0;
       if (lane == 4 * b && r == 0 && i < p.i_end) {
         const size_t pair = (size_t)i * K + j;

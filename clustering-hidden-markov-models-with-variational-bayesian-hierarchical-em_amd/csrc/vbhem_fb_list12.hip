@@ -216,6 +216,7 @@ void fb_list12_kernel(const SplitArgs p) {
       }
     double mabs = 0.0, rs = 0.0;
     bool nfp = false;
+    uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
 #if VBHEM_EF_VALU
     // Ef = E + amax[sigma] rowsum(Ab)[beta]: one fma per element from the row sums
     // (fb_bwd12_kernel's VBHEM_EF_VALU; amQ holds the P rows 4I + r here)
@@ -226,7 +227,11 @@ void fb_list12_kernel(const SplitArgs p) {
 #pragma unroll
       for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
       rsj[jj] = x;
+#if VBHEM_RANGE_CMP
+      bigm |= gt_mask(x, 1.0 + 1e-6);
+#else
       rs = fmax(rs, x);
+#endif
     }
 #pragma unroll
     for (int i2 = 0; i2 < NB; ++i2)
@@ -236,7 +241,11 @@ void fb_list12_kernel(const SplitArgs p) {
         V[i2][jj] = e;
         const double ef = fma(amQ[i2], rsj[jj], e);
         Ef[i2][jj] = ef;
+#if VBHEM_RANGE_CMP
+        bigm |= ge_mask(fabs(e), vlim) | ge_mask(fabs(ef), vlim);
+#else
         mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
+#endif
         nfp |= !isfinite(ef);
       }
 #else
@@ -261,7 +270,7 @@ void fb_list12_kernel(const SplitArgs p) {
       rs = fmax(rs, x);
     }
 #endif
-    const bool rbad = !(mabs < vlim) || rs > 1.0 + 1e-6;
+    const bool rbad = lane_in(bigm) || !(mabs < vlim) || rs > 1.0 + 1e-6;
     int zmin = 0x7fffffff;
 
     // ---- K2: backward recursion (fb_bwd12_kernel's step), G_t kept for the forward ----

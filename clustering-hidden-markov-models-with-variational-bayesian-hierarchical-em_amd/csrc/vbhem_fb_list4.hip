@@ -214,6 +214,7 @@ void fb_list4_kernel(const SplitArgs p) {
       }
     double mabs = 0.0, rs = 0.0;
     bool nfp = false;
+    uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
 #if VBHEM_EF_VALU
     // Ef = E + amax[sigma] rowsum(Ab)[beta]: one fma per element from the row sums
     // (fb_bwd4_kernel's VBHEM_EF_VALU; amQ holds the P rows 4I + r here)
@@ -227,10 +228,18 @@ void fb_list4_kernel(const SplitArgs p) {
         const double e = cur.e[i2][jj];
         V[i2][jj] = e;
         Ef[i2][jj] = fma(amQ[i2], rsj[jj], e);
+#if VBHEM_RANGE_CMP
+        bigm |= ge_mask(fabs(e), vlim) | ge_mask(fabs(Ef[i2][jj]), vlim);
+#else
         mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[i2][jj])));
+#endif
         nfp |= !isfinite(Ef[i2][jj]);
       }
+#if VBHEM_RANGE_CMP
+    bigm |= gt_mask(rsj[0], 1.0 + 1e-6) | gt_mask(rsj[1], 1.0 + 1e-6);
+#else
     rs = fmax(rsj[0], rsj[1]);
+#endif
 #else
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
@@ -245,7 +254,7 @@ void fb_list4_kernel(const SplitArgs p) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) rs = fmax(rs, mfma4(1.0, AbT[1][jj], mfma4(1.0, AbT[0][jj], 0.0)));
 #endif
-    const bool rbad = !(mabs < vlim) || rs > 1.0 + 1e-6;
+    const bool rbad = lane_in(bigm) || !(mabs < vlim) || rs > 1.0 + 1e-6;
     int zmin = 0x7fffffff;
 
     // ---- K2: backward recursion (fb_bwd4_kernel's step), G_t kept for the forward ----

@@ -35,6 +35,23 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
+// VBHEM_RANGE_CMP: the per-tile range check (|E|, |Ef| < vlim, Ab row sums <= 1) as one
+// ordered compare per element into a wave mask instead of an fmax chain, which the
+// compiler emits with NaN canonicalisation (three maxes per pair) and, written as
+// per-lane compares, folds back into that chain.  Ordered, so a NaN element is skipped
+// exactly as fmax skips it.  fb_bwd4_kernel at C4: 1.252-1.264 vs 1.277-1.292 ms (4
+// interleaved repeats on one box, profiles/r05ax_ab_range_cmp.txt); C5 within noise
+#ifndef VBHEM_RANGE_CMP
+#define VBHEM_RANGE_CMP 1
+#endif
+__device__ __forceinline__ uint64_t ge_mask(double x, double lim) {
+  return __builtin_amdgcn_fcmp(x, lim, 3);  // FCMP_OGE
+}
+__device__ __forceinline__ uint64_t gt_mask(double x, double lim) {
+  return __builtin_amdgcn_fcmp(x, lim, 2);  // FCMP_OGT
+}
+__device__ __forceinline__ bool lane_in(uint64_t m) { return (m >> __lane_id()) & 1; }
+
 // s_waitcnt vmcnt(0) alone (expcnt 7, lgkmcnt 15 on gfx9), issued where the only vector
 // memory operations in flight are a prefetch that has had most of an item to land: the
 // compiler's own wait before the prefetched registers are copied would otherwise come
