@@ -160,10 +160,10 @@ void fb_bwd4_kernel(const SplitArgs p) {
   const int tid = threadIdx.x;
 #if VBHEM_BWD4_ETAB2
   stage_etab2(etab, tid, 64 * kNWB);
-  stage_log8k(ltab8, tid, 64 * kNWB);
+  stage_log8k<false>(ltab8, tid, 64 * kNWB);
 #elif VBHEM_BWD4_BIGLOG
   for (int x = tid; x < 2048; x += 64 * kNWB) etab[x] = kExpTab4[x] * 0x1p-1010;
-  stage_log8k(ltab8, tid, 64 * kNWB);
+  stage_log8k<false>(ltab8, tid, 64 * kNWB);
 #else
   stage_tables(etab, ltab, tid, 64 * kNWB);
 #endif
@@ -408,7 +408,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
       if constexpr (!ZS_)
         zmin[q] = min(zmin[q], min(min(__double2hiint(zf[0]), __double2hiint(zf[1])),
                                    min(__double2hiint(zf[2]), __double2hiint(zf[3]))));
-      log_q_n<4, true>(yf, zf, wqf, ltab8);
+      log_q_n<4, true, false>(yf, zf, wqf, ltab8);
 #pragma unroll
       for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -545,7 +545,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
                                        min(__double2hiint(zf[4 * q + 2]), __double2hiint(zf[4 * q + 3]))));
         }
 #if VBHEM_BWD4_BIGLOG
-        log_q_n<NE, VBHEM_BWD4_DECOUPLE != 0>(yf, zf, wqf, ltab8);
+        log_q_n<NE, VBHEM_BWD4_DECOUPLE != 0, false>(yf, zf, wqf, ltab8);
 #elif VBHEM_BWD4_DECOUPLE
         log_d_n<NE>(yf, zf, wqf, ltab);
 #else
@@ -607,7 +607,7 @@ void fb_bwd4_kernel(const SplitArgs p) {
         const double zsf[1] = {zs};
         const int wqf[1] = {(int)(w + kWq0)};
 #if VBHEM_BWD4_BIGLOG
-        log_q_n<1, false>(lse1, zsf, wqf, ltab8);
+        log_q_n<1, false, false>(lse1, zsf, wqf, ltab8);
 #else
         log_m_n<1>(lse1, zsf, wqf, ltab);
 #endif

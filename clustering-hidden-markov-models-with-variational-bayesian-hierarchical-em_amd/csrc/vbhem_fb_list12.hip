@@ -85,7 +85,7 @@ void fb_list12_kernel(const SplitArgs p) {
   __shared__ int tots[kList4MaxK];     // the gate lists' lengths
   const int tid = threadIdx.x;
   for (int x = tid; x < 2048; x += 64 * kL12NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
-  stage_log8k(ltab8, tid, 64 * kL12NWB);
+  stage_log8k<false>(ltab8, tid, 64 * kL12NWB);
   const int K = p.K, SB = FAST ? 12 : p.SB;
   using off_t_ = typename std::conditional<FAST, unsigned, size_t>::type;
   auto ld = [](const double *base, off_t_ x) {
@@ -330,7 +330,7 @@ void fb_list12_kernel(const SplitArgs p) {
         }
 #pragma unroll
         for (int x = 0; x < NE; ++x) zmin = min(zmin, __double2hiint(zf[x]));
-        log_q_n<NE, true>(yf, zf, wqf, ltab8);
+        log_q_n<NE, true, false>(yf, zf, wqf, ltab8);
 #pragma unroll
         for (int x = 0; x < NE; ++x) sv[x / NB][x % NB] = yf[x];
       }
@@ -382,7 +382,7 @@ void fb_list12_kernel(const SplitArgs p) {
         const double zsf[1] = {rowsum_all12(ef[jj] + ef[NB + jj] + ef[2 * NB + jj])};
         const int wqf[1] = {(int)(wc[jj] + kWq0)};
         double l1[1];
-        log_q_n<1, false>(l1, zsf, wqf, ltab8);
+        log_q_n<1, false, false>(l1, zsf, wqf, ltab8);
         lse[jj] = l1[0];
         bad |= !isfinite(l1[0]);
       }

@@ -205,18 +205,38 @@ __device__ __forceinline__ void stage_tables(double *etab, double *ltab, int tid
 // logs (scripts/gen_log_table.py) and copied into each block's LDS: 16-byte loads from
 // L2 instead of a division and a libm log per entry (computing it took ~6 us of every
 // fb_bwd4_kernel launch, profiles/r05ah_ab_shard_cheap_stage.txt)
+// VBHEM_LOG_FREXP: log_q_n's mantissa as v_frexp_mant_f64 in [1/2, 1) against a staged
+// 2/c (both scalings exact, so the same r bit for bit) instead of inserting the exponent
+// of 1.0 into Z's high word, which costs a v_bfi_b32 and, as the compiler allocates it,
+// a v_mov_b32 for the low word.  fb_bwd12_kernel: step 226 -> 216 VALU, 4.79 -> 4.74 ms per
+// C5 group (profiles/r05ay_ab_log_frexp.txt).  FX = false keeps the old form where it did
+// not pay: fb_bwd4_kernel (step 104 -> 99 VALU, but 1.266 -> 1.272 ms at C4, within noise)
+// and fb_list12_kernel (the extra live register spills)
+#ifndef VBHEM_LOG_FREXP
+#define VBHEM_LOG_FREXP 1
+#endif
+constexpr bool kLogFrexp = VBHEM_LOG_FREXP != 0;
+
+template <bool FX = kLogFrexp>
 __device__ __forceinline__ void stage_log8k(double *ltab, int tid, int nt) {
   const double2 *src = reinterpret_cast<const double2 *>(kLogTab8k);
   double2 *dst = reinterpret_cast<double2 *>(ltab);
   // (unrolled: a 4-wave block's 32 copies per thread go out in two batches, not one
   // memory latency after another)
 #pragma unroll 16
-  for (int k = tid; k < 8192; k += nt) dst[k] = src[k];
+  for (int k = tid; k < 8192; k += nt) {
+    if constexpr (FX) {
+      const double2 v = src[k];
+      dst[k] = make_double2(2.0 * v.x, v.y);  // 2/c: log_q_n's mantissa is in [1/2, 1)
+    } else {
+      dst[k] = src[k];
+    }
+  }
 }
 
 // log(Z) + M, 8192-interval table, log1p(r) = r - r^2/2 (|r| <= 2^-14): kk = the
 // binary exponent of Z plus the maximum's term (integer, exact), then one fma
-template <int N, bool DEC>
+template <int N, bool DEC, bool FX = kLogFrexp>
 __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
                                         const double *ltab) {
   double zz[N], ic[N], w[N];
@@ -229,7 +249,10 @@ __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], co
     unsigned ex = hi >> 20;
     asm("" : "+v"(ex));
     const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
-    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    if constexpr (FX)
+      zz[x] = __builtin_amdgcn_frexp_mant(z[x]);
+    else
+      zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
 #ifdef VBHEM_ABL_NOLTAB  // ablation (timing only, wrong results): no log table read
     const double2 e = {1.0, 0.0};
 #else
