@@ -360,6 +360,33 @@ def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch, S):
     assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
+@pytest.mark.parametrize("shift", [8.0e5, -8.0e5])
+@pytest.mark.parametrize("S", [8, 12])
+def test_range_check_mfma_kernels(vb, vo, S, shift):
+    """Cluster 0's emission constants shifted by |shift| > the kernels' |V| limit (7e5):
+    no underflow, only the per-tile range check (|E|, |Ef| >= vlim as ordered compare
+    masks, VBHEM_RANGE_CMP) flags its pairs in the MFMA kernels (fb_bwd4_kernel /
+    fb_bwd12_kernel, and the list kernels when the cluster is gated), and the exact
+    fallback must give the oracle's numbers."""
+    N, K, d = 41, 2, 3
+    cs = make_case(N, K, S, S, d, 1, seed=7, tau=10)
+    consts = {k: np.array(v, copy=True) for k, v in cs["consts"].items()}
+    consts["c"][0] += shift
+    base, T = cs["base"], cs["T"]
+    pairs = vo.c_estep_pairs(base, consts, T)
+    assert np.isfinite(pairs["LL_elbo"]).all()
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, pairs, 1)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
+    assert eng.fallback_count() >= N  # every pair of cluster 0 failed the range check
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, k
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
 def test_host_pointer_entry_point(vb, vo, capi_lib):
     """vbhem_estep_pairs_host (what the MEX gateway calls): host arrays in/out."""
     from vbhem_amd import _capi
