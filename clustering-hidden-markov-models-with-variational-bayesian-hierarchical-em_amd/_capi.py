@@ -104,6 +104,7 @@ EXPORTS = {
     "vbhem_timing_read_em_math": (_c_int, [ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_longlong)]),
     "vbhem_set_fused_mode": (_c_int, [_c_int]),
+    "vbhem_debug_extra_lds": (_c_size, [_c_size]),
     "vbhem_em_prelude": (_c_int, [ctypes.POINTER(PostT), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "vbhem_em_lower_bound": (_c_int, [ctypes.POINTER(PostT), ctypes.POINTER(EmOptT), _vp, _vp,
                                       _vp, _vp, _vp, ctypes.POINTER(ctypes.c_double)]),

@@ -173,11 +173,29 @@ def vbhem_h3m_cluster(hmms: list, K, S, opt: Optional[dict] = None, device="cuda
     o = default_options(Ks[0], Ss[0], base.d, **{k: v for k, v in opt.items()
                                                   if k not in ("K", "S")})
     if o.get("initmode") == "auto":
-        # vbhem_h3m_cluster.m:359-395: every initialisation in turn, the best bound wins
-        modes = list(o.get("initmodes", ["baseem", "gmmNew", "wtkmeans"]))
-        runs = [vbhem_h3m_c(base, dict(o, initmode=m), device, engine_factory) for m in modes]
+        # vbhem_h3m_cluster.m:359-395: every initialisation in turn, each with its own
+        # initopt.mode (opt['initmodes'] with opt['initopts'], default {'baseem', 'gmmNew',
+        # 'wtkmeans'} with {'u', 'r0', 'r0'}), the best bound wins; keep_best_random_trial
+        # (default 1, :208) keeps every mode's run as h3m_out_trials (:391-393).  The
+        # 'wtkmeans' / 'gmmNew' centres come from a k-means++ stand-in for MATLAB's kmeans,
+        # so which mode wins is parity unpinned.
+        if "initmodes" in o:
+            modes = list(o["initmodes"])
+            if "initopts" not in o or len(o["initopts"]) != len(modes):
+                raise ValueError("opt['initmodes'] needs opt['initopts'] of the same length "
+                                 "(vbhem_h3m_cluster.m:366-368)")
+            iopts = list(o["initopts"])
+        else:
+            modes, iopts = ["baseem", "gmmNew", "wtkmeans"], ["u", "r0", "r0"]
+        runs = []
+        for m, io in zip(modes, iopts):
+            r = vbhem_h3m_c(base, dict(o, initmode=m, initopt_mode=io), device, engine_factory)
+            runs.append(dict(r, Initmodes=m))
         ind = int(np.argmax([r["LL"] for r in runs]))
         out = dict(runs[ind])
         out.update(initmode=modes[ind], init_trials_LL=[r["LL"] for r in runs])
+        if o.get("keep_best_random_trial", 1):
+            out["h3m_out_trials"] = runs
+        out["LL_orignal"] = out["LL"]   # (sic, :398)
         return out
     return vbhem_h3m_c(base, o, device, engine_factory)

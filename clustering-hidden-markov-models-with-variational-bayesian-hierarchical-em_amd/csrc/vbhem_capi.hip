@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -21,6 +22,9 @@
 #include "vbhem_internal.h"
 #include "vbhem_exact.h"
 #include "vbhem_math.h"
+
+// the fault-injection hook of vbhem_debug_extra_lds (tests only; 0 in production)
+static std::atomic<size_t> g_debug_extra_lds{0};
 
 namespace {
 
@@ -415,8 +419,8 @@ size_t carve_fused(void *ws, const vbhem_base_t *b, const vbhem_cluster_t *c, in
   w.gate_cnt = cv.take<int>((size_t)w.nslab * K);
   w.list = cv.take<int>(g * K);
   w.list_tot = cv.take<int>((size_t)K);
-  // A' [K][S][S], then [K][S] the row maxima of logA (fb_bwd4_kernel writes them)
-  w.Atg = cv.take<double>((size_t)K * S * S + (size_t)K * S);
+  // A' [K][S][S] (read-only for every recursion kernel)
+  w.Atg = cv.take<double>((size_t)K * S * S);
   // the exact fallback's scratch last: its size does not move the hot buffers
   w.scratch = cv.take<double>(exact_stride(S, SB, T) * kExactThreads);
   return cv.off + 256;
@@ -709,10 +713,9 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
                                       std::max(1, vbhem::bwd2_resident_blocks(ca.S, ca.nwb, c.bwd2_lds)));
       unsigned nb = std::max(1u, std::min(nt2, all / (unsigned)ca.K));
       if (nb >= 8) nb = nb / 8 * 8;
-      // VBHEM_DEBUG_EXTRA_LDS=n: n more bytes of dynamic LDS -- fault injection for the
+      // vbhem_debug_extra_lds(n): n more bytes of dynamic LDS -- fault injection for the
       // tests of a refused launch (tests/test_robustness.py), never set in production
-      const char *xl = std::getenv("VBHEM_DEBUG_EXTRA_LDS");
-      const size_t lds2 = c.bwd2_lds + (xl ? (size_t)std::strtoull(xl, nullptr, 10) : 0);
+      const size_t lds2 = c.bwd2_lds + g_debug_extra_lds.load(std::memory_order_relaxed);
       e = vbhem::launch_bwd2(ca, (unsigned)ca.K * nb, lds2, st, ev1 ? ev0 : nullptr, ev1);
       if (e != hipSuccess) return hip_fail(e, "fb_bwd2_kernel");
       g_last_kernel[0] = "vbhem::fb_bwd2_kernel<" + std::to_string(ca.S) + ">";
@@ -751,6 +754,8 @@ int run_fb(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *LL, doubl
 extern "C" {
 
 const char *vbhem_last_error(void) { return g_err.c_str(); }
+
+size_t vbhem_debug_extra_lds(size_t bytes) { return g_debug_extra_lds.exchange(bytes); }
 
 const char *vbhem_last_kernel(int pass) {
   return (pass == 0 || pass == 1) ? g_last_kernel[pass].c_str() : "";

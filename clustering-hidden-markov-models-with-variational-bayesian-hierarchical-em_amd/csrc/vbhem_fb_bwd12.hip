@@ -16,9 +16,10 @@
 // the VALU keeps the exp and the log of every element (9 per lane) and the maxima.
 // Column maxima: blocks J = 0, 1 as fb_bwd4_kernel (one permlane16 / permlane32 pair
 // reduces both, row r then holds block r & 1), block J = 2 by its own full row
-// reduction.  The exp / log are fb_bwd4_kernel's round-4 ones: maxima
-// rounded to a multiple of ln 2 (the exp table index independent of the maximum), the
-// 8192-interval log table with a second-order log1p; the tables take 144 KB of LDS,
+// reduction.  The exp / log are fb_bwd4_kernel's: maxima rounded to a
+// multiple of ln 2 (the exp table index independent of the maximum), the 8192-interval
+// log table with a second-order log1p and the exponent applied to the table's 1/c
+// (round 6, vbhem_mfma4.h); the tables take 144 KB of LDS,
 // one block per CU, two waves per SIMD, each with its next tile's inputs in flight
 // (as fb_bwd4_kernel).  Underflow / range / non-finite handling as fb_bwd4_kernel: a pair
 // whose inputs could leave the integer range of the maxima, or whose Z underflowed,
@@ -40,11 +41,6 @@
 // 3 waves without the prefetch 5.10-5.13 ms (84 bytes of scratch), 3 with it 5.72
 // (284 bytes), 2 without it 5.37-5.40, 2 with it 4.93-4.96
 #define VBHEM_BWD12_WAVES 2
-#endif
-
-// VBHEM_EF_VALU: Ef from the row sums by one fma per element (fb_bwd4_kernel's switch)
-#ifndef VBHEM_EF_VALU
-#define VBHEM_EF_VALU 1
 #endif
 
 namespace vbhem {
@@ -85,11 +81,11 @@ void fb_bwd12_kernel(const SplitArgs p) {
   // one array, the exp table first: both tables' LDS offsets fit ds_read's offset field
   __shared__ __attribute__((aligned(16))) double tabs[2048 + 2 * 8192];
   double *const etab = tabs;           // 2^(i/2048 - 1010)
-  double *const ltab8 = tabs + 2048;   // {1/c, -log(1/c)}
+  double *const ltab8 = tabs + 2048;   // {2^1023/c, -log(1/c)} (stage_log8k_x)
   __shared__ double amax[S], lpi[S];
   const int tid = threadIdx.x;
   for (int x = tid; x < 2048; x += 64 * kNWB12) etab[x] = kExpTab4[x] * 0x1p-1010;
-  stage_log8k(ltab8, tid, 64 * kNWB12);
+  stage_log8k_x(ltab8, tid, 64 * kNWB12);
   const int SB = p.SB, K = p.K, T = p.T;
   // persistent: NB blocks per cluster; XCD-aware when NBk % 8 == 0 (as fb_bwd4_kernel)
   const int bk = blockIdx.x, NBk = (int)gridDim.x / K;
@@ -191,7 +187,6 @@ void fb_bwd12_kernel(const SplitArgs p) {
     for (int tile = wave * NBk + t0; tile < ntile; tile += tstride) {
       const int i0 = p.i_begin + tile * 4;
       const int i = i0 + b;
-      const int ic = i < p.i_end ? i : p.i_end - 1;
       TileIn nxt;
       load_tile(min(tile + tstride, ntile - 1), nxt);  // (past the last tile: a repeat)
       double Ef[NB][NB], V[NB][NB], AbT[NB][NB];
@@ -203,25 +198,19 @@ void fb_bwd12_kernel(const SplitArgs p) {
           const int be = 4 * jj + c, bp = 4 * j2 + r;
           AbT[j2][jj] = (be < SBk && bp < SBk) ? cur.a[j2][jj] : 0.0;
         }
-      double mabs = 0.0;
       bool nf = false;
-      uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
-#if VBHEM_EF_VALU
+      uint64_t bigm = 0;  // the lanes failing the range check
       // row sums of Ab first (P layout: column 4J + c's sum in every lane row), then
-      // Ef = E + amax[sigma] rowsum(Ab)[beta] as one fma per element (row sigma = 4I + r)
-      // instead of NB MFMAs
-      double rsj[NB], rs = 0.0;  // (the |V| bound assumes row sums <= 1)
+      // Ef = E + amax[sigma] rowsum(Ab)[beta] as one fma per element (row sigma = 4I + r);
+      // the range check (|E|, |Ef| < vlim, row sums <= 1) as ordered compares into a mask
+      double rsj[NB];
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj) {
         double x = 0.0;
 #pragma unroll
         for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
         rsj[jj] = x;
-#if VBHEM_RANGE_CMP
         bigm |= gt_mask(x, 1.0 + 1e-6);
-#else
-        rs = fmax(rs, x);
-#endif
       }
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2) {
@@ -232,40 +221,11 @@ void fb_bwd12_kernel(const SplitArgs p) {
           V[i2][jj] = e;
           const double ef = fma(amr, rsj[jj], e);
           Ef[i2][jj] = ef;
-#if VBHEM_RANGE_CMP
           bigm |= ge_mask(fabs(e), vlim) | ge_mask(fabs(ef), vlim);
-#else
-          mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
-#endif
           nf |= !isfinite(ef);
         }
       }
-#else
-#pragma unroll
-      for (int i2 = 0; i2 < NB; ++i2)
-#pragma unroll
-        for (int jj = 0; jj < NB; ++jj) {
-          const double e = cur.e[i2][jj];
-          V[i2][jj] = e;
-          // Ef = E + amax[sigma] sum_b' Ab[beta][b'] on the matrix cores
-          const double am = amax[4 * i2 + c];
-          double ef = e;
-#pragma unroll
-          for (int k2 = 0; k2 < NB; ++k2) ef = mfma4(am, AbT[k2][jj], ef);
-          Ef[i2][jj] = ef;
-          mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
-          nf |= !isfinite(ef);
-        }
-      double rs = 0.0;  // row sums of Ab (the |V| bound assumes <= 1)
-#pragma unroll
-      for (int jj = 0; jj < NB; ++jj) {
-        double x = 0.0;
-#pragma unroll
-        for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
-        rs = fmax(rs, x);
-      }
-#endif
-      const bool rbad = lane_in(bigm) || !(mabs < vlim) || rs > 1.0 + 1e-6;
+      const bool rbad = lane_in(bigm);
       int zmin = 0x7fffffff;
 
       // ---- K2: backward recursion, t = T-1 .. 1 ----
@@ -275,8 +235,9 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
         for (int x = 0; x < NE; ++x) sf[x] = red_s(V[x / NB][x % NB]);
         // the exp table values need no maximum: their reads go out first
+        const unsigned emsk = etab_mask();
 #pragma unroll
-        for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, sf[x]);
+        for (int x = 0; x < NE; ++x) tv[x] = etab_atm(etab, sf[x], emsk);
         unsigned xm[NB];
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj)
@@ -331,7 +292,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
             for (int x = 0; x < NE; ++x) zmin = min(zmin, __double2hiint(zf[x]));
           }
-          log_q_n<NE, true>(yf, zf, wqf, ltab8);
+          log_x_n<NE, true>(yf, zf, wqf, ltab8);
 #pragma unroll
           for (int x = 0; x < NE; ++x) sv[x / NB][x % NB] = yf[x];
         }
@@ -388,7 +349,7 @@ void fb_bwd12_kernel(const SplitArgs p) {
           double lse1[1];
           const double zsf[1] = {zs};
           const int wqf[1] = {(int)(wc[jj] + kWq0)};
-          log_q_n<1, false>(lse1, zsf, wqf, ltab8);
+          log_x_n<1, false>(lse1, zsf, wqf, ltab8);
           const int be = 4 * jj + c;
           const double pr = be < SBk ? cur.pr[jj] : 0.0;
           y += pr * lse1[0];

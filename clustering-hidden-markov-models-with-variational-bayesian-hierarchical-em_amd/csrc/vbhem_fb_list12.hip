@@ -30,10 +30,6 @@
 #include "vbhem_math.h"
 #include "vbhem_mfma4.h"
 
-// VBHEM_EF_VALU: Ef from the row sums by one fma per element (fb_bwd4_kernel's switch)
-#ifndef VBHEM_EF_VALU
-#define VBHEM_EF_VALU 1
-#endif
 
 namespace vbhem {
 
@@ -85,7 +81,7 @@ void fb_list12_kernel(const SplitArgs p) {
   __shared__ int tots[kList4MaxK];     // the gate lists' lengths
   const int tid = threadIdx.x;
   for (int x = tid; x < 2048; x += 64 * kL12NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
-  stage_log8k<false>(ltab8, tid, 64 * kL12NWB);
+  stage_log8k(ltab8, tid, 64 * kL12NWB);
   const int K = p.K, SB = FAST ? 12 : p.SB;
   using off_t_ = typename std::conditional<FAST, unsigned, size_t>::type;
   auto ld = [](const double *base, off_t_ x) {
@@ -185,11 +181,7 @@ void fb_list12_kernel(const SplitArgs p) {
         for (int y = 0; y < NB; ++y) AT[x][y] = At[(4 * y + c) * S + 4 * x + r];
 #pragma unroll
       for (int i2 = 0; i2 < NB; ++i2) {
-#if VBHEM_EF_VALU
         const double *la = p.logA + ((size_t)j * S + 4 * i2 + r) * S;  // (P rows: the fma below)
-#else
-        const double *la = p.logA + ((size_t)j * S + 4 * i2 + c) * S;
-#endif
         double mx = la[0];
 #pragma unroll
         for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
@@ -214,12 +206,10 @@ void fb_list12_kernel(const SplitArgs p) {
         const int be = 4 * jj + c, bp = 4 * j2 + r;
         AbT[j2][jj] = (be < SB && bp < SB) ? cur.ab[j2][jj] : 0.0;
       }
-    double mabs = 0.0, rs = 0.0;
     bool nfp = false;
-    uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
-#if VBHEM_EF_VALU
+    uint64_t bigm = 0;  // the lanes failing the range check (ordered compares into a mask)
     // Ef = E + amax[sigma] rowsum(Ab)[beta]: one fma per element from the row sums
-    // (fb_bwd12_kernel's VBHEM_EF_VALU; amQ holds the P rows 4I + r here)
+    // (as fb_bwd12_kernel; amQ holds the P rows 4I + r here)
     double rsj[NB];
 #pragma unroll
     for (int jj = 0; jj < NB; ++jj) {
@@ -227,11 +217,7 @@ void fb_list12_kernel(const SplitArgs p) {
 #pragma unroll
       for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
       rsj[jj] = x;
-#if VBHEM_RANGE_CMP
       bigm |= gt_mask(x, 1.0 + 1e-6);
-#else
-      rs = fmax(rs, x);
-#endif
     }
 #pragma unroll
     for (int i2 = 0; i2 < NB; ++i2)
@@ -241,47 +227,24 @@ void fb_list12_kernel(const SplitArgs p) {
         V[i2][jj] = e;
         const double ef = fma(amQ[i2], rsj[jj], e);
         Ef[i2][jj] = ef;
-#if VBHEM_RANGE_CMP
         bigm |= ge_mask(fabs(e), vlim) | ge_mask(fabs(ef), vlim);
-#else
-        mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
-#endif
         nfp |= !isfinite(ef);
       }
-#else
-#pragma unroll
-    for (int i2 = 0; i2 < NB; ++i2)
-#pragma unroll
-      for (int jj = 0; jj < NB; ++jj) {
-        const double e = cur.e[i2][jj];
-        V[i2][jj] = e;
-        double ef = e;
-#pragma unroll
-        for (int k2 = 0; k2 < NB; ++k2) ef = mfma4(amQ[i2], AbT[k2][jj], ef);
-        Ef[i2][jj] = ef;
-        mabs = fmax(mabs, fmax(fabs(e), fabs(ef)));
-        nfp |= !isfinite(ef);
-      }
-#pragma unroll
-    for (int jj = 0; jj < NB; ++jj) {
-      double x = 0.0;
-#pragma unroll
-      for (int k2 = 0; k2 < NB; ++k2) x = mfma4(1.0, AbT[k2][jj], x);
-      rs = fmax(rs, x);
-    }
-#endif
-    const bool rbad = lane_in(bigm) || !(mabs < vlim) || rs > 1.0 + 1e-6;
+    const bool rbad = lane_in(bigm);
     int zmin = 0x7fffffff;
 
     // ---- K2: backward recursion (fb_bwd12_kernel's step), G_t kept for the forward ----
+    // (the log keeps log_q_n's form on the unscaled table: with fb_bwd12_kernel's
+    // log_x_n this kernel, at one wave per SIMD and 512 registers, spilled 92 bytes)
     double lat[T][NB][NB];
 #pragma unroll
     for (int t = T - 1; t >= 1; --t) {
       double sf[NE], tv[NE];
 #pragma unroll
       for (int x = 0; x < NE; ++x) sf[x] = red_s(V[x / NB][x % NB]);
+      const unsigned emsk = etab_mask();
 #pragma unroll
-      for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, sf[x]);
+      for (int x = 0; x < NE; ++x) tv[x] = etab_atm(etab, sf[x], emsk);
       unsigned xm[NB];
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj)
@@ -330,7 +293,7 @@ void fb_list12_kernel(const SplitArgs p) {
         }
 #pragma unroll
         for (int x = 0; x < NE; ++x) zmin = min(zmin, __double2hiint(zf[x]));
-        log_q_n<NE, true, false>(yf, zf, wqf, ltab8);
+        log_q_n<NE, true>(yf, zf, wqf, ltab8);
 #pragma unroll
         for (int x = 0; x < NE; ++x) sv[x / NB][x % NB] = yf[x];
       }
@@ -382,7 +345,7 @@ void fb_list12_kernel(const SplitArgs p) {
         const double zsf[1] = {rowsum_all12(ef[jj] + ef[NB + jj] + ef[2 * NB + jj])};
         const int wqf[1] = {(int)(wc[jj] + kWq0)};
         double l1[1];
-        log_q_n<1, false, false>(l1, zsf, wqf, ltab8);
+        log_q_n<1, false>(l1, zsf, wqf, ltab8);
         lse[jj] = l1[0];
         bad |= !isfinite(l1[0]);
       }

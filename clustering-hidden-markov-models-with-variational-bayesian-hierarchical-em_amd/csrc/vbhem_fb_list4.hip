@@ -34,24 +34,17 @@
 #include "vbhem_math.h"
 #include "vbhem_mfma4.h"
 
-// VBHEM_LIST4_R4: the backward half with fb_bwd4_kernel's round-4 step (the exp table
-// index decoupled from the column maxima, the 8192-interval log table: 144 KB of LDS,
-// one 8-wave block per CU) -- A/B switch
-#ifndef VBHEM_LIST4_R4
-#define VBHEM_LIST4_R4 0
-#endif
-
-// VBHEM_EF_VALU: Ef from the row sums by one fma per element (fb_bwd4_kernel's switch)
-#ifndef VBHEM_EF_VALU
-#define VBHEM_EF_VALU 1
-#endif
+// (The backward half keeps the round-3 step on 32 KB of tables -- 2^(j/2048) and the
+// 1024-interval log -- two 4-wave blocks per CU: fb_bwd4_kernel's larger-table step
+// measured no gain here, 0.242 vs 0.244 ms at C4 (profiles/r04e_ab_l4r4_c4.txt), since
+// the forward sweep sets this kernel's time.)
 
 namespace vbhem {
 
 namespace {
 using namespace m4;
 constexpr int kL4Waves = 2;   // waves per SIMD (the lattice is 72 VGPRs)
-constexpr int kL4NWB = VBHEM_LIST4_R4 ? 8 : 4;   // waves per block
+constexpr int kL4NWB = 4;    // waves per block
 constexpr int kL4T = 10;      // the tau this kernel is built for (C3 - C5)
 }  // namespace
 
@@ -61,22 +54,12 @@ template <int T, bool FAST>
 __global__ __launch_bounds__(64 * kL4NWB) __attribute__((amdgpu_waves_per_eu(kL4Waves)))
 void fb_list4_kernel(const SplitArgs p) {
   constexpr int S = 8;
-#if VBHEM_LIST4_R4
-  __shared__ __attribute__((aligned(16))) double tabs[2048 + 2 * 8192];
-  double *const etab = tabs, *const ltab8 = tabs + 2048;
-#else
   __shared__ __attribute__((aligned(16))) double etab[2048];
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];
-#endif
   __shared__ int pre[kList4MaxK + 1];  // first quad item of every cluster
   __shared__ int tots[kList4MaxK];     // the gate lists' lengths
   const int tid = threadIdx.x;
-#if VBHEM_LIST4_R4
-  for (int x = tid; x < 2048; x += 64 * kL4NWB) etab[x] = kExpTab4[x] * 0x1p-1010;
-  stage_log8k(ltab8, tid, 64 * kL4NWB);
-#else
   stage_tables(etab, ltab, tid, 64 * kL4NWB);
-#endif
   const int K = p.K, SB = FAST ? 8 : p.SB;
   using off_t_ = typename std::conditional<FAST, unsigned, size_t>::type;
   auto ld = [](const double *base, off_t_ x) {
@@ -183,11 +166,7 @@ void fb_list4_kernel(const SplitArgs p) {
         }
 #pragma unroll
       for (int i2 = 0; i2 < 2; ++i2) {
-#if VBHEM_EF_VALU
         const double *la = p.logA + ((size_t)j * S + 4 * i2 + r) * S;  // (P rows: the fma below)
-#else
-        const double *la = p.logA + ((size_t)j * S + 4 * i2 + c) * S;
-#endif
         double mx = la[0];
 #pragma unroll
         for (int s2 = 1; s2 < S; ++s2) mx = fmax(mx, la[s2]);
@@ -212,12 +191,10 @@ void fb_list4_kernel(const SplitArgs p) {
         const int be = 4 * jj + c, bp = 4 * j2 + r;
         AbT[j2][jj] = (be < SB && bp < SB) ? cur.ab[j2][jj] : 0.0;
       }
-    double mabs = 0.0, rs = 0.0;
     bool nfp = false;
-    uint64_t bigm = 0;  // VBHEM_RANGE_CMP: the lanes failing the range check
-#if VBHEM_EF_VALU
+    uint64_t bigm = 0;  // the lanes failing the range check (ordered compares into a mask)
     // Ef = E + amax[sigma] rowsum(Ab)[beta]: one fma per element from the row sums
-    // (fb_bwd4_kernel's VBHEM_EF_VALU; amQ holds the P rows 4I + r here)
+    // (as fb_bwd4_kernel; amQ holds the P rows 4I + r here)
     double rsj[2];
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) rsj[jj] = mfma4(1.0, AbT[1][jj], mfma4(1.0, AbT[0][jj], 0.0));
@@ -228,36 +205,14 @@ void fb_list4_kernel(const SplitArgs p) {
         const double e = cur.e[i2][jj];
         V[i2][jj] = e;
         Ef[i2][jj] = fma(amQ[i2], rsj[jj], e);
-#if VBHEM_RANGE_CMP
         bigm |= ge_mask(fabs(e), vlim) | ge_mask(fabs(Ef[i2][jj]), vlim);
-#else
-        mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[i2][jj])));
-#endif
         nfp |= !isfinite(Ef[i2][jj]);
       }
-#if VBHEM_RANGE_CMP
     bigm |= gt_mask(rsj[0], 1.0 + 1e-6) | gt_mask(rsj[1], 1.0 + 1e-6);
-#else
-    rs = fmax(rsj[0], rsj[1]);
-#endif
-#else
-#pragma unroll
-    for (int i2 = 0; i2 < 2; ++i2)
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const double e = cur.e[i2][jj];
-        V[i2][jj] = e;
-        Ef[i2][jj] = mfma4(amQ[i2], AbT[1][jj], mfma4(amQ[i2], AbT[0][jj], e));
-        mabs = fmax(mabs, fmax(fabs(e), fabs(Ef[i2][jj])));
-        nfp |= !isfinite(Ef[i2][jj]);
-      }
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) rs = fmax(rs, mfma4(1.0, AbT[1][jj], mfma4(1.0, AbT[0][jj], 0.0)));
-#endif
-    const bool rbad = lane_in(bigm) || !(mabs < vlim) || rs > 1.0 + 1e-6;
+    const bool rbad = lane_in(bigm);
     int zmin = 0x7fffffff;
 
-    // ---- K2: backward recursion (fb_bwd4_kernel's step), G_t kept for the forward ----
+    // ---- K2: backward recursion (fb_bwd4_kernel's round-3 step), G_t kept for the forward ----
     double lat[T][2][2];
 #pragma unroll
     for (int t = T - 1; t >= 1; --t) {
@@ -266,24 +221,6 @@ void fb_list4_kernel(const SplitArgs p) {
       for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) s[i2][jj] = red_s(V[i2][jj]);
-#if VBHEM_LIST4_R4
-      const double sf[4] = {s[0][0], s[0][1], s[1][0], s[1][1]};
-      double tv[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) tv[x] = etab_at(etab, sf[x]);
-      const unsigned w = colmax_rows(max(lo_u(s[0][0]), lo_u(s[1][0])), max(lo_u(s[0][1]), lo_u(s[1][1]))) >> 11;
-      const int wq = (int)w - (1 << 20) - 1023;
-      const int mq[2] = {__builtin_amdgcn_ds_bpermute(qsrc0, wq), __builtin_amdgcn_ds_bpermute(qsrc1, wq)};
-      unsigned wp[2];
-      split_rows(w - 1010u, wp[0], wp[1]);
-      {
-        const double vf[4] = {V[0][0], V[0][1], V[1][0], V[1][1]};
-        const unsigned wpf[4] = {wp[0], wp[1], wp[0], wp[1]};
-        double gf[4];
-        exp_d_n<4>(gf, vf, sf, tv, wpf);
-        lat[t][0][0] = gf[0]; lat[t][0][1] = gf[1]; lat[t][1][0] = gf[2]; lat[t][1][1] = gf[3];
-      }
-#else
       const unsigned w = colmax_rows(max(lo_u(s[0][0]), lo_u(s[1][0])), max(lo_u(s[0][1]), lo_u(s[1][1])));
       const int wq = (int)(w + kWq0);
       const int mq[2] = {__builtin_amdgcn_ds_bpermute(qsrc0, wq), __builtin_amdgcn_ds_bpermute(qsrc1, wq)};
@@ -297,7 +234,6 @@ void fb_list4_kernel(const SplitArgs p) {
         exp_m_n<4>(gf, vf, sf, wpf, etab);
         lat[t][0][0] = gf[0]; lat[t][0][1] = gf[1]; lat[t][1][0] = gf[2]; lat[t][1][1] = gf[3];
       }
-#endif
       double z[4];
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
@@ -309,11 +245,7 @@ void fb_list4_kernel(const SplitArgs p) {
       double svf[4];
       {
         const int wqf[4] = {mq[0], mq[0], mq[1], mq[1]};
-#if VBHEM_LIST4_R4
-        log_q_n<4, true>(svf, z, wqf, ltab8);
-#else
         log_m_n<4>(svf, z, wqf, ltab);
-#endif
       }
       // sv(I, J') is Z^T's block (J', I) = svf[2 J' + I]
 #pragma unroll
@@ -351,11 +283,7 @@ void fb_list4_kernel(const SplitArgs p) {
       {
         const double zsf[1] = {zs};
         const int wqf[1] = {(int)(w + kWq0)};
-#if VBHEM_LIST4_R4
-        log_q_n<1, false>(lser, zsf, wqf, ltab8);
-#else
         log_m_n<1>(lser, zsf, wqf, ltab);
-#endif
       }
       bad = zmin < kZMinHi || rbad || !isfinite(lser[0]);
       const auto sl = __builtin_amdgcn_permlane16_swap(lo_u(lser[0]), lo_u(lser[0]), false, false);

@@ -35,15 +35,12 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
-// VBHEM_RANGE_CMP: the per-tile range check (|E|, |Ef| < vlim, Ab row sums <= 1) as one
-// ordered compare per element into a wave mask instead of an fmax chain, which the
-// compiler emits with NaN canonicalisation (three maxes per pair) and, written as
-// per-lane compares, folds back into that chain.  Ordered, so a NaN element is skipped
-// exactly as fmax skips it.  fb_bwd4_kernel at C4: 1.252-1.264 vs 1.277-1.292 ms (4
-// interleaved repeats on one box, profiles/r05ax_ab_range_cmp.txt); C5 within noise
-#ifndef VBHEM_RANGE_CMP
-#define VBHEM_RANGE_CMP 1
-#endif
+// The per-tile range check (|E|, |Ef| < vlim, Ab row sums <= 1) as one ordered compare
+// per element into a wave mask instead of an fmax chain, which the compiler emits with
+// NaN canonicalisation (three maxes per pair) and, written as per-lane compares, folds
+// back into that chain.  Ordered, so a NaN element is skipped exactly as fmax skips it.
+// fb_bwd4_kernel at C4: 1.252-1.264 vs 1.277-1.292 ms (4 interleaved repeats on one box,
+// profiles/r05ax_ab_range_cmp.txt); C5 within noise
 __device__ __forceinline__ uint64_t ge_mask(double x, double lim) {
   return __builtin_amdgcn_fcmp(x, lim, 3);  // FCMP_OGE
 }
@@ -142,9 +139,6 @@ __device__ __forceinline__ void log_m_n(double (&y)[N], const double (&z)[N], co
 // column maxima of a quad's two column blocks: x0 / x1 = this lane row's maximum of
 // block J = 0 / 1; the result's lane row r holds block J = r & 1 (over all 4 rows)
 __device__ __forceinline__ unsigned colmax_rows(unsigned x0, unsigned x1) {
-#ifdef VBHEM_ABL_NOPERM  // ablation (timing only, wrong results): no cross-row maxima
-  return max(x0, x1);
-#endif
   const auto a = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
   const unsigned u = max((unsigned)a[0], (unsigned)a[1]);
   const auto b = __builtin_amdgcn_permlane32_swap(u, u, false, false);
@@ -205,38 +199,18 @@ __device__ __forceinline__ void stage_tables(double *etab, double *ltab, int tid
 // logs (scripts/gen_log_table.py) and copied into each block's LDS: 16-byte loads from
 // L2 instead of a division and a libm log per entry (computing it took ~6 us of every
 // fb_bwd4_kernel launch, profiles/r05ah_ab_shard_cheap_stage.txt)
-// VBHEM_LOG_FREXP: log_q_n's mantissa as v_frexp_mant_f64 in [1/2, 1) against a staged
-// 2/c (both scalings exact, so the same r bit for bit) instead of inserting the exponent
-// of 1.0 into Z's high word, which costs a v_bfi_b32 and, as the compiler allocates it,
-// a v_mov_b32 for the low word.  fb_bwd12_kernel: step 226 -> 216 VALU, 4.79 -> 4.74 ms per
-// C5 group (profiles/r05ay_ab_log_frexp.txt).  FX = false keeps the old form where it did
-// not pay: fb_bwd4_kernel (step 104 -> 99 VALU, but 1.266 -> 1.272 ms at C4, within noise)
-// and fb_list12_kernel (the extra live register spills)
-#ifndef VBHEM_LOG_FREXP
-#define VBHEM_LOG_FREXP 1
-#endif
-constexpr bool kLogFrexp = VBHEM_LOG_FREXP != 0;
-
-template <bool FX = kLogFrexp>
 __device__ __forceinline__ void stage_log8k(double *ltab, int tid, int nt) {
   const double2 *src = reinterpret_cast<const double2 *>(kLogTab8k);
   double2 *dst = reinterpret_cast<double2 *>(ltab);
   // (unrolled: a 4-wave block's 32 copies per thread go out in two batches, not one
   // memory latency after another)
 #pragma unroll 16
-  for (int k = tid; k < 8192; k += nt) {
-    if constexpr (FX) {
-      const double2 v = src[k];
-      dst[k] = make_double2(2.0 * v.x, v.y);  // 2/c: log_q_n's mantissa is in [1/2, 1)
-    } else {
-      dst[k] = src[k];
-    }
-  }
+  for (int k = tid; k < 8192; k += nt) dst[k] = src[k];
 }
 
 // log(Z) + M, 8192-interval table, log1p(r) = r - r^2/2 (|r| <= 2^-14): kk = the
 // binary exponent of Z plus the maximum's term (integer, exact), then one fma
-template <int N, bool DEC, bool FX = kLogFrexp>
+template <int N, bool DEC>
 __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
                                         const double *ltab) {
   double zz[N], ic[N], w[N];
@@ -249,16 +223,9 @@ __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], co
     unsigned ex = hi >> 20;
     asm("" : "+v"(ex));
     const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
-    if constexpr (FX)
-      zz[x] = __builtin_amdgcn_frexp_mant(z[x]);
-    else
-      zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
-#ifdef VBHEM_ABL_NOLTAB  // ablation (timing only, wrong results): no log table read
-    const double2 e = {1.0, 0.0};
-#else
+    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
     const double2 e = *reinterpret_cast<const double2 *>(
         __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 3) & 0x1fff0u), 16));
-#endif
     ic[x] = e.x;
     w[x] = fma((double)kk, DEC ? 0x1.62e42fefa39efp-1 : kLn2N, e.y);
   }
@@ -270,31 +237,80 @@ __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], co
   }
 }
 
-// log(Z) + M with the 1024-interval table (m4::log_m_n's series) for the decoupled
-// maxima: kk = exponent + the maximum's multiple of ln 2
-template <int N>
-__device__ __forceinline__ void log_d_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
+// ---- round 6: the step's integer work cut (fb_bwd4_kernel, fb_bwd12_kernel) ----
+// The exp table's byte offset (lo(s) << 3) & 0x3ff8 with the mask from an SGPR the
+// combiner cannot see: with the constant it knows the offsets fit 16 bits and packs two
+// elements into v_perm + v_pk_lshlrev + v_and + v_bitop3 + v_lshrrev (five ops where
+// v_lshlrev + v_and twice are four).  (An "x8" range reduction that would have put 8 n in
+// the low word, leaving one v_and, does not exist: the low word holds s in units of its
+// ulp, so scaling the shift constant only moves the rounding point.)
+#ifndef VBHEM_AB_EMASK
+#define VBHEM_AB_EMASK 1   // (A/B, round 6)
+#endif
+#ifndef VBHEM_AB_LOGX
+#define VBHEM_AB_LOGX 1    // (A/B, round 6: 0 log_q_n's form, 2 the exponent by shift + sub)
+#endif
+__device__ __forceinline__ unsigned etab_mask() {
+  unsigned m = 0x3ff8u;
+#if VBHEM_AB_EMASK
+  asm("" : "+s"(m));
+#endif
+  return m;
+}
+__device__ __forceinline__ double etab_atm(const double *etab, double s, unsigned msk) {
+  return *reinterpret_cast<const double *>(
+      __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & msk), 8));
+}
+// The 8192-interval log table with 1/c scaled by 2^1023 (stage_log8k_x): for Z = 2^(ex -
+// 1023) zz the remainder r = zz / c - 1 is Z (2^1023/c) 2^-ex - 1, and 2^-ex goes into
+// the table value's exponent field by one integer op (v_mad_i32_i24 ex, -2^20, hi), where
+// log_q_n inserted 1.0's exponent into Z (a v_bfi_b32 and, as allocated, a v_mov_b32 for
+// the low word).  Both scalings are exact, so r is the same bit for bit.  ic 2^1023 is
+// finite (c > 1, so 1/c < 1), and ic 2^(1023 - ex) stays normal for every Z the kernels
+// accept (2^-665 <= Z <= S; a Z outside that is flagged or non-finite anyway).
+__device__ __forceinline__ void stage_log8k_x(double *ltab, int tid, int nt) {
+  const double2 *src = reinterpret_cast<const double2 *>(kLogTab8k);
+  double2 *dst = reinterpret_cast<double2 *>(ltab);
+#pragma unroll 16
+  for (int k = tid; k < 8192; k += nt) {
+    const double2 v = src[k];
+    dst[k] = make_double2(VBHEM_AB_LOGX ? v.x * 0x1p1023 : v.x, v.y);
+  }
+}
+// log(Z) + M on stage_log8k_x's table: kk = Z's biased exponent + wq (DEC: M a multiple
+// of ln 2, wq = k - 1023; otherwise M = m ln2/2048, wq = m - 1023 2048 and kk = ex 2048 + wq)
+template <int N, bool DEC>
+__device__ __forceinline__ void log_x_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
                                         const double *ltab) {
-  double zz[N], ic[N], w[N];
-  unsigned one_hi = 0x3ff00000u;
-  asm("" : "+v"(one_hi));
+#if VBHEM_AB_LOGX == 0
+  log_q_n<N, DEC>(y, z, wq, ltab);
+  return;
+#endif
+  double ic[N], w[N];
+  // -2^20 in an SGPR the combiner cannot see: __mul24 by a known power of two would
+  // become a shift and a subtraction (two ops); this way it is one v_mad_i32_i24
+  int m20 = -1048576;
+#if VBHEM_AB_LOGX == 1
+  asm("" : "+s"(m20));
+#endif
 #pragma unroll
   for (int x = 0; x < N; ++x) {
     const unsigned hi = (unsigned)__double2hiint(z[x]);
-    const unsigned zh = (hi & 0x000fffffu) | (one_hi & 0xfff00000u);
-    const int kk = (int)(hi >> 20) + wq[x];
-    zz[x] = __hiloint2double((int)zh, __double2loint(z[x]));
+    unsigned ex = hi >> 20;
+    asm("" : "+v"(ex));
+    const int kk = DEC ? (int)ex + wq[x] : (int)(ex << 11) + wq[x];
     const double2 e = *reinterpret_cast<const double2 *>(
-        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 6) & 0x3ff0u), 16));
-    ic[x] = e.x;
-    w[x] = fma((double)kk, 0x1.62e42fefa39efp-1, e.y);
+        __builtin_assume_aligned(reinterpret_cast<const char *>(ltab) + ((hi >> 3) & 0x1fff0u), 16));
+    // ic 2^(1023 - ex): one 24-bit multiply-add on the high word
+    const int ich = __mul24((int)ex, m20) + __double2hiint(e.x);
+    ic[x] = __hiloint2double(ich, __double2loint(e.x));
+    w[x] = fma((double)kk, DEC ? 0x1.62e42fefa39efp-1 : kLn2N, e.y);
   }
 #pragma unroll
   for (int x = 0; x < N; ++x) {
-    const double sh = fma(zz[x], ic[x], -0.5);
-    const double s2 = sh * sh;
-    const double q = fma(sh, 4.0 / 3.0, -1.0);
-    y[x] = fma(fma(q, s2, sh), 2.0, w[x]);
+    const double r = fma(z[x], ic[x], -1.0);
+    const double h = fma(r, -0.5, 1.0);
+    y[x] = fma(r, h, w[x]);
   }
 }
 
@@ -317,59 +333,6 @@ __device__ __forceinline__ void exp_d_n(double (&g)[N], const double (&v)[N], co
 __device__ __forceinline__ double etab_at(const double *etab, double s) {
   return *reinterpret_cast<const double *>(
       __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & 0x3ff8u), 8));
-}
-
-// ---- the paired exp table {t, t/2} (t = 2^(i/2048 - 1010)): exp(r) t to second order
-// as t + r (t + (t/2) r), two fp64 operations after the range reduction instead of three
-// (0.5 r, r + r^2/2, t + t (r + r^2/2)); one 16-byte LDS read per element, as the log's
-__device__ __forceinline__ double2 etab2_at(const double *etab2, double s) {
-  return *reinterpret_cast<const double2 *>(
-      __builtin_assume_aligned(reinterpret_cast<const char *>(etab2) + ((lo_u(s) << 4) & 0x7ff0u), 16));
-}
-template <int N>
-__device__ __forceinline__ void exp_d2_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
-                                         const double2 (&t)[N], const unsigned (&wph)[N]) {
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
-    const double m = fma(fma(t[x].y, r, t[x].x), r, t[x].x);
-    unsigned e = __builtin_elementwise_sub_sat(lo_u(s[x]) >> 11, wph[x]);
-    asm("" : "+v"(e));
-    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
-  }
-}
-// exp_m_n on the paired table (the termination's exps)
-template <int N>
-__device__ __forceinline__ void exp_m2_n(double (&g)[N], const double (&v)[N], const double (&s)[N],
-                                         const unsigned (&wp)[N], const double *etab2) {
-  double2 t[N];
-  unsigned d[N];
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    d[x] = __builtin_elementwise_sub_sat(lo_u(s[x]), wp[x]);
-    t[x] = *reinterpret_cast<const double2 *>(
-        __builtin_assume_aligned(reinterpret_cast<const char *>(etab2) + ((d[x] << 4) & 0x7ff0u), 16));
-  }
-#pragma unroll
-  for (int x = 0; x < N; ++x) {
-    const double r = fma(-(s[x] - kShiftU), kLn2N, v[x]);
-    const double m = fma(fma(t[x].y, r, t[x].x), r, t[x].x);
-    unsigned e = d[x] >> 11;
-    asm("" : "+v"(e));
-    g[x] = __hiloint2double((int)((e << 20) + (unsigned)__double2hiint(m)), __double2loint(m));
-  }
-}
-__device__ __forceinline__ void stage_etab2(double *etab2, int tid, int nt) {
-  for (int x = tid; x < 2048; x += nt) {
-    const double t = kExpTab4[x] * 0x1p-1010;
-    etab2[2 * x] = t;
-    etab2[2 * x + 1] = 0.5 * t;
-  }
-}
-// a wave-uniform double from lane l (an SGPR pair)
-__device__ __forceinline__ double readlane_d(double x, int l) {
-  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
-                          __builtin_amdgcn_readlane(__double2loint(x), l));
 }
 
 }  // namespace m4

@@ -1722,7 +1722,10 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
   // the MFMA kernel on the statistics copy Us (prepared base sets; S <= 16 rows of one
   // MFMA tile, SB <= 16, at most 12 feature tiles over 4 waves); also for the small
   // moment vectors of the grouped kernel (C3: statistics 0.039 -> 0.032 ms per step)
-  if (a.Us && !no_u && a.S <= 16 && a.SB <= 16 && us_nup(a.NU) <= 12 * 16 &&
+  // (it reads Z at the 32-bit offset (i - i_buf0) K + j: the base group times K must stay
+  // below 2^32 -- always so for a workspace group, checked anyway)
+  const bool z32 = (unsigned long long)(a.i_end - a.i_buf0) * (unsigned long long)a.K < (1ull << 32);
+  if (a.Us && !no_u && z32 && a.S <= 16 && a.SB <= 16 && us_nup(a.NU) <= 12 * 16 &&
       !std::getenv("VBHEM_NO_STATS_M")) {
     // one 1-D grid over all clusters' gated pairs (balanced parts; the block maps
     // itself to (cluster, part)); at most nzero_m parts per cluster, so the slabs past

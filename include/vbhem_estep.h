@@ -265,6 +265,13 @@ int vbhem_timing_read_gated(double *fwd_ms, long long *fwd_launches);
  * the last call; recorded while vbhem_timing_enable(1) is on. */
 int vbhem_timing_read_em_math(double *ms, long long *launches);
 
+/* Test hook (fault injection, no reference counterpart): add `bytes` of dynamic LDS
+ * to the next fb_bwd2_kernel launches of this process, so the runtime refuses them
+ * (tests/test_robustness.py: a refused launch must not leave a HIP error pending).
+ * 0 turns it off; returns the previous value.  Never set in production: unlike an
+ * environment variable, nothing outside the calling program can switch it on. */
+size_t vbhem_debug_extra_lds(size_t bytes);
+
 const char *vbhem_last_error(void);
 const char *vbhem_version(void);
 /* The kernel the calling thread's last E-step ran for a recursion pass, as the

@@ -27,11 +27,14 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 constexpr int kIters = UB_ITERS;
 
 enum Op { FMA64, ADD64, MUL64, MAX64, RNDNE64, CVT_PAIR, LDEXP64, AND32, ADDU32, FMA32,
-          MFMA16, MFMA4, MFMA16_FMA, MFMA4_FMA, NOP_ };
+          MFMA16, MFMA4, MFMA16_FMA, MFMA4_FMA, MADI24, BFI32, LSHLADD, SUBCLAMP, PERMLANE16,
+          MOV32, CVTF64I32, FRMANT64, NOP_ };
 static const char *kOpName[] = {"v_fma_f64", "v_add_f64", "v_mul_f64", "v_max_f64",
                                 "v_rndne_f64", "cvt_i32_f64+cvt_f64_i32", "v_ldexp_f64",
                                 "v_and_b32", "v_add_u32", "v_fma_f32", "mfma_f64_16x16x4",
-                                "mfma_f64_4x4x4", "mfma16 + 16 fma_f64", "mfma4 + 4 fma_f64"};
+                                "mfma_f64_4x4x4", "mfma16 + 16 fma_f64", "mfma4 + 4 fma_f64",
+                                "v_mad_i32_i24", "v_bfi_b32", "v_lshl_add_u32", "v_sub_u32 clamp",
+                                "v_permlane16_swap", "v_mov_b32", "v_cvt_f64_i32", "v_frexp_mant_f64"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void rate_kernel(double *out, long long *cyc, double seed) {
@@ -68,6 +71,16 @@ __global__ __launch_bounds__(256) void rate_kernel(double *out, long long *cyc, 
       if constexpr (OP == AND32) asm volatile("v_and_b32 %0, %0, %1" : "+v"(ia[q]) : "v"(0x7fffffff));
       if constexpr (OP == ADDU32) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ia[q]) : "v"(1));
       if constexpr (OP == FMA32) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(fa[q]) : "v"(1.0f), "v"(1e-9f));
+      if constexpr (OP == MADI24) asm volatile("v_mad_i32_i24 %0, %0, %1, %2" : "+v"(ia[q]) : "v"(3), "v"(1));
+      if constexpr (OP == BFI32) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(ia[q]) : "v"(0x000fffff), "v"(0x3ff00000));
+      if constexpr (OP == LSHLADD) asm volatile("v_lshl_add_u32 %0, %0, 1, %1" : "+v"(ia[q]) : "v"(7));
+      if constexpr (OP == SUBCLAMP) asm volatile("v_sub_u32_e64 %0, %0, %1 clamp" : "+v"(ia[q]) : "v"(1));
+      if constexpr (OP == PERMLANE16) {
+        if (q % 2 == 0) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(ia[q]), "+v"(ia[q + 1]));
+      }
+      if constexpr (OP == MOV32) asm volatile("v_mov_b32 %0, %1" : "=v"(ia[q]) : "v"(ia[(q + 1) % 8]));
+      if constexpr (OP == CVTF64I32) asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(a[q]) : "v"(ia[q]));
+      if constexpr (OP == FRMANT64) asm volatile("v_frexp_mant_f64 %0, %0" : "+v"(a[q]));
     }
     if constexpr (OP == MFMA16 || OP == MFMA16_FMA) {
 #pragma unroll
@@ -149,6 +162,7 @@ static int run_rate(double *d_out, long long *d_cyc, int blocks) {
   // instructions per wave per iteration
   double ninst = 8;
   if (OP == CVT_PAIR) ninst = 16;
+  if (OP == PERMLANE16) ninst = 4;
   if (OP == MFMA16 || OP == MFMA4) ninst = 4;
   if (OP == MFMA16_FMA) ninst = 4;   // cycles per MFMA with 16 fp64 FMAs alongside
   if (OP == MFMA4_FMA) ninst = 4;
@@ -181,7 +195,11 @@ int main() {
       run_rate<LDEXP64>(d_out, d_cyc, blocks) || run_rate<AND32>(d_out, d_cyc, blocks) ||
       run_rate<ADDU32>(d_out, d_cyc, blocks) || run_rate<FMA32>(d_out, d_cyc, blocks) ||
       run_rate<MFMA16>(d_out, d_cyc, blocks) || run_rate<MFMA4>(d_out, d_cyc, blocks) ||
-      run_rate<MFMA16_FMA>(d_out, d_cyc, blocks) || run_rate<MFMA4_FMA>(d_out, d_cyc, blocks))
+      run_rate<MFMA16_FMA>(d_out, d_cyc, blocks) || run_rate<MFMA4_FMA>(d_out, d_cyc, blocks) ||
+      run_rate<MADI24>(d_out, d_cyc, blocks) || run_rate<BFI32>(d_out, d_cyc, blocks) ||
+      run_rate<LSHLADD>(d_out, d_cyc, blocks) || run_rate<SUBCLAMP>(d_out, d_cyc, blocks) ||
+      run_rate<PERMLANE16>(d_out, d_cyc, blocks) || run_rate<MOV32>(d_out, d_cyc, blocks) ||
+      run_rate<CVTF64I32>(d_out, d_cyc, blocks) || run_rate<FRMANT64>(d_out, d_cyc, blocks))
     return 1;
   // one wave per SIMD: latency-bound chains (8 independent) for reference
   printf("-- 1 wave per SIMD --\n");

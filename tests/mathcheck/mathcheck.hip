@@ -93,6 +93,42 @@ __global__ void logtabm_kernel(int n, const double* __restrict__ x, double* __re
   }
 }
 
+// round 6: the log on the 2^1023-scaled 1/c table (log_x_n, fb_bwd4_kernel /
+// fb_bwd12_kernel) beside the form it replaces (log_q_n on the plain table), and the exp
+// table offsets from the SGPR mask (etab_atm) beside etab_at, column maximum 0: log at x
+// (both the decoupled and the 2048-unit maxima), exp at -x.  Tables in global memory
+// (the helpers take any pointer)
+__global__ void stagex_kernel(double* et, double* lx, double* lq) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+  for (int k = tid; k < 2048; k += nt) et[k] = vbhem::m4::kExpTab4[k] * 0x1p-1010;
+  vbhem::m4::stage_log8k_x(lx, tid, nt);
+  vbhem::m4::stage_log8k(lq, tid, nt);
+}
+__global__ void logtabx_kernel(int n, const double* __restrict__ x, double* __restrict__ out,
+                               const double* et, const double* lx, const double* lq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  using namespace vbhem::m4;
+  double y[1];
+  const double z[1] = {x[i]};
+  const int wq[1] = {-1023}, wq0[1] = {-1023 * 2048};
+  log_x_n<1, true>(y, z, wq, lx);
+  out[6 * i + 0] = y[0];
+  log_q_n<1, true>(y, z, wq, lq);
+  out[6 * i + 1] = y[0];
+  log_x_n<1, false>(y, z, wq0, lx);
+  out[6 * i + 2] = y[0];
+  log_q_n<1, false>(y, z, wq0, lq);
+  out[6 * i + 3] = y[0];
+  const double v[1] = {-x[i]}, s[1] = {red_s(-x[i])};
+  const double tm[1] = {etab_atm(et, s[0], etab_mask())}, t[1] = {etab_at(et, s[0])};
+  const unsigned wph[1] = {(1u << 20) - 1010u};
+  exp_d_n<1>(y, v, s, tm, wph);
+  out[6 * i + 4] = y[0];
+  exp_d_n<1>(y, v, s, t, wph);
+  out[6 * i + 5] = y[0];
+}
+
 __global__ void math_kernel(int n, const double* __restrict__ x, double* __restrict__ e,
                             double* __restrict__ l, double* __restrict__ r) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -214,6 +250,27 @@ int logtabe_device(int n, const double* x, double* l, double* e) {
 
 int logtabm_device(int n, const double* x, double* l, double* e) {
   return logtab_device_impl(n, x, l, e, 4);
+}
+
+// logtabx_kernel on device 0: out[6 i + (log new, log old, log2048 new, log2048 old,
+// exp new, exp old)]
+int logtabx_device(int n, const double* x, double* out) {
+  double *dx = nullptr, *dout = nullptr, *tabs = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)(n > 0 ? n : 1);
+  hipError_t st = hipMalloc(&dx, bytes);
+  if (st == hipSuccess) st = hipMalloc(&dout, 6 * bytes);
+  if (st == hipSuccess) st = hipMalloc(&tabs, sizeof(double) * (2048 + 4 * 8192));
+  if (st == hipSuccess) st = hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+  if (st == hipSuccess && n > 0) {
+    stagex_kernel<<<64, 256>>>(tabs, tabs + 2048, tabs + 2048 + 2 * 8192);
+    logtabx_kernel<<<(n + 255) / 256, 256>>>(n, dx, dout, tabs, tabs + 2048, tabs + 2048 + 2 * 8192);
+    st = hipGetLastError();
+  }
+  if (st == hipSuccess) st = hipMemcpy(out, dout, 6 * sizeof(double) * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(dout);
+  (void)hipFree(tabs);
+  return (int)st;
 }
 
 // Same on device 0 (host arrays in/out).  Returns 0 or a hipError_t.

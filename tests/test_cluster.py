@@ -4,6 +4,7 @@ with the oracle stand-in engine (tests/oracle_engine.py) in place of the
 device E-step: model selection over K and S (+gammaln), trials and their best
 bound, groups, and a short L-BFGS hyperparameter run."""
 import numpy as np
+import pytest
 from scipy.special import gammaln
 
 from oracle_engine import OracleEngine
@@ -175,6 +176,20 @@ def test_cluster_wtkmeans_and_auto(vb):
     assert auto["initmode"] in ("baseem", "gmmNew", "wtkmeans")
     assert auto["LL"] == max(auto["init_trials_LL"])
     np.testing.assert_allclose(auto["init_trials_LL"][2], r["LL"], rtol=1e-12)
+    # keep_best_random_trial (default 1): every mode's run kept (vbhem_h3m_cluster.m:391-393)
+    assert [t["Initmodes"] for t in auto["h3m_out_trials"]] == ["baseem", "gmmNew", "wtkmeans"]
+    assert [t["LL"] for t in auto["h3m_out_trials"]] == auto["init_trials_LL"]
+    # opt.initmodes needs opt.initopts (vbhem_h3m_cluster.m:366-368); one mode alone
+    with pytest.raises(ValueError):
+        cluster.vbhem_h3m_cluster(None, 2, 2, dict(OPT, initmode="auto", initmodes=["wtkmeans"],
+                                                   trials=3, max_iter=20),
+                                  base=base, engine_factory=_factory)
+    one = cluster.vbhem_h3m_cluster(None, 2, 2, dict(OPT, initmode="auto", initmodes=["wtkmeans"],
+                                                     initopts=["r0"], trials=3, max_iter=20,
+                                                     keep_best_random_trial=0),
+                                    base=base, engine_factory=_factory)
+    np.testing.assert_allclose(one["LL"], r["LL"], rtol=1e-12)
+    assert "h3m_out_trials" not in one
 
 
 def test_hier_em_vs_loop_restatement(vb):

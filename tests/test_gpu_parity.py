@@ -387,6 +387,69 @@ def test_range_check_mfma_kernels(vb, vo, S, shift):
     assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
+def _emission(base, consts):
+    """E[i, j, sigma, beta] of mex.c:715-865 (full covariance), numpy."""
+    mu, Sg = base["centres"], base["covars"]
+    m, P, c = consts["m"], consts["P"], consts["c"]
+    d = mu.shape[-1]
+    diff = mu[:, None, None, :, :] - m[None, :, :, None, :]          # [N][K][S][SB][d]
+    quad = np.einsum("nksbx,ksxy,nksby->nksb", diff, P, diff)
+    tr = np.einsum("ksxy,nbyx->nksb", P, Sg)
+    return -0.5 * (d * np.log(2 * np.pi) + c[None, :, :, None] + tr + quad)
+
+
+@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}])
+@pytest.mark.parametrize("case", ["near", "far", "rowsum", "far+rowsum"])
+@pytest.mark.parametrize("S", [8, 12])
+def test_range_check_exact_flags(vb, vo, S, case, env, monkeypatch):
+    """The per-tile range check of the MFMA kernels flags exactly the pairs it must
+    (ADVICE r05): one base state of one base pushed towards or out of range -- its E
+    column made very negative through that state's covariance (every cluster shares one
+    precision, so every E entry of the column lands in a chosen window) -- and / or one
+    base row of A summing to 1.5.  Windows: "near" |E| in [1.1e4, 5e4], large but
+    inside the integer maxima's limit (7e5 / T - 3): nothing flagged; "far" |E| >= 8e4,
+    past it, so the backward pass flags the base's K pairs and the gate-list pass its
+    gated ones again; "rowsum" flags the row's base in both passes.  The fallback count
+    must equal that exactly, and every output must be the oracle's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    N, K, d, T = 41, 3, 3, 10
+    cs = make_case(N, K, S, S, d, 1, seed=9, tau=T)
+    base = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in cs["base"].items()}
+    consts = {k: np.array(v, copy=True) for k, v in cs["consts"].items()}
+    consts["P"][:] = consts["P"][0, 0]          # one precision: E columns move together
+    i0, b0, i1 = 17, 3, 29
+    if "near" in case or "far" in case:
+        trP = float(np.trace(consts["P"][0, 0]))
+        E0 = _emission(base, consts)[i0, :, :, b0]
+        target = 3.0e4 if "near" in case else 1.6e5
+        lam = 2.0 * (target + E0.mean()) / trP
+        base["covars"][i0, b0] += lam * np.eye(d)
+        E1 = _emission(base, consts)[i0, :, :, b0]
+        lo, hi = (1.1e4, 5.0e4) if "near" in case else (8.0e4, 1e9)
+        assert (-E1 >= lo).all() and (-E1 <= hi).all(), (E1.min(), E1.max())
+    if "rowsum" in case:
+        base["A"][i1, 2] *= 1.5 / base["A"][i1, 2].sum()
+    pairs = vo.c_estep_pairs(base, consts, T)
+    assert np.isfinite(pairs["LL_elbo"]).all()
+    tN = 100.0 * N * base["omega"]
+    logOmega, hz, Z, Nj = vo.responsibilities(pairs["LL_elbo"], tN, cs["post"]["alpha"])
+    st = vo.c_statistics(Z, pairs, 1)
+    eng = engine(vb, base, consts, T)
+    eng.set_log_omega(logOmega)
+    got = vb.host.unpack_stats(eng.fused(torch.as_tensor(tN, device=DEV)).cpu().numpy(), K, S, d, 1)
+    gated = (Z > 1e-8)
+    expect = 0
+    if "far" in case:
+        expect += K + int(gated[i0].sum())
+    if "rowsum" in case:
+        expect += K + int(gated[i1].sum())
+    assert eng.fallback_count() == expect
+    for k in ("Nj", "N1", "M", "Nr", "Y", "SC"):
+        assert stat_err(got[k], st[k]) < 1e-9, k
+    assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
+
+
 def test_host_pointer_entry_point(vb, vo, capi_lib):
     """vbhem_estep_pairs_host (what the MEX gateway calls): host arrays in/out."""
     from vbhem_amd import _capi

@@ -191,3 +191,33 @@ def test_mfma_kernels_exp_log_device_build(mathcheck):
     rel = np.abs(e[m] - np.exp(-x[m])) / np.exp(-x[m])
     assert (rel <= 1e-12 + 1e-16 * x[m]).all(), float(rel.max())
     assert (e[x > 710] > 0).all() and (e[x > 710] < 1e-300).all()
+
+
+@pytest.mark.gpu
+def test_scaled_log_table_device_build(mathcheck):
+    """Round 6 (vbhem_mfma4.h): the log on the 2^1023-scaled 1/c table (log_x_n, the
+    table's exponent lowered by Z's with one v_mad_i32_i24) gives the same bits as
+    log_q_n on the plain table over the positive normals up to 1e300 (the scaled 1/c
+    stays normal), for the decoupled (k ln 2) and the 2048-unit maxima; the exp table
+    read through the SGPR mask (etab_atm) the same bits as etab_at; both within the
+    accuracy test_mfma_kernels_exp_log_device_build holds the old forms to."""
+    dp = ctypes.POINTER(ctypes.c_double)
+    fn = mathcheck.logtabx_device
+    fn.argtypes = [ctypes.c_int, dp, dp]
+    rng = np.random.default_rng(21)
+    x = np.concatenate([np.exp(rng.uniform(np.log(1e-300), np.log(1e300), N // 2)),
+                        rng.uniform(0.99, 1.01, N // 8), rng.uniform(0.0, 8.0, N // 8),
+                        rng.uniform(0.0, 700.0, N // 8), rng.uniform(700.0, 7.0e5, N // 8),
+                        [1e-300, 1.0, 2.0, 8.0, 700.0, 745.0, 6.99e5]])
+    out = np.zeros(6 * len(x))
+    assert fn(len(x), x.ctypes.data_as(dp), out.ctypes.data_as(dp)) == 0
+    out = out.reshape(-1, 6)
+    assert np.array_equal(out[:, 0], out[:, 1])
+    assert np.array_equal(out[:, 2], out[:, 3])
+    m = x < 7.0e5   # the exp's integer range (red_s)
+    assert np.array_equal(out[m, 4], out[m, 5])
+    ref = np.log(x)
+    assert (np.abs(out[:, 0] - ref) <= 2.0 * np.spacing(np.abs(ref)) + 2e-13).all()
+    e = x <= 700
+    rel = np.abs(out[e, 4] - np.exp(-x[e])) / np.exp(-x[e])
+    assert (rel <= 1e-12 + 1e-16 * x[e]).all(), float(rel.max())

@@ -233,7 +233,7 @@ def test_fused_many_clusters(vb, vo, K):
 @pytest.mark.gpu
 def test_refused_launch_does_not_poison_the_caller(vb, vo, monkeypatch):
     """A launch the runtime refuses (here: fb_bwd2_kernel asked for more dynamic LDS
-    than a CU has, through the fault-injection switch VBHEM_DEBUG_EXTRA_LDS) returns a
+    than a CU has, through the fault-injection hook vbhem_debug_extra_lds) returns a
     non-zero status with the kernel named -- and leaves no pending HIP error behind:
     the caller's next torch launch and a normal fused E-step in the same process run
     and match the oracle.  (Round 4: one refused launch left hipErrorInvalidValue
@@ -244,10 +244,13 @@ def test_refused_launch_does_not_poison_the_caller(vb, vo, monkeypatch):
     logOm = host.log_omega_tilde(cs["P"].alpha)
     eng.set_log_omega(logOm)
     tN = _tn(cs)
-    monkeypatch.setenv("VBHEM_DEBUG_EXTRA_LDS", str(200 * 1024))
-    with pytest.raises(_capi.VbhemError, match=r"status -4\).*fb_bwd2_kernel"):
-        eng.fused(tN)
-    monkeypatch.delenv("VBHEM_DEBUG_EXTRA_LDS")
+    lib = _capi.lib()
+    lib.vbhem_debug_extra_lds(200 * 1024)
+    try:
+        with pytest.raises(_capi.VbhemError, match=r"status -4\).*fb_bwd2_kernel"):
+            eng.fused(tN)
+    finally:
+        assert lib.vbhem_debug_extra_lds(0) == 200 * 1024
     z = torch.zeros(1000, device=DEV, dtype=torch.float64) + 1.0   # torch's own launches
     torch.cuda.synchronize()
     assert float(z.sum()) == 1000.0
