@@ -235,9 +235,8 @@ void fb_bwd12_kernel(const SplitArgs p) {
 #pragma unroll
         for (int x = 0; x < NE; ++x) sf[x] = red_s(V[x / NB][x % NB]);
         // the exp table values need no maximum: their reads go out first
-        const unsigned emsk = etab_mask();
 #pragma unroll
-        for (int x = 0; x < NE; ++x) tv[x] = etab_atm(etab, sf[x], emsk);
+        for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, sf[x]);
         unsigned xm[NB];
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj)

@@ -62,9 +62,9 @@
 //   * the range check (|E|, |Ef| < vlim, Ab row sums <= 1) as ordered compares into a wave
 //     mask (an fmax chain compiles with NaN canonicalisation)
 //   * round 6: the log's exponent applied to the table's 1/c by one v_mad_i32_i24
-//     instead of inserting 1.0's exponent into Z (v_bfi_b32 + v_mov_b32), and the exp
-//     table offsets as v_lshlrev + v_and (vbhem_mfma4.h: log_x_n, etab_atm) -- 104 ->
-//     98 VALU instructions per quad-step, same bits (profiles/r06_isa_step.txt)
+//     instead of inserting 1.0's exponent into Z (v_bfi_b32 + v_mov_b32; vbhem_mfma4.h
+//     log_x_n): 104 -> 100 VALU instructions per quad-step, same bits, 1.249 -> 1.238 ms
+//     per C4 launch (profiles/r06d_ab_c4_bwd4_logx_emask.txt, profiles/r06_isa_step.txt)
 
 namespace vbhem {
 
@@ -237,9 +237,8 @@ void fb_bwd4_kernel(const SplitArgs p) {
         sf[x] = red_s(vv[x]);
       }
       // table values first (they do not need the maxima), then the maxima chain
-      const unsigned emsk = etab_mask();
 #pragma unroll
-      for (int x = 0; x < 4; ++x) tv[x] = etab_atm(etab, sf[x], emsk);
+      for (int x = 0; x < 4; ++x) tv[x] = etab_at(etab, sf[x]);
       const unsigned w = colmax_rows(max(lo_u(sf[0]), lo_u(sf[2])), max(lo_u(sf[1]), lo_u(sf[3]))) >> 11;
       const int wq = (int)w - (1 << 20) - 1023;
       int mq[2];

@@ -242,9 +242,8 @@ void fb_list12_kernel(const SplitArgs p) {
       double sf[NE], tv[NE];
 #pragma unroll
       for (int x = 0; x < NE; ++x) sf[x] = red_s(V[x / NB][x % NB]);
-      const unsigned emsk = etab_mask();
 #pragma unroll
-      for (int x = 0; x < NE; ++x) tv[x] = etab_atm(etab, sf[x], emsk);
+      for (int x = 0; x < NE; ++x) tv[x] = etab_at(etab, sf[x]);
       unsigned xm[NB];
 #pragma unroll
       for (int jj = 0; jj < NB; ++jj)

@@ -237,30 +237,7 @@ __device__ __forceinline__ void log_q_n(double (&y)[N], const double (&z)[N], co
   }
 }
 
-// ---- round 6: the step's integer work cut (fb_bwd4_kernel, fb_bwd12_kernel) ----
-// The exp table's byte offset (lo(s) << 3) & 0x3ff8 with the mask from an SGPR the
-// combiner cannot see: with the constant it knows the offsets fit 16 bits and packs two
-// elements into v_perm + v_pk_lshlrev + v_and + v_bitop3 + v_lshrrev (five ops where
-// v_lshlrev + v_and twice are four).  (An "x8" range reduction that would have put 8 n in
-// the low word, leaving one v_and, does not exist: the low word holds s in units of its
-// ulp, so scaling the shift constant only moves the rounding point.)
-#ifndef VBHEM_AB_EMASK
-#define VBHEM_AB_EMASK 1   // (A/B, round 6)
-#endif
-#ifndef VBHEM_AB_LOGX
-#define VBHEM_AB_LOGX 1    // (A/B, round 6: 0 log_q_n's form, 2 the exponent by shift + sub)
-#endif
-__device__ __forceinline__ unsigned etab_mask() {
-  unsigned m = 0x3ff8u;
-#if VBHEM_AB_EMASK
-  asm("" : "+s"(m));
-#endif
-  return m;
-}
-__device__ __forceinline__ double etab_atm(const double *etab, double s, unsigned msk) {
-  return *reinterpret_cast<const double *>(
-      __builtin_assume_aligned(reinterpret_cast<const char *>(etab) + ((lo_u(s) << 3) & msk), 8));
-}
+// ---- round 6 (fb_bwd4_kernel, fb_bwd12_kernel) ----
 // The 8192-interval log table with 1/c scaled by 2^1023 (stage_log8k_x): for Z = 2^(ex -
 // 1023) zz the remainder r = zz / c - 1 is Z (2^1023/c) 2^-ex - 1, and 2^-ex goes into
 // the table value's exponent field by one integer op (v_mad_i32_i24 ex, -2^20, hi), where
@@ -274,7 +251,7 @@ __device__ __forceinline__ void stage_log8k_x(double *ltab, int tid, int nt) {
 #pragma unroll 16
   for (int k = tid; k < 8192; k += nt) {
     const double2 v = src[k];
-    dst[k] = make_double2(VBHEM_AB_LOGX ? v.x * 0x1p1023 : v.x, v.y);
+    dst[k] = make_double2(v.x * 0x1p1023, v.y);
   }
 }
 // log(Z) + M on stage_log8k_x's table: kk = Z's biased exponent + wq (DEC: M a multiple
@@ -282,17 +259,12 @@ __device__ __forceinline__ void stage_log8k_x(double *ltab, int tid, int nt) {
 template <int N, bool DEC>
 __device__ __forceinline__ void log_x_n(double (&y)[N], const double (&z)[N], const int (&wq)[N],
                                         const double *ltab) {
-#if VBHEM_AB_LOGX == 0
-  log_q_n<N, DEC>(y, z, wq, ltab);
-  return;
-#endif
   double ic[N], w[N];
   // -2^20 in an SGPR the combiner cannot see: __mul24 by a known power of two would
-  // become a shift and a subtraction (two ops); this way it is one v_mad_i32_i24
+  // become a shift and a subtraction (two ops, measured 4 % slower); this way it is one
+  // v_mad_i32_i24
   int m20 = -1048576;
-#if VBHEM_AB_LOGX == 1
   asm("" : "+s"(m20));
-#endif
 #pragma unroll
   for (int x = 0; x < N; ++x) {
     const unsigned hi = (unsigned)__double2hiint(z[x]);

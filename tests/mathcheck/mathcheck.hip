@@ -94,9 +94,8 @@ __global__ void logtabm_kernel(int n, const double* __restrict__ x, double* __re
 }
 
 // round 6: the log on the 2^1023-scaled 1/c table (log_x_n, fb_bwd4_kernel /
-// fb_bwd12_kernel) beside the form it replaces (log_q_n on the plain table), and the exp
-// table offsets from the SGPR mask (etab_atm) beside etab_at, column maximum 0: log at x
-// (both the decoupled and the 2048-unit maxima), exp at -x.  Tables in global memory
+// fb_bwd12_kernel) beside the form it replaces (log_q_n on the plain table), column
+// maximum 0: log at x (both the decoupled and the 2048-unit maxima), exp at -x.  Tables in global memory
 // (the helpers take any pointer)
 __global__ void stagex_kernel(double* et, double* lx, double* lq) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
@@ -121,9 +120,9 @@ __global__ void logtabx_kernel(int n, const double* __restrict__ x, double* __re
   log_q_n<1, false>(y, z, wq0, lq);
   out[6 * i + 3] = y[0];
   const double v[1] = {-x[i]}, s[1] = {red_s(-x[i])};
-  const double tm[1] = {etab_atm(et, s[0], etab_mask())}, t[1] = {etab_at(et, s[0])};
+  const double t[1] = {etab_at(et, s[0])};
   const unsigned wph[1] = {(1u << 20) - 1010u};
-  exp_d_n<1>(y, v, s, tm, wph);
+  exp_d_n<1>(y, v, s, t, wph);
   out[6 * i + 4] = y[0];
   exp_d_n<1>(y, v, s, t, wph);
   out[6 * i + 5] = y[0];

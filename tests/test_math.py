@@ -198,9 +198,9 @@ def test_scaled_log_table_device_build(mathcheck):
     """Round 6 (vbhem_mfma4.h): the log on the 2^1023-scaled 1/c table (log_x_n, the
     table's exponent lowered by Z's with one v_mad_i32_i24) gives the same bits as
     log_q_n on the plain table over the positive normals up to 1e300 (the scaled 1/c
-    stays normal), for the decoupled (k ln 2) and the 2048-unit maxima; the exp table
-    read through the SGPR mask (etab_atm) the same bits as etab_at; both within the
-    accuracy test_mfma_kernels_exp_log_device_build holds the old forms to."""
+    stays normal), for the decoupled (k ln 2) and the 2048-unit maxima, within the
+    accuracy test_mfma_kernels_exp_log_device_build holds the old form to (the exp pair
+    of the kernel is the unchanged exp_d_n, checked here beside it)."""
     dp = ctypes.POINTER(ctypes.c_double)
     fn = mathcheck.logtabx_device
     fn.argtypes = [ctypes.c_int, dp, dp]
