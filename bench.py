@@ -179,7 +179,10 @@ def cpu_baseline(vo, base_np, consts, T, N_total, K, target_s):
     nproc, model = host_cpu()
     multi = dict(value=1.0 / (tm * N_total / n), unit="E-steps/s", cores=threads, kind="port",
                  sample=f"the same {n}-base sample, pairs over {threads} OpenMP threads ({tm:.2f} s)",
-                 host_nproc=nproc, host_cpu=model)
+                 host_nproc=nproc, host_cpu=model,
+                 note=("threads = OMP_NUM_THREADS, which the GPU box sets to the one-GPU job's "
+                       "CPU share (16 of its logical CPUs; the others belong to the other GPUs' "
+                       "jobs); the reference MEX itself is single-threaded"))
     return dict(value=1.0 / (t * N_total / n), unit="E-steps/s", cores=1, kind="port",
                 sample=(f"oracle/vbhem_oracle.c (C port of the reference mex.c E-step, 1 thread) + "
                         f"responsibilities + statistics on {n} of {N_total} base HMMs x {K} clusters "

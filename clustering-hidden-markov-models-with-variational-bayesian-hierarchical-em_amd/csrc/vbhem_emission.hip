@@ -781,6 +781,163 @@ __global__ __launch_bounds__(UNWAVE_MAXT) void emission_u_kernel(EmissionArgs p)
   }
 }
 
+// emission_db_kernel<KQ, RC, NTW>: the chunked path (W' restaged per RC-row-tile chunk,
+// C5's K S = 384 rows) with the chunks double-buffered in LDS and E written by buffer
+// stores.  emission_u_kernel's chunked loop waits for everything in flight before it
+// stages a chunk (s_waitcnt vmcnt(0)): the previous chunk's E stores included, which
+// sat on the critical path (a timing build without the stores ran 1.65 vs 1.85 ms per
+// C5 group).  Here chunk ch + 1's LDS-DMA is issued right after the
+// barrier that opens chunk ch, and the wait before chunk ch + 1 counts only the E
+// stores issued after that DMA -- every lane issues exactly NTW RC 4 of them per
+// chunk (buffer stores; a column past the base range or a padding row carries an
+// out-of-range offset and is dropped), so vmcnt(NTW RC 4) is exact.  Each chunk's
+// buffer holds its W' row tiles in A-operand lane order and its RC 16 biases.  Same
+// accumulation order as emission_u_kernel: the same E bits (checked bit for bit on
+// C5, scripts/cmp_libs.py).  Measured (round 6, C5 N = 1500): 1.757 ms per emission
+// launch against 1.864 for the chunked path (VBHEM_EM_NODB=1).
+template <int KQ, int RC, int NTW>
+__global__ __launch_bounds__(256) void emission_db_kernel(EmissionArgs p) {
+  constexpr int CW = KQ * RC * 64;       // W' doubles per chunk
+  constexpr int CB = CW + RC * 16;       // + its biases
+  constexpr int NST = NTW * RC * 4;      // E stores per lane and chunk
+  // the two chunk buffers as two LDS objects, the chunk loop unrolled by two so each
+  // half reads one and fills the other: the compiler's LDS-DMA tracking can then see
+  // that the DMA in flight does not write what the half reads (with one array indexed
+  // by a runtime buffer number it waited for the DMA -- vmcnt(0) -- before the first
+  // MFMA of every chunk)
+  __shared__ __attribute__((aligned(16))) double buf0[CB];
+  __shared__ __attribute__((aligned(16))) double buf1[CB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NW = blockDim.x >> 6;
+  const int KS = p.K * p.S, SB = p.SB;
+  const int nchunk = p.ksp / 16 / RC;   // even (the launcher checks)
+  const long long c_begin = (long long)p.i_begin * SB, c_end = (long long)p.i_end * SB;
+  const long long t_first = (c_begin - p.u_col0) / 16;
+  const long long t_last = (c_end - p.u_col0 + 15) / 16;
+  const long long per_round = (long long)gridDim.x * NW * NTW;
+  const long long rounds = (t_last - t_first + per_round - 1) / per_round;
+  const int kl = lane >> 4, cl = lane & 15;
+  const unsigned ldE8 = (unsigned)p.e_ld * 8u;
+  typedef __attribute__((address_space(3))) void *lds_ptr;
+  // chunk ch into dst: W' (two A-operand rows of 16 bytes per lane and wave
+  // instruction) and, from wave 0's first lanes, its RC 16 biases
+  // (written as inline asm: the builtin makes the compiler's LDS-DMA tracking wait for
+  // the DMA in flight -- vmcnt(0) -- before the reads of the other buffer in one of the
+  // two halves; the asm is invisible to it, and the waits above are explicit.  M0 takes
+  // the wave's LDS destination, one wait state before the load reads it; nothing else
+  // in this kernel uses M0, so it is not declared clobbered -- the compiler reserves it
+  // and warns)
+  auto dma = [&](int ch, double *dst) {
+    constexpr int nblk = KQ * RC / 2;
+    const unsigned base = (unsigned)(size_t)(lds_ptr)dst;
+    for (int b = wave; b < nblk; b += NW) {
+      const int x = b * 128 + 2 * lane;
+      const int t = x / (RC * 64), rem = x - t * (RC * 64), rt = rem >> 6, l = rem & 63;
+      const int row = (ch * RC + rt) * 16 + (l & 15), e = 4 * t + (l >> 4);
+      const double *g = p.W + (size_t)e * p.ksp + row;
+      const unsigned la = __builtin_amdgcn_readfirstlane(base + (unsigned)b * 1024u);
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                   ::"v"(g), "s"(la) : "memory");
+    }
+    if (wave == 0 && lane < RC * 16 / 2) {
+      const double *g = p.bias + ch * RC * 16 + 2 * lane;
+      const unsigned la = __builtin_amdgcn_readfirstlane(base + (unsigned)CW * 8u);
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                   ::"v"(g), "s"(la) : "memory");
+    }
+  };
+  const __amdgpu_buffer_rsrc_t re =
+      __builtin_amdgcn_make_buffer_rsrc(p.E, (short)0, (int)(unsigned)((size_t)KS * p.e_ld * 8), 0x00020000);
+  double u[NTW][KQ];
+  unsigned cofs[NTW];
+  bool cv[NTW];
+  // one chunk: wait for its DMA, barrier, the next chunk's DMA into the other buffer,
+  // the MFMAs from this one, the E stores
+  auto chunk = [&](int ch, bool first, const double *Wl, double *other, int nch, bool more) {
+    if (first) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the U tiles came after
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    // every wave's share landed and every wave's reads of the other buffer are done:
+    // an execution barrier without __syncthreads' release fence, which would wait for
+    // the E stores still in flight (vmcnt(0)) -- what this kernel avoids
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (more) dma(nch, other);
+    const double *bl = Wl + CW;
+    double4_t acc[NTW][RC];
+#pragma unroll
+    for (int q = 0; q < RC; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const double bv = bl[q * 16 + kl + 4 * v];
+#pragma unroll
+        for (int n = 0; n < NTW; ++n) acc[n][q][v] = bv;
+      }
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) {
+#pragma unroll
+      for (int q = 0; q < RC; ++q) {
+        const double w = Wl[(t * RC + q) * 64 + lane];
+#pragma unroll
+        for (int n = 0; n < NTW; ++n)
+          acc[n][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, u[n][t], acc[n][q], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NTW; ++n)
+#pragma unroll
+      for (int q = 0; q < RC; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int row = (ch * RC + q) * 16 + kl + 4 * v;
+          const unsigned off = (cv[n] && row < KS) ? cofs[n] + (unsigned)row * ldE8 : 0xfffffff8u;
+          // element by element: the store of a bit-cast vector element from the MFMA
+          // accumulator compiled to element 0 four times (hipcc 7.2, seen in the ISA)
+          const double x = acc[n][q][v];
+          em_u2 bits;
+          bits.x = (unsigned)__double2loint(x);
+          bits.y = (unsigned)__double2hiint(x);
+          __builtin_amdgcn_raw_buffer_store_b64(bits, re, (int)off, 0, 0);
+        }
+  };
+  if (rounds > 0) dma(0, buf0);
+#pragma unroll 1
+  for (long long r = 0; r < rounds; ++r) {
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) {
+      const long long tile = t_first + r * per_round + ((long long)blockIdx.x * NW + wave) * NTW + n;
+      const bool tv = tile < t_last;
+      const double *Ut = p.U + kUHead + (size_t)(tv ? tile : t_first) * KQ * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) u[n][t] = Ut[(size_t)t * 64];
+      const long long col = p.u_col0 + tile * 16 + cl;
+      cv[n] = tv && col >= c_begin && col < c_end;
+      cofs[n] = (unsigned)(cv[n] ? col - (long long)p.i_buf0 * SB : 0) * 8u;
+    }
+    const bool last = r + 1 == rounds;
+#pragma unroll 1
+    for (int ch = 0; ch < nchunk; ch += 2) {
+      chunk(ch, ch == 0, buf0, buf1, ch + 1, true);
+      // (the round's last chunk fills buf0 with the next round's chunk 0)
+      chunk(ch + 1, false, buf1, buf0, ch + 2 < nchunk ? ch + 2 : 0, ch + 2 < nchunk || !last);
+    }
+  }
+}
+
+template <int KQ, int RC, int NTW>
+static hipError_t launch_db_fn(const EmissionArgs &a, hipStream_t st) {
+  if (a.kdp / 4 != KQ || (a.ksp / 16) % (2 * RC) != 0) return hipErrorInvalidValue;
+  auto *fn = &emission_db_kernel<KQ, RC, NTW>;
+  const size_t lds = 0;  // (static: the two chunk buffers)
+  const int per_cu = resident_per_cu(reinterpret_cast<const void *>(fn), 256, lds);
+  const long long c_begin = (long long)a.i_begin * a.SB, c_end = (long long)a.i_end * a.SB;
+  const long long ntile = (c_end - a.u_col0 + 15) / 16 - (c_begin - a.u_col0) / 16;
+  const long long want = (ntile + 4 * NTW - 1) / (4 * NTW);
+  const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, (long long)device_cus() * per_cu));
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_u_prep(const UPrepArgs &a, hipStream_t st) {
   if (a.d < 1 || a.d > kUHead || a.u_col0 % 16 != 0) return hipErrorInvalidValue;
   const long long c_end = (long long)a.i_end * a.SB;
@@ -937,7 +1094,12 @@ hipError_t launch_emission(const EmissionArgs &a, size_t lds, hipStream_t st) {
       return one ? launch_u_fn<12, 8, 1, false, true>(a, lds, st) : launch_u_fn<12, 8, 1>(a, lds, st);
     }
     // W' restaged per chunk: two column tiles per wave halve the staging per column
-    if (a.kdp / 4 == 38) return launch_u_fn<38, 4, UNTW, true>(a, lds, st);  // d = 16 full (C5)
+    if (a.kdp / 4 == 38) {  // d = 16 full (C5)
+      // double-buffered chunks with buffer stores (E below 4 GB; VBHEM_EM_NODB: A/B)
+      if (em_bst_ok(a) && (a.ksp / 16) % 4 == 0 && !std::getenv("VBHEM_EM_NODB"))
+        return launch_db_fn<38, 2, 2>(a, st);
+      return launch_u_fn<38, 4, UNTW, true>(a, lds, st);
+    }
     return launch_u_fn<kUMaxKq, 4, UNTW>(a, lds, st);
   }
   if (a.wfull) {
