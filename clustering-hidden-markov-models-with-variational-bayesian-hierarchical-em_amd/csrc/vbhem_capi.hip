@@ -577,6 +577,7 @@ int run_fb_list(const FbCtx &c, int i_begin, int i_end, int i_buf0, double *nu1,
   if (c.list4) {  // S = 8, SB <= 8, T = 10: fb_list4_kernel (MFMA), one wave per quad item
     ca.Atg = c.bwd.a.Atg;
     const unsigned grid = (unsigned)(vbhem::device_cus() * std::max(1, vbhem::list4_resident_blocks()));
+    set_inline(vbhem::list4_inline_waves(ca, grid));
     e = vbhem::launch_list4(ca, grid, st);
     if (e != hipSuccess) return hip_fail(e, "fb_list4_kernel");
     g_last_kernel[1] = "vbhem::fb_list4_kernel<" + std::to_string(ca.T) +

@@ -22,14 +22,16 @@
 // An item's inputs are loaded during the previous item's forward sweep (C4 list pass
 // 0.240 -> 0.206 ms, profiles/r05v_ab_c4_list4_prefetch.txt).
 // The fallback flags are fb_bwd4_kernel's (underflow of Z, |V| range, non-finite
-// inputs); a flagged pair is recomputed by the exact kernel (or the statistics
-// kernel that folds it), as for fb_split_kernel's list mode.
+// inputs); a flagged pair is recomputed by the wave itself after its item loop
+// (xinline: queued in LDS; no fb_exact_kernel launch after the pass) or by the exact
+// kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <type_traits>
 
+#include "vbhem_exact.h"
 #include "vbhem_internal.h"
 #include "vbhem_math.h"
 #include "vbhem_mfma4.h"
@@ -47,6 +49,9 @@ constexpr int kL4Waves = 2;   // waves per SIMD (the lattice is 72 VGPRs)
 constexpr int kL4NWB = 4;    // waves per block
 constexpr int kL4T = 10;      // the tau this kernel is built for (C3 - C5)
 }  // namespace
+constexpr int kL4XQ = 1024;   // flagged pairs queued per wave (xinline; list4_xq_fits)
+namespace {
+}  // namespace
 
 // FAST: SB == 8 (no clamp or zero select in the item's addresses and operands) and
 // 32-bit load offsets (A, the prior and E below 4 GB), as fb_bwd4_kernel<O32>
@@ -58,6 +63,7 @@ void fb_list4_kernel(const SplitArgs p) {
   __shared__ __attribute__((aligned(16))) double ltab[2 * 1024];
   __shared__ int pre[kList4MaxK + 1];  // first quad item of every cluster
   __shared__ int tots[kList4MaxK];     // the gate lists' lengths
+  __shared__ int xq[kL4NWB * kL4XQ];   // per wave: its flagged pairs (xinline)
   const int tid = threadIdx.x;
   stage_tables(etab, ltab, tid, 64 * kL4NWB);
   const int K = p.K, SB = FAST ? 8 : p.SB;
@@ -122,7 +128,7 @@ void fb_list4_kernel(const SplitArgs p) {
     const int tot = tots[jj];
     return p.list[(size_t)jj * p.list_cap + (n0 + b_ < tot ? n0 + b_ : n0)];
   };
-  int js = 0, jsn = 0;
+  int js = 0, jsn = 0, nq = 0;
   ItemIn cur;
   int icur = 0;
   if (gw < nitem) {
@@ -394,16 +400,35 @@ void fb_list4_kernel(const SplitArgs p) {
 #pragma unroll
         for (int i3 = 0; i3 < 2; ++i3) p.xi[(lp * S + 4 * i2 + r) * S + 4 * i3 + c] = Ap[i2][i3] * H[i2][i3];
       if (pbad && !pnf && lane == 4 * b) {
-        // underflow or range with finite inputs: the exact kernel recomputes the pair
-        // (not inline: the exact recursion would take this kernel past 256 VGPRs)
-        const int slot = atomicAdd(p.flag_count, 1);
+        // underflow or range with finite inputs: the pair is recomputed by the exact
+        // recursion -- below, by this wave (xinline), or by the exact kernel
         atomicAdd(p.flag_count + 1, 1);
-        p.flag_list[slot] = (int)((size_t)i * K + j);
+        if (!p.xinline) {
+          const int slot = atomicAdd(p.flag_count, 1);
+          p.flag_list[slot] = (int)((size_t)i * K + j);
+        }
+      }
+    }
+    if (p.xinline) {
+      // the wave's flagged pairs into its LDS queue (recomputed after the item loop)
+      const unsigned long long fm = __ballot(act && pbad && !pnf && lane == 4 * b);
+      if (fm) {
+        const int l = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u));
+        if (fm >> lane & 1) xq[(tid >> 6) * kL4XQ + nq + l] = (int)((size_t)i * K + j);
+        nq += __builtin_popcountll(fm);
       }
     }
     cur = nxt;
     icur = inext;
     js = jsn;
+  }
+  // the exact recursion of the wave's flagged pairs (SplitArgs::xinline: the host
+  // inlines when every wave's queue bound fits and the grid has a scratch slot per
+  // wave), after the item loop, where none of the loop's registers are live
+  if (p.xinline) {
+    const int *q = xq + (tid >> 6) * kL4XQ;
+    for (int x = 0; x < nq; ++x)
+      exact_pair_wave<true>(p.xf, __builtin_amdgcn_readfirstlane(q[x]), p.xscr + (size_t)gw * p.xstride, nullptr);
   }
 }
 
@@ -415,6 +440,12 @@ bool list4_fast(const SplitArgs &a) {
   const unsigned long long lim = 0xffffffffull / 8;
   return a.SB == 8 && (unsigned long long)a.i_end * a.SB * a.SB < lim &&
          (unsigned long long)a.K * a.S * (unsigned long long)a.e_ld < lim;
+}
+long long list4_inline_waves(const SplitArgs &a, unsigned grid) {
+  const long long nw = (long long)grid * kL4NWB;
+  const long long items = (long long)a.K * ((a.i_end - a.i_begin + 3) / 4);  // all lists full
+  if (nw < 1 || 4 * ((items + nw - 1) / nw) > kL4XQ) return 1ll << 40;
+  return nw;
 }
 int list4_resident_blocks() {
   auto *fn = &fb_list4_kernel<kL4T, true>;

@@ -277,8 +277,10 @@ struct SplitArgs {
   // fb_split_kernel's list mode): a wavefront that flags a pair recomputes it itself
   // (exact_pair_wave, vbhem_exact.h; Theta and the small arrays in the wavefront's
   // scratch slot xscr + wave * xstride, one slot per wavefront of the persistent grid)
-  // instead of listing it for an fb_exact_kernel launch after the pass
-  int xinline;  // fb_split_kernel list mode, kSplitInlineMinS <= S <= kSplitInlineMaxS only
+  // instead of listing it for an fb_exact_kernel launch after the pass -- at once
+  // (fb_split_kernel, kSplitInlineMinS <= S <= kSplitInlineMaxS only) or from a
+  // per-wave LDS queue after the item loop (fb_list4_kernel, list4_inline_waves)
+  int xinline;
   double *xscr;
   long long xstride;
   FbArgs xf;
@@ -389,6 +391,10 @@ hipError_t launch_bwd12(const SplitArgs &a, unsigned grid, hipStream_t st, hipEv
 constexpr int kList4MaxK = 1024;
 bool list4_supported(int S, int SB, int T, int K);
 int list4_resident_blocks();  // per CU
+// the wavefronts of a grid of fb_list4_kernel when its per-wave queue of flagged pairs
+// (xinline) cannot overflow -- every cluster's list full -- else a count no inline
+// fallback accepts
+long long list4_inline_waves(const SplitArgs &a, unsigned grid);
 hipError_t launch_list4(const SplitArgs &a, unsigned grid, hipStream_t st);
 
 // fb_list12_kernel (vbhem_fb_list12.hip): the gate-list pass for S = 12, SB <= 12, T = 10

@@ -20,12 +20,15 @@ for cfg in C4 C3 C5; do
   timeout -k 10 600 python -u bench.py --config $cfg > $OUT/bench_$cfg.json 2> $OUT/bench_$cfg.err
   rc=$?; tail -c 300 $OUT/bench_$cfg.json; echo; [ $rc -ne 0 ] && exit $rc
 done
-[ "$NOPROF" = 1 ] && if [ "$SHARD" = 1 ]; then
+shard() {
   PASSES=trace bash scripts/profile.sh ${TAG}_shard --N 12500 --steps 20 --warmup 5 --no-parity-sample --em-iters 0 || exit $?
   python3 scripts/prof_summary.py gpurun_out/prof_${TAG}_shard $OUT/summary_shard > $OUT/summary_shard.txt 2>&1
   head -12 $OUT/summary_shard.txt
+}
+if [ "$NOPROF" = 1 ]; then
+  [ "$SHARD" = 1 ] && shard
+  exit 0
 fi
-exit 0
 bash scripts/profile.sh $TAG --steps 20 --warmup 5 || exit $?
 python3 scripts/prof_summary.py gpurun_out/prof_$TAG $OUT/summary_c4 > $OUT/summary_c4.txt 2>&1
 head -12 $OUT/summary_c4.txt
@@ -34,9 +37,5 @@ for cfg in C3 C5; do
   python3 scripts/prof_summary.py gpurun_out/prof_${TAG}_$(echo $cfg | tr A-Z a-z) $OUT/summary_$(echo $cfg | tr A-Z a-z) > $OUT/summary_$(echo $cfg | tr A-Z a-z).txt 2>&1
   head -12 $OUT/summary_$(echo $cfg | tr A-Z a-z).txt
 done
-if [ "$SHARD" = 1 ]; then
-  PASSES=trace bash scripts/profile.sh ${TAG}_shard --N 12500 --steps 20 --warmup 5 --no-parity-sample --em-iters 0 || exit $?
-  python3 scripts/prof_summary.py gpurun_out/prof_${TAG}_shard $OUT/summary_shard > $OUT/summary_shard.txt 2>&1
-  head -12 $OUT/summary_shard.txt
-fi
+[ "$SHARD" = 1 ] && shard
 exit 0

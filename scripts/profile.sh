@@ -11,7 +11,7 @@ ARGS="$@"
 # the PMC passes run the full-size E-steps only (no shard simulation, no EM-loop
 # timing): every launch of a kernel then has the same size and the per-dispatch
 # averages are the full-size launch's counters (prof_summary.py records this)
-PMC_ARGS="--no-shard-sim --em-iters 0 --no-parity-sample --steps 6 --warmup 2"
+PMC_ARGS="--no-shard-sim --em-iters 0 --no-parity-sample --steps 6 --warmup 2 --settle-ms 0"
 run() {  # name, extra rocprof args
   local name=$1; shift
   local extra=$ARGS

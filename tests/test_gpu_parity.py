@@ -332,16 +332,18 @@ def test_exact_fallback_gated_pairs(vb, vo, N, K, env, monkeypatch):
     assert elem_err(eng.LL.cpu().numpy(), pairs["LL_elbo"]) < RTOL_PAIRS
 
 
-@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}])
-@pytest.mark.parametrize("S", [8, 12])
-def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch, S):
+@pytest.mark.parametrize("env", [{}, {"VBHEM_NO_FOLD_EXACT": "1"}, {"VBHEM_NO_LIST_INLINE": "1"}])
+@pytest.mark.parametrize("S,N", [(8, 41), (8, 5000), (12, 41)])
+def test_exact_fallback_mfma_kernels(vb, vo, env, monkeypatch, S, N):
     """The adversarial cluster at S = Sb = 8 (12), T = 10: its pairs underflow in the
     MFMA backward pass (fb_bwd4_kernel / fb_bwd12_kernel) and, being gated, again in
     the gate-list pass (fb_list4_kernel / fb_list12_kernel); both passes' flags reach
-    the exact fallback (folded into the consumers, or two fb_exact_kernel launches)."""
+    the exact fallback (folded into the consumers -- fb_list4_kernel's from its per-wave
+    queue; at N = 5000 waves hold two items, 8 queued pairs -- or fb_exact_kernel
+    launches)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    N, K = 41, 2
+    K = 2
     cs, consts = adversarial_case(1, S=S, Sb=S, d=3, N=N, K=K, T=10)
     consts["c"][1:] = 1.0e4
     base, T = cs["base"], cs["T"]
