@@ -371,15 +371,38 @@ def main():
         if not (rccl is not None and hs_dev is not None):
             hs.copy_(st, non_blocking=True)
 
+    # one rank: the E-step's last kernel stores a ticket into a coherent pinned word
+    # once the statistics are in host memory (vbhem_arm_done_word), and the host polls
+    # it -- no event after each step: an event is a queue marker that idles the GPU
+    # ~5.7 us per E-step (12,500-base trace, gpurun_out/prof_r06l_shard).  With a
+    # collective the statistics are final only after it: an event there.
+    word = (eng.done_word() if world == 1 and rccl is None and not os.environ.get("VBHEM_BENCH_COPY")
+            and not os.environ.get("VBHEM_BENCH_EVENT") else None)
+    tickets = [0, 0]
+    seq = [0]
+
     def launch(k):
-        """Enqueue E-step k: statistics into pinned host buffer k % 2, then an event."""
+        """Enqueue E-step k: statistics into pinned host buffer k % 2, then its ticket
+        (or an event)."""
         hs = hbufs[k % 2]
         if world == 1 and rccl is None and not os.environ.get("VBHEM_BENCH_COPY"):
+            if word is not None:
+                seq[0] += 1
+                tickets[k % 2] = seq[0]
+                eng.fused(tN, out=hs, done=(word, seq[0]))
+                return hs
             eng.fused(tN, out=hs)
         else:
             collective(eng.fused(tN), k, hs)
         done[k % 2].record(stream)
         return hs
+
+    def wait(k):
+        """The host waits for E-step k's statistics."""
+        if word is not None:
+            word.wait(tickets[k % 2])
+        else:
+            done[k % 2].synchronize()
 
     def step():
         """One E-step, the host waiting for its statistics before anything else."""
@@ -398,7 +421,7 @@ def main():
         while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
             launch(n)
             if n > 0:
-                done[(n - 1) % 2].synchronize()
+                wait(n - 1)
             n += 1
         torch.cuda.synchronize()
         settle = {"ms": (time.perf_counter() - ts) * 1e3, "steps": n}
@@ -427,7 +450,7 @@ def main():
         if s % time_every == 0:
             _capi.timing_enable(False)
         if s > 0:
-            done[(s - 1) % 2].synchronize()
+            wait(s - 1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     stats = stats.clone()
@@ -610,25 +633,37 @@ def main():
         for _ in range(3):
             eng_s.fused(tN_s, out=hs[0])
             stream.synchronize()
+        # the timed region's pacing: one step of run-ahead, the host waiting for each
+        # step's statistics by the completion word (or an event, as above)
+        word_s = eng_s.done_word() if word is not None else None
+        seq_s = [0]
+
+        def run_ahead(n=None, ms=None):
+            t0 = time.perf_counter()
+            k = 0
+            tick = [0, 0]
+            while (k < n) if n is not None else ((time.perf_counter() - t0) * 1e3 < ms):
+                if word_s is not None:
+                    seq_s[0] += 1
+                    tick[k % 2] = seq_s[0]
+                    eng_s.fused(tN_s, out=hs[k % 2], done=(word_s, seq_s[0]))
+                else:
+                    eng_s.fused(tN_s, out=hs[k % 2])
+                    ev_s[k % 2].record(stream)
+                if k > 0:
+                    if word_s is not None:
+                        word_s.wait(tick[(k - 1) % 2])
+                    else:
+                        ev_s[(k - 1) % 2].synchronize()
+                k += 1
+            stream.synchronize()
+            return time.perf_counter() - t0
+
         # the clocks settle again (the host-side math above left the GPU idle)
-        ts0 = time.perf_counter()
-        k = 0
-        while (time.perf_counter() - ts0) * 1e3 < args.settle_ms:
-            eng_s.fused(tN_s, out=hs[k % 2])
-            ev_s[k % 2].record(stream)
-            if k > 0:
-                ev_s[(k - 1) % 2].synchronize()
-            k += 1
-        stream.synchronize()
+        if args.settle_ms > 0:
+            run_ahead(ms=args.settle_ms)
         nss = max(20, args.steps)
-        ts0 = time.perf_counter()
-        for k in range(nss):  # one step of run-ahead, as the timed region above
-            eng_s.fused(tN_s, out=hs[k % 2])
-            ev_s[k % 2].record(stream)
-            if k > 0:
-                ev_s[(k - 1) % 2].synchronize()
-        stream.synchronize()
-        es_ms = (time.perf_counter() - ts0) / nss * 1e3
+        es_ms = run_ahead(n=nss) / nss * 1e3
         ts0 = time.perf_counter()
         for _ in range(nss):
             eng_s.fused(tN_s, out=hs[0])
@@ -724,7 +759,9 @@ def main():
                                   for r in range(world)],
             ms_per_step_per_rank=[s / args.steps * 1e3 for s in per_rank_s]),
         "pacing": ("one E-step of run-ahead (the C++ EM loop's): step k+1 is enqueued before "
-                   "the host waits for step k's statistics in pinned memory"),
+                   "the host waits for step k's statistics in pinned memory"
+                   + (" -- by polling the completion word the step's last kernel writes "
+                      "(vbhem_arm_done_word)" if word is not None else " -- by an event")),
         "synchronous": {"value": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
                         "note": "the host waits for each step's statistics before launching "
                                 "the next (no overlap of the host hand-over)"},

@@ -87,6 +87,9 @@ EXPORTS = {
                                           _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "vbhem_last_fallback_count": (_c_int, [_vp, _vp]),
     "vbhem_host_device_pointer": (_c_int, [_vp, ctypes.POINTER(_vp)]),
+    "vbhem_arm_done_word": (_c_int, [_vp, ctypes.c_ulonglong]),
+    "vbhem_done_word_alloc": (_c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
+    "vbhem_done_word_free": (_c_int, [_vp]),
     "vbhem_ctx_create": (_c_int, [_c_int, ctypes.POINTER(BaseT), _c_int, _c_int, _c_int, _c_int,
                                   ctypes.POINTER(_vp)]),
     "vbhem_ctx_fused": (_c_int, [_vp, ctypes.POINTER(ClusterT), _vp, _vp, _vp, _vp, _vp]),

@@ -901,10 +901,47 @@ int vbhem_estep_fused(const vbhem_base_t *base, const vbhem_cluster_t *clus, int
                                   LL_elbo_dev, workspace_dev, workspace_bytes, stream);
 }
 
+// vbhem_arm_done_word: the completion word of the next fused call (taken by that call)
+static std::atomic<unsigned long long *> g_done_word{nullptr};
+static std::atomic<unsigned long long> g_done_val{0};
+
+int vbhem_arm_done_word(void *word, unsigned long long value) {
+  if (word && reinterpret_cast<uintptr_t>(word) % 8 != 0) return fail(VBHEM_ERR_ARG, "done word not 8-byte aligned");
+  g_done_val.store(value);
+  g_done_word.store(static_cast<unsigned long long *>(word));
+  return VBHEM_OK;
+}
+
+int vbhem_done_word_alloc(void **host_ptr, void **dev_ptr) {
+  if (!host_ptr || !dev_ptr) return fail(VBHEM_ERR_ARG, "null pointer");
+  void *h = nullptr;
+  hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(done word)");
+  std::memset(h, 0, 64);
+  void *d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return hip_fail(e, "hipHostGetDevicePointer(done word)");
+  }
+  *host_ptr = h;
+  *dev_ptr = d;
+  return VBHEM_OK;
+}
+
+int vbhem_done_word_free(void *host_ptr) {
+  if (!host_ptr) return VBHEM_OK;
+  const hipError_t e = hipHostFree(host_ptr);
+  return e == hipSuccess ? VBHEM_OK : hip_fail(e, "hipHostFree(done word)");
+}
+
 int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *clus, int R, int T,
                              const double *tildeN_dev, const double *logOmega_dev,
                              double *stats_dev, double *hatZ_dev, double *LL_elbo_dev,
                              void *workspace_dev, size_t workspace_bytes, void *stream) {
+  // (taken first: a call that fails leaves nothing armed for the next one)
+  unsigned long long *const done_word = g_done_word.exchange(nullptr);
+  const unsigned long long done_val = g_done_val.load();
   int rc = check_inputs(base, clus, T);
   if (rc != VBHEM_OK) return rc;
   if (R < 1 || clus->K % R != 0)
@@ -1055,7 +1092,7 @@ int vbhem_estep_fused_trials(const vbhem_base_t *base, const vbhem_cluster_t *cl
     if (ev0) g_timing.stats.emplace_back(ev0, timing_event(st));
   }
   e = vbhem::launch_stats_final(w.slabs, nslab_used, stats_slabs, w.slab_len, sa.KT, S, sa.SL,
-                                stats_dev, st, w.fpre);
+                                stats_dev, st, w.fpre, done_word, done_val);
   if (e != hipSuccess) return hip_fail(e, "stats_final_kernel");
   guard.fpre = nullptr;
   return VBHEM_OK;

@@ -461,7 +461,10 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
 // section of SL doubles)
 // fpre (optional): the flag head (flags - kFlagPre) to close: last total, counters
 // zeroed, tag written (kFlagPre)
+// done (optional, needs fpre): after every block's statistics are stored at system
+// scope, the last block to finish stores done_val there (vbhem_arm_done_word)
 hipError_t launch_stats_final(const double *slabs, int nslab, int nslab_stats, int slab_len, int KT,
-                              int S, int SL, double *out, hipStream_t st, int *fpre = nullptr);
+                              int S, int SL, double *out, hipStream_t st, int *fpre = nullptr,
+                              unsigned long long *done = nullptr, unsigned long long done_val = 0);
 
 }  // namespace vbhem

@@ -865,14 +865,19 @@ constexpr int kFinalCols = 16, kFinalParts = 16;
 __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, int nslab_all,
                                                           int nslab_stats, int slab_len, int KT,
                                                           int S, int SL, double *out, int *fpre,
-                                                          unsigned long long tag) {
+                                                          unsigned long long tag,
+                                                          unsigned long long *done,
+                                                          unsigned long long done_val) {
   __shared__ double part[kFinalParts][kFinalCols];
   // the call's last kernel closes the flag head (kFlagPre): the total kept, the counters
-  // zeroed, the tag written -- the next call's in-kernel preparation finds them clean
+  // zeroed, the tag written -- the next call's in-kernel preparation finds them clean.
+  // With a completion word, counter [2] (fb_exact_kernel's blocks-done, zero between
+  // passes) counts this kernel's finished blocks instead: the last one resets it
   if (fpre && blockIdx.x == 0 && threadIdx.x == 0) {
     int *fc = fpre + kFlagPre;
     fpre[2] = fc[1];
-    for (int c = 0; c < kFlagHead; ++c) fc[c] = 0;
+    for (int c = 0; c < kFlagHead; ++c)
+      if (!(done && c == 2)) fc[c] = 0;
     *reinterpret_cast<unsigned long long *>(fpre) = tag;
   }
   const int c = threadIdx.x % kFinalCols, pp = threadIdx.x / kFinalCols;
@@ -905,7 +910,26 @@ __global__ __launch_bounds__(256) void stats_final_kernel(const double *slabs, i
     if (fpre && __hip_atomic_load(fpre + kFlagLost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                     kFlagLostMark)
       s = __builtin_nan("");
-    out[x] = s;
+    if (done)  // written through to the system (the host polls the word, not an event)
+      __hip_atomic_store(reinterpret_cast<unsigned long long *>(out + x), __double_as_longlong(s),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      out[x] = s;
+  }
+  if (done && fpre) {
+    // every store of this block acknowledged (written through at system scope: what a
+    // system-scope release would wait for, without its L2 write-back), then one count
+    // per block; the last block to count publishes the word after all of them
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int *cnt = fpre + kFlagPre + 2;
+      const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (int)gridDim.x - 1) {
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(done, done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -1770,11 +1794,12 @@ hipError_t launch_stats_list(const StatsArgs &a, int nchunk, size_t lds, hipStre
 }
 
 hipError_t launch_stats_final(const double *slabs, int nslab, int nslab_stats, int slab_len, int KT,
-                              int S, int SL, double *out, hipStream_t st, int *fpre) {
+                              int S, int SL, double *out, hipStream_t st, int *fpre,
+                              unsigned long long *done, unsigned long long done_val) {
   if (nslab_stats < 1 || nslab_stats > nslab || SL < 1 || slab_len % SL != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(stats_final_kernel, dim3((slab_len + kFinalCols - 1) / kFinalCols), dim3(256),
                      0, st, slabs, nslab, nslab_stats, slab_len, KT, S, SL, out, fpre,
-                     fpre ? flag_tag() : 0ull);
+                     fpre ? flag_tag() : 0ull, fpre ? done : nullptr, done_val);
   return hipGetLastError();
 }
 

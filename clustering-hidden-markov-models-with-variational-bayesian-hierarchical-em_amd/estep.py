@@ -163,7 +163,11 @@ class EStepEngine:
         # pinned host memory: the kernel writes it through its device address
         return self._device_address(out)
 
-    def fused(self, tildeN: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    def done_word(self) -> "DoneWord":
+        """A completion word for ``fused(done=(word, value))`` (coherent pinned host memory)."""
+        return DoneWord(self.lib)
+
+    def fused(self, tildeN: torch.Tensor, out: torch.Tensor = None, done=None) -> torch.Tensor:
         """Pairs + responsibilities + gated Z-weighted sums + ELBO partials.
 
         tildeN: [N] (device, fp64) virtual-sample counts of this shard.
@@ -171,7 +175,10 @@ class EStepEngine:
         device, or ``out`` when given -- a device vector, or a pinned host vector
         (``host_stats_buffer``) that the statistics kernel writes directly (no
         copy after the E-step; read it after synchronising the stream).  hat_Z and
-        L_elbo are left in ``self.hatZ`` / ``self.LL``."""
+        L_elbo are left in ``self.hatZ`` / ``self.LL``.  ``done=(word, value)``: the
+        call's last kernel stores ``value`` into ``word`` (a DoneWord) once the
+        statistics are written and visible to the host (vbhem_arm_done_word), so a host
+        running ahead can wait with ``word.wait(value)`` instead of an event."""
         if self._ws_fused is None:
             nb = int(self.lib.vbhem_fused_trials_workspace_bytes(
                 ctypes.byref(self._bt), ctypes.byref(self._ct), self.trials, self.T))
@@ -194,6 +201,10 @@ class EStepEngine:
                 self._fused_args.clear()
             self._fused_args[key] = (fn, name, args)
         fn, name, args = self._fused_args[key]
+        if done is not None:
+            word, value = done
+            _capi.check(self.lib.vbhem_arm_done_word(ctypes.c_void_p(word.dev), int(value)),
+                        "vbhem_arm_done_word")
         _capi.check(fn(*args), name)
         return res
 
@@ -206,3 +217,39 @@ class EStepEngine:
         if n < 0:
             _capi.check(n, "vbhem_last_fallback_count")
         return int(n)
+
+
+class DoneWord:
+    """A 64-bit completion word in coherent pinned host memory (vbhem_done_word_alloc):
+    ``EStepEngine.fused(done=(word, v))`` has the E-step's last kernel store v into it
+    once the statistics are visible to the host; ``wait(v)`` spins until it reads >= v."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _capi.check(lib.vbhem_done_word_alloc(ctypes.byref(h), ctypes.byref(d)), "vbhem_done_word_alloc")
+        self.host, self.dev = int(h.value), int(d.value)
+        self._word = ctypes.c_uint64.from_address(self.host)
+
+    @property
+    def value(self) -> int:
+        return int(self._word.value)
+
+    def wait(self, value: int, timeout_s: float = 60.0) -> None:
+        """Spin until the word reads >= value (ctypes re-reads the memory every time)."""
+        import time
+        w = self._word
+        if w.value >= value:
+            return
+        t0 = time.perf_counter()
+        while w.value < value:
+            if time.perf_counter() - t0 > timeout_s:
+                raise TimeoutError(f"done word {w.value} < {value} after {timeout_s} s")
+
+    def __del__(self):
+        try:
+            if self.host:
+                self.lib.vbhem_done_word_free(ctypes.c_void_p(self.host))
+                self.host = 0
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass

@@ -242,6 +242,22 @@ int vbhem_last_fallback_count(void *stream, const void *workspace_dev);
  * stream.  VBHEM_ERR_ARG if host_ptr is not registered pinned memory. */
 int vbhem_host_device_pointer(void *host_ptr, void **dev_ptr);
 
+/* Completion word for the NEXT vbhem_estep_fused call of this process (one-shot; no
+ * reference counterpart -- the MEX returns synchronously): once that call's
+ * statistics are written and visible to the host, its last kernel stores `value`
+ * into the 64-bit word at `word` (a device address, e.g. vbhem_host_device_pointer of
+ * a pinned host word), after the statistics, at system scope.  A host that runs
+ * E-steps ahead of itself can poll the word instead of recording an event after each
+ * call (an event is a queue marker: ~5.7 us of idle GPU per E-step on MI355X).
+ * word = NULL disarms.  The statistics must themselves be host memory or be read
+ * after a stream synchronisation. */
+int vbhem_arm_done_word(void *word, unsigned long long value);
+/* A zeroed 64-bit completion word in coherent (fine-grained) pinned host memory:
+ * *host_ptr for the host's reads, *dev_ptr for vbhem_arm_done_word.  Free with
+ * vbhem_done_word_free(host_ptr). */
+int vbhem_done_word_alloc(void **host_ptr, void **dev_ptr);
+int vbhem_done_word_free(void *host_ptr);
+
 /* Kernel timing for benchmarking/profiling, per host thread: while enabled,
  * hipEvents are recorded on the launch stream around the kernel launches of this
  * thread (never into a stream that is capturing a graph: such launches are simply
