@@ -414,15 +414,30 @@ def main():
     # sustained work (C4, same box: 1.84 ms per timed step after 5 warmup steps,
     # 1.795 ms after 300 -- gpurun_out/r06j); the untimed steps below run the timed
     # region's own protocol for --settle-ms, then the W warmup steps follow as before
+    # (several ranks: every E-step has a collective, so all ranks run the same step
+    # count -- from one timed step, the largest over the ranks -- not a time limit)
     settle = {"ms": 0.0, "steps": 0}
     if args.settle_ms > 0:
         ts = time.perf_counter()
         n = 0
-        while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
-            launch(n)
-            if n > 0:
-                wait(n - 1)
-            n += 1
+        if world > 1:
+            t1s = time.perf_counter()
+            step()
+            nset = torch.tensor([min(20000, int(args.settle_ms / max(1e-3, (time.perf_counter() - t1s) * 1e3)) + 1)],
+                                dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(nset, op=dist.ReduceOp.MAX)
+            nset = int(nset.item())
+            for n in range(nset):
+                launch(n)
+                if n > 0:
+                    wait(n - 1)
+            n = nset + 1
+        else:
+            while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+                launch(n)
+                if n > 0:
+                    wait(n - 1)
+                n += 1
         torch.cuda.synchronize()
         settle = {"ms": (time.perf_counter() - ts) * 1e3, "steps": n}
     for _ in range(args.warmup):
