@@ -421,6 +421,7 @@ def main():
         ts = time.perf_counter()
         n = 0
         if world > 1:
+            step()  # (the first one pays the communicator's lazy setup)
             t1s = time.perf_counter()
             step()
             nset = torch.tensor([min(20000, int(args.settle_ms / max(1e-3, (time.perf_counter() - t1s) * 1e3)) + 1)],
