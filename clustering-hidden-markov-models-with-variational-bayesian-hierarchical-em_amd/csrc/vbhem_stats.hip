@@ -436,12 +436,22 @@ __global__ __launch_bounds__(kListThreads) void gate_list_kernel(const StatsArgs
     const int KC = min(K - j0, kListThreads), R = kListThreads / KC;
     const int r = tid / KC, j = j0 + (tid - r * KC);
     if (r < R) {
+      // 32 chunks' counts in flight per thread (clamped addresses, then masked sums): one
+      // memory round trip for up to 32 R chunks instead of one per 8
       int sb = 0, stt = 0;
-#pragma unroll 8
-      for (int c = r; c < nchunk; c += R) {
-        const int v = p.gate_cnt[(size_t)c * K + j];
-        stt += v;
-        sb += c < me ? v : 0;
+      for (int c0 = r; c0 < nchunk; c0 += 32 * R) {
+        int v[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int c = min(c0 + q * R, nchunk - 1);
+          v[q] = p.gate_cnt[(size_t)c * K + j];
+        }
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int c = c0 + q * R;
+          stt += c < nchunk ? v[q] : 0;
+          sb += c < me ? v[q] : 0;
+        }
       }
       pb[tid] = sb;
       pt[tid] = stt;
